@@ -1,0 +1,107 @@
+"""ctypes binding of the CPU oracle (oracle/polar_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker / timed CPU baseline. The product package
+(sc_polar_decoder_hls_amd) never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+# FSM state indices of orc_decode_fsm's state_counts (polar_oracle.c)
+STATES = ("INIT", "F", "R", "G", "H", "H0", "F_REP", "G_R1", "G_SPC", "END")
+
+NODE_R0, NODE_R1, NODE_REP, NODE_SPC, NODE_RN = 0x00, 0x0F, 0x02, 0x04, 0x08
+
+
+def build(force=False):
+    """Compile the oracle with its Makefile (gcc); returns the .so path."""
+    src = os.path.join(_HERE, "polar_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u32, i32, p = ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
+        for name, args in (("orc_qconv_format", (i32, u32)), ("orc_F_sm", (i32, u32, u32)),
+                           ("orc_G_sm", (i32, u32, u32, u32)), ("orc_Gext_sm", (i32, u32, u32, u32)),
+                           ("orc_full_adder_sm", (i32, u32, u32)), ("orc_full_adder_sat_sm", (i32, u32, u32)),
+                           ("orc_leaf16", (p, u32)), ("orc_rep_add_tree16", (p, u32)),
+                           ("orc_min_mask16", (p,)), ("orc_classify_group", (u32,))):
+            f = getattr(L, name)
+            f.argtypes = list(args)
+            f.restype = u32 if name != "orc_classify_group" else i32
+        L.orc_decode_fsm.argtypes = [i32, p, p, p, i32, p]
+        L.orc_decode_fsm.restype = i32
+        L.orc_decode_rec.argtypes = [i32, p, p, p, i32]
+        L.orc_decode_rec.restype = i32
+        L.orc_encode.argtypes = [i32, p, p, i32]
+        L.orc_encode.restype = None
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def decode_fsm(mask, llr, return_counts=False):
+    """Literal FSM decode. mask: (N,) 0/1; llr: (B, N) int8. Returns xhat (B, N) uint8."""
+    mask = np.ascontiguousarray(mask, dtype=np.uint8)
+    llr = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
+    B, N = llr.shape
+    out = np.zeros((B, N), dtype=np.uint8)
+    counts = np.zeros(len(STATES), dtype=np.int64)
+    rc = lib().orc_decode_fsm(N, _ptr(mask), _ptr(llr), _ptr(out), B, _ptr(counts))
+    if rc != 0:
+        raise RuntimeError("orc_decode_fsm failed: %d" % rc)
+    if return_counts:
+        return out, dict(zip(STATES, counts.tolist()))
+    return out
+
+
+def decode_rec(mask, llr):
+    """Recursive-restatement decode (same I/O as decode_fsm)."""
+    mask = np.ascontiguousarray(mask, dtype=np.uint8)
+    llr = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
+    B, N = llr.shape
+    out = np.zeros((B, N), dtype=np.uint8)
+    rc = lib().orc_decode_rec(N, _ptr(mask), _ptr(llr), _ptr(out), B)
+    if rc != 0:
+        raise RuntimeError("orc_decode_rec failed: %d" % rc)
+    return out
+
+
+def encode(u):
+    """x = u F^{(x)n}, natural order. u: (B, N) 0/1."""
+    u = np.ascontiguousarray(np.atleast_2d(u), dtype=np.uint8)
+    B, N = u.shape
+    x = np.zeros_like(u)
+    lib().orc_encode(N, _ptr(u), _ptr(x), B)
+    return x
+
+
+def leaf16(llr_sm, fb):
+    a = np.ascontiguousarray(llr_sm, dtype=np.uint32)
+    return lib().orc_leaf16(_ptr(a), fb)
+
+
+def rep_add_tree16(llr_sm, old):
+    a = np.ascontiguousarray(llr_sm, dtype=np.uint32)
+    return lib().orc_rep_add_tree16(_ptr(a), old)
+
+
+def min_mask16(llr_sm):
+    a = np.ascontiguousarray(llr_sm, dtype=np.uint32)
+    return lib().orc_min_mask16(_ptr(a))

@@ -1,0 +1,730 @@
+/*
+ * polar_oracle.c -- CPU ORACLE for the SC polar decoder hot path.
+ *
+ *   *** TEST INFRASTRUCTURE ONLY. ***
+ *   Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ *   library, and only as the checker (or the timed CPU baseline). The product path
+ *   (sc_polar_decoder_hls_amd / libpolar_sc.so) never links, loads or calls it.
+ *
+ * What it is: a plain-C restatement of the reference decoder of
+ * ydelomier/SC_Polar_decoder_HLS (SystemC / Vivado-HLS, config of src/module/config.h:
+ * LLR_BITS=6, SIGMAG, EXTENDED=1, PRUNING_LEVEL=2, ELAG_R1=ELAG_REP=ELAG_SPC=1,
+ * ELAG_REP2=ELAG_SPC2=ELAG_RARE=0, ELAG_H0=1, PAR=16).
+ *
+ * Two independent restatements live here:
+ *   1. orc_decode_fsm  -- a LITERAL cycle-free simulation of my_module::do_prunning and
+ *      my_module::do_action (src/module/my_module.h:61-166, 174-1877): the same memories
+ *      (llr_mem_a/b, bit_mem_1/2, Bit_Frozen, Node_Type), the same pointer registers with
+ *      COUNTER (= sc_uint<log2N+1>) wrap-around, the same 2-bit and 8-bit shift-register
+ *      stacks (shared/src/functions.h:11-37) and the same FSM transitions. Every
+ *      arithmetic primitive is a bit-width-exact restatement of the SystemC function it
+ *      names (Q-bit patterns, masks instead of sc_bigint widths).
+ *   2. orc_decode_rec  -- the recursive (Appendix A of SURVEY.md) formulation the GPU
+ *      schedule compiler is derived from. Tests require 1 == 2 on random masks and data.
+ *
+ * Pinning status: the reference cannot be built here (it needs systemc.h / libsystemc
+ * and Vivado HLS, neither present; building it against stand-in headers is not allowed),
+ * and it ships no recorded decoder outputs. The only known-answer vectors it holds are
+ * the 9 hard-coded codewords of src/testbench/sc_encoder/sc_encoder.h:74-88; those pin
+ * the encoding / frozen-bit conventions and noiseless decoding (tests/golden/kat_*.json).
+ * The fixed-point corner cases (signed zero, G saturation at 15, REP 511 clamp, SPC tie
+ * rule) are PARITY UNPINNED by reference outputs: they follow the literal text of the
+ * cited SystemC source, cross-checked by the two restatements above and by the
+ * bit-level primitive tests in tests/test_oracle_primitives.py.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define PAR 16
+#define LLR_BITS 6
+
+/* node codes: shared/src/library.h:34-40 */
+#define NODE_R0   0x00
+#define NODE_R1   0x0F
+#define NODE_REP  0x02
+#define NODE_SPC  0x04
+#define NODE_REP2 0x03
+#define NODE_SPC2 0x05
+#define NODE_RN   0x08
+
+static inline uint32_t msk(int q) { return (q >= 32) ? 0xFFFFFFFFu : ((1u << q) - 1u); }
+
+/* ------------------------------------------------------------------------------------ */
+/* Scalar primitives (shared/src/scalar.h)                                               */
+/* ------------------------------------------------------------------------------------ */
+
+/* qconv_format<Q> (scalar.h:229-239): CA2 -> SIGMAG (Q-bit patterns). */
+uint32_t orc_qconv_format(int Q, uint32_t a)
+{
+    a &= msk(Q);
+    uint32_t abs_ = a & msk(Q - 1);
+    uint32_t inv = (~abs_) & msk(Q);
+    uint32_t add = (inv + 1u) & msk(Q);
+    uint32_t sig = (a >> (Q - 1)) & 1u;
+    return sig ? add : a;
+}
+
+/* qsat_sm<Q>(sc_biguint<Q+1> a) (scalar.h:94-99): bound is (0,(sc_uint<Q-1>)0xFFFFFF) =
+ * 2^(Q-1)-1; returns a Q-bit pattern. */
+static uint32_t qsat_sm(int Q, uint32_t a)
+{
+    uint32_t bound = msk(Q - 1);
+    if (a > bound) return bound;
+    return a & msk(Q);
+}
+
+/* qfull_add_sub_sm<Q>(a, b, s) (scalar.h:196-225): Q-bit SM in, (Q+1)-bit SM out.
+ * s = 1 flips the sign of a. */
+static uint32_t qfull_add_sub_sm(int Q, uint32_t a, uint32_t b, uint32_t s)
+{
+    uint32_t sla = (a >> (Q - 1)) & 1u;
+    uint32_t siga = sla ^ (s & 1u);
+    uint32_t sigb = (b >> (Q - 1)) & 1u;
+    uint32_t xsig = siga ^ sigb;
+    uint32_t absla = a & msk(Q - 1);          /* range(Q-2,0), zero-extended to Q bits */
+    uint32_t invla = (~absla) & msk(Q);
+    uint32_t abslb = b & msk(Q - 1);
+    uint32_t invlb = (~abslb) & msk(Q);
+    uint32_t is_min = (absla < abslb) ? 1u : 0u;
+    uint32_t sel_a = xsig & is_min;
+    uint32_t sel_b = xsig & (is_min ^ 1u);
+    uint32_t absA = sel_a ? invla : absla;
+    uint32_t absB = sel_b ? invlb : abslb;
+    uint32_t somme = (absA + absB + xsig) & msk(Q);
+    uint32_t sig_somme = is_min ? sigb : siga;
+    return (sig_somme << Q) | somme;
+}
+
+/* qfull_adder_sm<Q>(a, b) (scalar.h:135-162): identical datapath without the sign flip. */
+uint32_t orc_full_adder_sm(int Q, uint32_t a, uint32_t b)
+{
+    return qfull_add_sub_sm(Q, a, b, 0u);
+}
+
+/* qfull_adder_sat_sm<Q>(a, b) (scalar.h:164-194): Q-bit in, Q-bit out, magnitude through
+ * qsat_sm<Q-1> (clamp 2^(Q-2)-1). */
+uint32_t orc_full_adder_sat_sm(int Q, uint32_t a, uint32_t b)
+{
+    uint32_t r = qfull_add_sub_sm(Q, a, b, 0u);
+    uint32_t somme = r & msk(Q);
+    uint32_t sig = (r >> Q) & 1u;
+    uint32_t sat = qsat_sm(Q - 1, somme);
+    return (sig << (Q - 1)) | sat;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Polar operators (shared/src/functions.h:124-281), one lane                             */
+/* ------------------------------------------------------------------------------------ */
+
+/* F_function_SM<P,Q> (functions.h:124-145): sign = xor, magnitude = min, no saturation. */
+uint32_t orc_F_sm(int Q, uint32_t la, uint32_t lb)
+{
+    uint32_t ma = la & msk(Q - 1), mb = lb & msk(Q - 1);
+    uint32_t m = (ma < mb) ? ma : mb;        /* qmin_sm: (a < b) ? a : b */
+    uint32_t s = ((la ^ lb) >> (Q - 1)) & 1u;
+    return (s << (Q - 1)) | m;
+}
+
+/* G_function_SM<P,Q> (functions.h:147-195): qfull_add_sub_sm, then VECTOR_SAT_SM<P,Q-1>
+ * on the Q-bit magnitude (clamp 2^(Q-2)-1 = 15 for Q = 6), concat sign. */
+uint32_t orc_G_sm(int Q, uint32_t la, uint32_t lb, uint32_t sa)
+{
+    uint32_t somme = qfull_add_sub_sm(Q, la, lb, sa);
+    uint32_t abs_ = somme & msk(Q);
+    uint32_t sign = (somme >> Q) & 1u;
+    uint32_t sat = qsat_sm(Q - 1, abs_) & msk(Q - 1);
+    return (sign << (Q - 1)) | sat;
+}
+
+/* G_extended_SM<P,Q> (functions.h:197-239): Q-bit in, (Q+1)-bit out, exact. */
+uint32_t orc_Gext_sm(int Q, uint32_t la, uint32_t lb, uint32_t sa)
+{
+    return qfull_add_sub_sm(Q, la, lb, sa);
+}
+
+/* F_simplified_SM (functions.h:241-256) for P=1 */
+static uint32_t F_simp(int Q, uint32_t la, uint32_t lb, uint32_t fb)
+{
+    return (((la ^ lb) >> (Q - 1)) & 1u) & fb;
+}
+
+/* G_simplified_SM (functions.h:258-281) for P=1 */
+static uint32_t G_simp(int Q, uint32_t la, uint32_t lb, uint32_t sa, uint32_t fb)
+{
+    uint32_t sla = (la >> (Q - 1)) & 1u;
+    uint32_t sigla = sla ^ sa;
+    uint32_t siglb = (lb >> (Q - 1)) & 1u;
+    uint32_t siga = sigla & fb, sigb = siglb & fb;
+    uint32_t absla = la & msk(Q - 1), abslb = lb & msk(Q - 1);
+    uint32_t is_min = (absla < abslb) ? 1u : 0u;
+    return is_min ? sigb : siga;
+}
+
+/* Spec_P2<Q> (functions.h:366-384) */
+static uint32_t spec_p2(int Q, const uint32_t *llr, uint32_t fb)
+{
+    uint32_t la = llr[0], lb = llr[1];
+    uint32_t sa1 = F_simp(Q, la, lb, fb & 1u);
+    uint32_t sb1 = G_simp(Q, la, lb, sa1, (fb >> 1) & 1u);
+    return (sb1 << 1) | (sa1 ^ sb1);
+}
+
+/* Spec_P{4,8,16}_ext<Q> (functions.h:413-438, 467-492, 521-546): exact leaf with
+ * widths growing by one bit per G_extended. Returns the n encoded bits x (lane 0 = bit 0). */
+static uint32_t spec_pn_ext(int n, int Q, const uint32_t *llr, uint32_t fb)
+{
+    if (n == 2) return spec_p2(Q, llr, fb);
+    int h = n / 2;
+    uint32_t la1[8] = {0}, lb1[8] = {0};
+    for (int j = 0; j < h; j++) la1[j] = orc_F_sm(Q, llr[j], llr[h + j]);
+    uint32_t sa1 = spec_pn_ext(h, Q, la1, fb & msk(h));
+    for (int j = 0; j < h; j++) lb1[j] = orc_Gext_sm(Q, llr[j], llr[h + j], (sa1 >> j) & 1u);
+    uint32_t sb1 = spec_pn_ext(h, Q + 1, lb1, (fb >> h) & msk(h));
+    return (sb1 << h) | ((sa1 ^ sb1) & msk(h));
+}
+
+/* Spec_Polar_Decoder<16,6> -> Spec_PolarDec_16 -> Spec_P16_ext<6> (library.h:149-172,
+ * functions.h:808-818). llr: 16 six-bit SM patterns; fb bit k = frozen-table bit of lane k
+ * (1 = information). */
+uint32_t orc_leaf16(const uint32_t *llr, uint32_t fb)
+{
+    return spec_pn_ext(16, LLR_BITS, llr, fb & 0xFFFFu);
+}
+
+/* ADD_TREE_16_SM<6> + ADDER_TREE_16<6> (functions.h:3036-3083, 3190-3205).
+ * llr: 16 six-bit SM. old_sum / return: 11-bit SM (sign bit 10). */
+uint32_t orc_rep_add_tree16(const uint32_t *llr, uint32_t old_sum)
+{
+    uint32_t v[16];
+    int n = 16, Q = LLR_BITS;
+    for (int i = 0; i < 16; i++) v[i] = llr[i] & msk(Q);
+    while (n > 1) {  /* ADD_TREE_{n}_SM<Q>: lanes j and j+n/2, a = lower lane */
+        int h = n / 2;
+        for (int j = 0; j < h; j++) v[j] = orc_full_adder_sm(Q, v[j], v[j + h]);
+        n = h;
+        Q += 1;
+    }
+    /* add_tree is (Q+4)=10 bits: sign bit 9, magnitude bits 8..0; extend to 11 bits */
+    uint32_t add_tree = v[0] & msk(10);
+    uint32_t ext = (((add_tree >> 9) & 1u) << 10) | (add_tree & msk(9));
+    return orc_full_adder_sat_sm(11, ext, old_sum & msk(11));
+}
+
+/* Min_Mask_16_SM<5> via Min_Mask_TREE_16<6> (functions.h:3652-3747, 3900-3913).
+ * Returns (min << 16) | one-hot mask. */
+static void min_mask_rec(int n, const uint32_t *mag, uint32_t *min_out, uint32_t *mask_out)
+{
+    if (n == 2) {   /* Min_Mask_2_SM: is_min = mb < ma ; mask = (is_min, ~is_min) */
+        uint32_t is_min = (mag[1] < mag[0]) ? 1u : 0u;
+        *min_out = is_min ? mag[1] : mag[0];
+        *mask_out = (is_min << 1) | (is_min ^ 1u);
+        return;
+    }
+    int h = n / 2;
+    uint32_t is_min = 0, m[8];
+    for (int j = 0; j < h; j++) {
+        uint32_t im = (mag[h + j] < mag[j]) ? 1u : 0u;
+        is_min |= im << j;
+        m[j] = im ? mag[h + j] : mag[j];
+    }
+    uint32_t mask_a = (is_min << h) | ((~is_min) & msk(h));
+    uint32_t rmin, imask;
+    min_mask_rec(h, m, &rmin, &imask);
+    uint32_t mask_b = (imask << h) | imask;
+    *min_out = rmin;
+    *mask_out = mask_a & mask_b;
+}
+
+uint32_t orc_min_mask16(const uint32_t *llr)
+{
+    uint32_t mag[16];
+    for (int i = 0; i < 16; i++) mag[i] = llr[i] & msk(LLR_BITS - 1);
+    uint32_t mn, mask;
+    min_mask_rec(16, mag, &mn, &mask);
+    return (mn << 16) | (mask & 0xFFFFu);
+}
+
+/* do_prunning group classification (my_module.h:75-155), priority R0 > R1 > REP > SPC
+ * (REP2/SPC2 disabled). fb bit k = frozen-table bit 16g+k. */
+int orc_classify_group(uint32_t fb)
+{
+    fb &= 0xFFFFu;
+    if (fb == 0) return NODE_R0;
+    if (fb == 0xFFFFu) return NODE_R1;
+    if (fb == 0x8000u) return NODE_REP;            /* last bit 1, others 0 */
+    if (fb == 0xFFFEu) return NODE_SPC;            /* first bit 0, others 1 */
+    return NODE_RN;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Stacks (functions.h:11-37): D entries of Q bits, entry 1 = top = lowest bits.           */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { int D; uint32_t e[64]; } stk_t;   /* e[0] = top */
+
+static void stk_push(stk_t *s, uint32_t v) { for (int i = s->D - 1; i > 0; i--) s->e[i] = s->e[i - 1]; s->e[0] = v; }
+static void stk_pop(stk_t *s, uint32_t v)  { for (int i = 0; i < s->D - 1; i++) s->e[i] = s->e[i + 1]; s->e[s->D - 1] = v; }
+static void stk_write(stk_t *s, uint32_t v) { s->e[0] = v; }
+static uint32_t stk_read(const stk_t *s, int adr) { return s->e[adr - 1]; }
+
+/* ------------------------------------------------------------------------------------ */
+/* Literal FSM (my_module.h)                                                              */
+/* ------------------------------------------------------------------------------------ */
+typedef uint32_t word_t[PAR];   /* one TYPE_LLRS: 16 six-bit SM patterns */
+
+enum { ST_INIT, ST_F, ST_R, ST_G, ST_H, ST_H0, ST_F_REP, ST_G_R1, ST_G_SPC, ST_END, ST_COUNT };
+
+typedef struct {
+    int N, NDIV, DEPTH_DIV;
+    uint32_t cmask;                 /* COUNTER = sc_uint<log2N + 1> */
+    word_t *llr_mem_a, *llr_mem_b;
+    uint16_t *bit_mem_1, *bit_mem_2;
+    uint16_t *bit_frozen;
+    uint8_t *node_type;
+    stk_t nts;                      /* Node_type_stack: 8-bit entries, never reset by INIT */
+    long state_count[ST_COUNT];
+} fsm_t;
+
+static int ilog2(int v) { int l = 0; while ((1 << l) < v) l++; return l; }
+
+/* my_module::do_prunning (my_module.h:61-166) */
+static void fsm_prune(fsm_t *m, const uint8_t *mask)
+{
+    for (int i = 0; i < m->NDIV; i++) {
+        uint32_t tab = 0;
+        for (int k = 0; k < PAR; k++) tab |= (uint32_t)(mask[i * PAR + k] & 1u) << k;
+        m->bit_frozen[i] = (uint16_t)tab;
+        m->node_type[i] = (uint8_t)orc_classify_group(tab);
+    }
+}
+
+/* type aggregation of my_module.h:403-435 + 447-471 (and 739-806): over groups
+ * [g0, g0+cnt) */
+static uint32_t aggregate(const fsm_t *m, int g0, int cnt)
+{
+    uint32_t R0 = 0x00, R1 = 0x0F, SPC_1st = 0x00, SPC_R1 = 0x0F, REP_R0 = 0x00, REP_last = 0x00;
+    for (int t = 0; t < cnt; t++) {
+        uint32_t T = m->node_type[g0 + t];
+        R0 |= T; R1 &= T;
+        if (t == 0) SPC_1st = T; else SPC_R1 &= T;
+        if (t == cnt - 1) REP_last = T; else REP_R0 |= T;
+    }
+    if (R0 == NODE_R0) return NODE_R0;
+    if (R1 == NODE_R1) return NODE_R1;
+    if (REP_R0 == NODE_R0 && ((REP_last >> 1) & 7u) == 0x01) return REP_last;
+    if (SPC_R1 == NODE_R1 && ((SPC_1st >> 1) & 7u) == 0x02) return SPC_1st;
+    return NODE_RN;
+}
+
+static void word_F(word_t r, const word_t a, const word_t b)
+{ for (int l = 0; l < PAR; l++) r[l] = orc_F_sm(LLR_BITS, a[l], b[l]); }
+static void word_G(word_t r, const word_t a, const word_t b, uint32_t sa)
+{ for (int l = 0; l < PAR; l++) r[l] = orc_G_sm(LLR_BITS, a[l], b[l], (sa >> l) & 1u); }
+static uint32_t word_sign(const word_t a)
+{ uint32_t s = 0; for (int l = 0; l < PAR; l++) s |= ((a[l] >> (LLR_BITS - 1)) & 1u) << l; return s; }
+
+#define CNT(x) ((x) & m->cmask)
+#define CHK(i) do { if ((uint32_t)(i) >= (uint32_t)m->NDIV) return -100; } while (0)
+
+/* one frame through do_action (my_module.h:174-1877); in: N_DIV words (wrapper_in output),
+ * out: N_DIV bit words (wrapper_out input) */
+static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
+{
+    const int NDIV = m->NDIV;
+    uint32_t ptr_FB = 0, N_REG = 0, NB_ITER = 0;
+    int R_state_condition = 0;
+    uint32_t adr_a = 0, adr_b = 0, adr_w_a = 0, adr_w_b = 0, adr_s = 0;
+    uint32_t ps_adr_a = 0, ps_adr_b = 0, ps_adr = 0;
+    word_t reg_result;
+    stk_t stack; stack.D = m->DEPTH_DIV; memset(stack.e, 0, sizeof stack.e);
+    uint32_t G_stack_value = 1;
+    uint32_t left_Node = 0, right_Node = 0;
+    memset(reg_result, 0, sizeof reg_result);
+
+    int st = ST_INIT, next = ST_INIT;
+    for (long guard = 0; guard < 100000000L; guard++) {
+        m->state_count[st]++;
+        switch (st) {
+        case ST_INIT: {                                             /* :285-333 */
+            for (int i = 0; i < NDIV / 2; i++) memcpy(m->llr_mem_a[i], in[i], sizeof(word_t));
+            for (int i = 0; i < NDIV / 2; i++) memcpy(m->llr_mem_b[i], in[NDIV / 2 + i], sizeof(word_t));
+            ptr_FB = 0;
+            N_REG = (uint32_t)NDIV;
+            adr_a = 0; adr_b = 0;
+            adr_w_a = (uint32_t)(NDIV >> 1); adr_w_b = (uint32_t)(NDIV >> 1);
+            adr_s = 0;
+            memset(stack.e, 0, sizeof stack.e);
+            stk_push(&m->nts, (NODE_RN << 4) | NODE_RN);
+            next = ST_F;
+            break;
+        }
+        case ST_F:                                                  /* :337-540 */
+        case ST_G: {                                                /* :669-877 */
+            const int isF = (st == ST_F);
+            if (isF) {
+                NB_ITER = CNT(N_REG >> 1);
+                N_REG = CNT(N_REG >> 1);
+                stk_push(&stack, 0);
+            } else {
+                NB_ITER = N_REG;
+                stk_write(&stack, G_stack_value);
+            }
+            for (uint32_t i = 0; i < NB_ITER; i++) {
+                word_t res;
+                CHK(adr_a); CHK(adr_b);
+                if (isF) {
+                    word_F(res, m->llr_mem_a[adr_a], m->llr_mem_b[adr_b]);
+                } else {
+                    uint32_t sa = 0;
+                    if (G_stack_value != 2) { CHK(ps_adr); sa = m->bit_mem_1[ps_adr]; }
+                    word_G(res, m->llr_mem_a[adr_a], m->llr_mem_b[adr_b], sa);
+                }
+                memcpy(reg_result, res, sizeof(word_t));
+                if (NB_ITER == 1) {
+                    if (isF) { CHK(adr_w_a); memcpy(m->llr_mem_a[adr_w_a], res, sizeof(word_t)); }
+                    else     { CHK(adr_w_b); memcpy(m->llr_mem_b[adr_w_b], res, sizeof(word_t)); }
+                } else if (i < (NB_ITER >> 1)) {
+                    CHK(adr_w_a); memcpy(m->llr_mem_a[adr_w_a], res, sizeof(word_t)); adr_w_a = CNT(adr_w_a + 1);
+                } else {
+                    CHK(adr_w_b); memcpy(m->llr_mem_b[adr_w_b], res, sizeof(word_t)); adr_w_b = CNT(adr_w_b + 1);
+                }
+                adr_a = CNT(adr_a + 1); adr_b = CNT(adr_b + 1);
+                if (!isF) ps_adr = CNT(ps_adr + 1);
+            }
+            /* node-type aggregation: only accumulated when NB_ITER > 1; otherwise the
+             * initial register values classify both halves as R0 (my_module.h:358-371) */
+            if (NB_ITER > 1) {
+                left_Node = aggregate(m, (int)ptr_FB, (int)(NB_ITER >> 1));
+                right_Node = aggregate(m, (int)(ptr_FB + (NB_ITER >> 1)), (int)(NB_ITER - (NB_ITER >> 1)));
+            } else {
+                left_Node = NODE_R0; right_Node = NODE_R0;
+            }
+            if (isF) stk_push(&m->nts, (left_Node << 4) | right_Node);
+            else     stk_write(&m->nts, (left_Node << 4) | right_Node);
+
+            if (N_REG > 1) {
+                switch (left_Node) {
+                case NODE_R0: {                                     /* H0 route :481-507 */
+                    N_REG = CNT(N_REG >> 1);
+                    stk_push(&stack, 0);
+                    stk_push(&m->nts, 0x00);
+                    adr_s = CNT(adr_s + N_REG);
+                    ptr_FB = CNT(ptr_FB + N_REG);
+                    uint32_t rn = stk_read(&m->nts, 2) & 0xFu;
+                    ps_adr = CNT(adr_s - N_REG);
+                    G_stack_value = 2;
+                    if (rn == NODE_R1) next = ST_G_R1;
+                    else if (rn == NODE_SPC) next = ST_G_SPC;
+                    else next = ST_G;
+                    break;
+                }
+                case NODE_REP: next = ST_F_REP; break;
+                default: next = ST_F; break;
+                }
+            } else {
+                adr_a = CNT(adr_a - 1); adr_b = CNT(adr_b - 1);
+                R_state_condition = isF;
+                next = ST_R;
+            }
+            break;
+        }
+        case ST_R: {                                                /* :544-665 */
+            CHK(ptr_FB);
+            uint32_t is_frozen = m->bit_frozen[ptr_FB];
+            ptr_FB = CNT(ptr_FB + 1);
+            uint32_t ps = orc_leaf16(reg_result, is_frozen);
+            CHK(adr_s);
+            m->bit_mem_1[adr_s] = (uint16_t)ps; m->bit_mem_2[adr_s] = (uint16_t)ps;
+            adr_s = CNT(adr_s + 1);
+            uint32_t rn = stk_read(&m->nts, 2) & 0xFu;
+            uint32_t condition = stk_read(&stack, 1);
+            if (R_state_condition) {
+                ps_adr = CNT(adr_s - N_REG);
+                G_stack_value = 1;
+                if (rn == NODE_R1) next = ST_G_R1;
+                else if (rn == NODE_SPC) next = ST_G_SPC;
+                else next = ST_G;
+            } else {
+                ps_adr_a = CNT(adr_s - (N_REG << 1));
+                ps_adr_b = CNT(adr_s - N_REG);
+                next = (condition == 1) ? ST_H : ST_H0;
+            }
+            break;
+        }
+        case ST_H:                                                  /* :881-998 */
+        case ST_H0: {                                               /* :1002-1104 */
+            const int isH = (st == ST_H);
+            NB_ITER = N_REG;
+            N_REG = CNT(N_REG << 1);
+            stk_pop(&stack, 0);
+            stk_pop(&m->nts, 0x00);
+            for (uint32_t i = 0; i < NB_ITER; i++) {
+                CHK(ps_adr_a); CHK(ps_adr_b);
+                uint16_t v = isH ? (uint16_t)(m->bit_mem_1[ps_adr_a] ^ m->bit_mem_2[ps_adr_b])
+                                 : m->bit_mem_2[ps_adr_b];
+                m->bit_mem_1[ps_adr_a] = v; m->bit_mem_2[ps_adr_a] = v;
+                ps_adr_a = CNT(ps_adr_a + 1); ps_adr_b = CNT(ps_adr_b + 1);
+            }
+            adr_a = CNT(adr_a - N_REG); adr_b = CNT(adr_b - N_REG);
+            adr_w_a = CNT(adr_w_a - NB_ITER); adr_w_b = CNT(adr_w_b - NB_ITER);
+            uint32_t condition = stk_read(&stack, 1);
+            uint32_t rn = stk_read(&m->nts, 2) & 0xFu;
+            if (condition == 1) {
+                ps_adr_a = CNT(adr_s - (N_REG << 1)); ps_adr_b = CNT(adr_s - N_REG);
+                next = ST_H;
+            } else if (condition == 2) {
+                ps_adr_a = CNT(adr_s - (N_REG << 1)); ps_adr_b = CNT(adr_s - N_REG);
+                next = ST_H0;
+            } else if (ptr_FB == (uint32_t)NDIV) {
+                next = ST_END;
+            } else {
+                ps_adr = CNT(adr_s - N_REG);
+                G_stack_value = 1;
+                if (rn == NODE_R1) next = ST_G_R1;
+                else if (rn == NODE_SPC) next = ST_G_SPC;
+                else next = ST_G;
+            }
+            break;
+        }
+        case ST_F_REP: {                                            /* :1292-1390 */
+            NB_ITER = CNT(N_REG >> 1);
+            N_REG = CNT(N_REG >> 1);
+            stk_push(&stack, 0);
+            stk_push(&m->nts, 0x00);
+            uint32_t sum = 0;   /* sc_bigint<LLR_BITS + LOG2_PAR + 1> = 11-bit SM pattern */
+            for (uint32_t i = 0; i < NB_ITER; i++) {
+                word_t res;
+                CHK(adr_a); CHK(adr_b); CHK(adr_s);
+                word_F(res, m->llr_mem_a[adr_a], m->llr_mem_b[adr_b]);
+                sum = orc_rep_add_tree16(res, sum);
+                m->bit_mem_1[adr_s] = 0; m->bit_mem_2[adr_s] = 0;
+                adr_a = CNT(adr_a + 1); adr_b = CNT(adr_b + 1); adr_s = CNT(adr_s + 1);
+            }
+            if ((sum >> 10) & 1u) {
+                adr_s = CNT(adr_s - NB_ITER);
+                for (uint32_t i = 0; i < NB_ITER; i++) {
+                    CHK(adr_s);
+                    m->bit_mem_1[adr_s] = 0xFFFF; m->bit_mem_2[adr_s] = 0xFFFF;
+                    adr_s = CNT(adr_s + 1);
+                }
+            }
+            ptr_FB = CNT(ptr_FB + NB_ITER);
+            adr_a = CNT(adr_a - NB_ITER); adr_b = CNT(adr_b - NB_ITER);
+            uint32_t rn = stk_read(&m->nts, 2) & 0xFu;
+            ps_adr = CNT(adr_s - N_REG);
+            G_stack_value = 1;
+            if (rn == NODE_R1) next = ST_G_R1;
+            else if (rn == NODE_SPC) next = ST_G_SPC;
+            else next = ST_G;
+            break;
+        }
+        case ST_G_R1:                                               /* :1571-1642 */
+        case ST_G_SPC: {                                            /* :1737-1842 */
+            const int isSPC = (st == ST_G_SPC);
+            NB_ITER = N_REG;
+            stk_write(&stack, G_stack_value);
+            stk_write(&m->nts, 0x00);
+            uint32_t parity = 0, old_min = 0xFFFFu & msk(LLR_BITS), old_mask = 0, adr_min = 0, sign_min = 0;
+            for (uint32_t i = 0; i < NB_ITER; i++) {
+                word_t res;
+                CHK(adr_a); CHK(adr_b); CHK(adr_s);
+                uint32_t sa = 0;
+                if (G_stack_value != 2) { CHK(ps_adr); sa = m->bit_mem_1[ps_adr]; }
+                word_G(res, m->llr_mem_a[adr_a], m->llr_mem_b[adr_b], sa);
+                uint32_t sign = word_sign(res);
+                m->bit_mem_1[adr_s] = (uint16_t)sign; m->bit_mem_2[adr_s] = (uint16_t)sign;
+                adr_a = CNT(adr_a + 1); adr_b = CNT(adr_b + 1); ps_adr = CNT(ps_adr + 1); adr_s = CNT(adr_s + 1);
+                if (isSPC) {
+                    uint32_t p = 0;                               /* Parity_TREE_16 */
+                    for (int l = 0; l < PAR; l++) p ^= (sign >> l) & 1u;
+                    parity ^= p;
+                    uint32_t mm = orc_min_mask16(res);            /* MIN_MASK_TREE_FCT */
+                    uint32_t new_min = (mm >> 16) & msk(LLR_BITS);
+                    uint32_t new_mask = mm & 0xFFFFu;
+                    if (new_min < old_min) { old_min = new_min; old_mask = new_mask; adr_min = i; sign_min = sign; }
+                }
+            }
+            if (isSPC && parity != 0) {
+                uint32_t a = CNT(adr_s - NB_ITER + adr_min);
+                CHK(a);
+                uint16_t v = (uint16_t)(sign_min ^ old_mask);
+                m->bit_mem_1[a] = v; m->bit_mem_2[a] = v;
+            }
+            ptr_FB = CNT(ptr_FB + NB_ITER);
+            adr_a = CNT(adr_a - NB_ITER); adr_b = CNT(adr_b - NB_ITER);
+            ps_adr_a = CNT(adr_s - (N_REG << 1)); ps_adr_b = CNT(adr_s - N_REG);
+            uint32_t condition = stk_read(&stack, 1);
+            next = (condition == 1) ? ST_H : ST_H0;
+            break;
+        }
+        case ST_END: {                                              /* :1848-1869 */
+            for (int i = 0; i < NDIV; i++) out[i] = m->bit_mem_1[i];
+            return 0;
+        }
+        default:
+            return -101;
+        }
+        st = next;
+    }
+    return -102;
+}
+
+/* wrapper_in (wrapper_in.h:26-44): 6-bit CA2 stream -> SM, 16 per word, lane i = i-th */
+static void wrap_in(const int8_t *llr, int N, word_t *w)
+{
+    for (int i = 0; i < N; i++)
+        w[i / PAR][i % PAR] = orc_qconv_format(LLR_BITS, (uint32_t)(uint8_t)llr[i] & msk(LLR_BITS));
+}
+
+/* decode nframes frames with the literal FSM. mask: N bytes (1 = information bit).
+ * llr: nframes*N int8 (2's complement, low 6 bits used as sc_bigint<6>).
+ * xhat: nframes*N bytes 0/1 (wrapper_out order). Returns 0 or a negative error.
+ * state_counts (optional, ST_COUNT longs): per-state visit counts over all frames. */
+int orc_decode_fsm(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
+                   long *state_counts)
+{
+    if (N < 32 || (N & (N - 1)) != 0) return -22;
+    fsm_t m;
+    memset(&m, 0, sizeof m);
+    m.N = N; m.NDIV = N / PAR;
+    m.DEPTH_DIV = ilog2(m.NDIV) + 1;           /* Writer.h:121: log2(N/PAR) + 1 */
+    m.cmask = msk(ilog2(N) + 1);               /* COUNTER = sc_uint<_DEPTH>, _DEPTH = log2N+1 */
+    m.nts.D = m.DEPTH_DIV;
+    m.llr_mem_a = (word_t *)calloc((size_t)m.NDIV, sizeof(word_t));
+    m.llr_mem_b = (word_t *)calloc((size_t)m.NDIV, sizeof(word_t));
+    m.bit_mem_1 = (uint16_t *)calloc((size_t)m.NDIV, 2);
+    m.bit_mem_2 = (uint16_t *)calloc((size_t)m.NDIV, 2);
+    m.bit_frozen = (uint16_t *)calloc((size_t)m.NDIV, 2);
+    m.node_type = (uint8_t *)calloc((size_t)m.NDIV, 1);
+    word_t *in = (word_t *)calloc((size_t)m.NDIV, sizeof(word_t));
+    uint16_t *out = (uint16_t *)calloc((size_t)m.NDIV, 2);
+    int rc = 0;
+    if (!m.llr_mem_a || !m.llr_mem_b || !m.bit_mem_1 || !m.bit_mem_2 || !m.bit_frozen ||
+        !m.node_type || !in || !out) { rc = -12; goto done; }
+    fsm_prune(&m, mask);
+    for (int f = 0; f < nframes; f++) {
+        wrap_in(llr + (size_t)f * N, N, in);
+        rc = fsm_frame(&m, in, out);
+        if (rc) goto done;
+        for (int i = 0; i < N; i++) xhat[(size_t)f * N + i] = (uint8_t)((out[i / PAR] >> (i % PAR)) & 1u);
+    }
+    if (state_counts) for (int s = 0; s < ST_COUNT; s++) state_counts[s] = m.state_count[s];
+done:
+    free(m.llr_mem_a); free(m.llr_mem_b); free(m.bit_mem_1); free(m.bit_mem_2);
+    free(m.bit_frozen); free(m.node_type); free(in); free(out);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Recursive restatement -- independent of the FSM registers     */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    int G;
+    const uint16_t *fb;     /* per group */
+    const uint8_t *type;    /* per group */
+    uint16_t *x;            /* per group, encoded bits */
+} rec_t;
+
+static uint32_t node_type(const rec_t *r, int g0, int cnt)
+{
+    uint32_t R0 = 0, R1 = 0x0F;
+    int all_r0_but_last = 1, all_r1_but_first = 1;
+    for (int t = 0; t < cnt; t++) {
+        uint32_t T = r->type[g0 + t];
+        R0 |= T; R1 &= T;
+        if (t < cnt - 1 && T != NODE_R0) all_r0_but_last = 0;
+        if (t > 0 && T != NODE_R1) all_r1_but_first = 0;
+    }
+    if (R0 == 0) return NODE_R0;
+    if (R1 == 0x0F) return NODE_R1;
+    if (all_r0_but_last && r->type[g0 + cnt - 1] == NODE_REP) return NODE_REP;
+    if (all_r1_but_first && r->type[g0] == NODE_SPC) return NODE_SPC;
+    return NODE_RN;
+}
+
+/* decode node covering groups [g0, g0+cnt) with LLR words lam[0..cnt) (6-bit SM) */
+static void rec_node(rec_t *r, int g0, int cnt, const word_t *lam, int is_root)
+{
+    if (cnt == 1) { r->x[g0] = (uint16_t)orc_leaf16(lam[0], r->fb[g0]); return; }
+    int h = cnt / 2;
+    uint32_t tl = is_root ? NODE_RN : node_type(r, g0, h);
+    uint32_t tr = is_root ? NODE_RN : node_type(r, g0 + h, h);
+    word_t *child = (word_t *)malloc((size_t)h * sizeof(word_t));
+    int left_zero = 0;
+    if (tl == NODE_R0) {
+        left_zero = 1;
+        for (int i = 0; i < h; i++) r->x[g0 + i] = 0;
+    } else if (tl == NODE_REP) {
+        uint32_t acc = 0;
+        for (int i = 0; i < h; i++) { word_t t; word_F(t, lam[i], lam[h + i]); acc = orc_rep_add_tree16(t, acc); }
+        uint16_t d = ((acc >> 10) & 1u) ? 0xFFFF : 0;
+        for (int i = 0; i < h; i++) r->x[g0 + i] = d;
+    } else {
+        for (int i = 0; i < h; i++) word_F(child[i], lam[i], lam[h + i]);
+        rec_node(r, g0, h, child, 0);
+    }
+    /* right child: lambda = G(a, b, x_left) (saturated) */
+    for (int i = 0; i < h; i++) word_G(child[i], lam[i], lam[h + i], left_zero ? 0u : r->x[g0 + i]);
+    if (tr == NODE_R1) {
+        for (int i = 0; i < h; i++) r->x[g0 + h + i] = (uint16_t)word_sign(child[i]);
+    } else if (tr == NODE_SPC) {
+        /* Wagner: parity of hard decisions; flip the min |lambda| position
+         * (lexicographic (|l|, group, bitrev4(lane)) -- equivalent to the in-group tournament
+         * of Min_Mask_16_SM plus the strict '<' across groups) */
+        uint32_t parity = 0, best = 0xFFFFFFFFu; int bg = 0, bl = 0;
+        for (int i = 0; i < h; i++) {
+            uint32_t s = word_sign(child[i]);
+            r->x[g0 + h + i] = (uint16_t)s;
+            for (int l = 0; l < PAR; l++) {
+                parity ^= (s >> l) & 1u;
+                uint32_t br = ((l & 1) << 3) | ((l & 2) << 1) | ((l & 4) >> 1) | ((l & 8) >> 3);
+                uint32_t key = ((child[i][l] & 0x1Fu) << 24) | ((uint32_t)i << 4) | br;
+                if (key < best) { best = key; bg = i; bl = l; }
+            }
+        }
+        if (parity) r->x[g0 + h + bg] ^= (uint16_t)(1u << bl);
+    } else {
+        rec_node(r, g0 + h, h, child, 0);
+    }
+    /* combine: H (xor) or H0 (copy) */
+    for (int i = 0; i < h; i++) r->x[g0 + i] = left_zero ? r->x[g0 + h + i] : (uint16_t)(r->x[g0 + i] ^ r->x[g0 + h + i]);
+    free(child);
+}
+
+int orc_decode_rec(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes)
+{
+    if (N < 32 || (N & (N - 1)) != 0) return -22;
+    int G = N / PAR;
+    uint16_t *fb = (uint16_t *)calloc((size_t)G, 2);
+    uint8_t *type = (uint8_t *)calloc((size_t)G, 1);
+    uint16_t *x = (uint16_t *)calloc((size_t)G, 2);
+    word_t *in = (word_t *)calloc((size_t)G, sizeof(word_t));
+    if (!fb || !type || !x || !in) { free(fb); free(type); free(x); free(in); return -12; }
+    for (int g = 0; g < G; g++) {
+        uint32_t t = 0;
+        for (int k = 0; k < PAR; k++) t |= (uint32_t)(mask[g * PAR + k] & 1u) << k;
+        fb[g] = (uint16_t)t; type[g] = (uint8_t)orc_classify_group(t);
+    }
+    rec_t r = { G, fb, type, x };
+    for (int f = 0; f < nframes; f++) {
+        wrap_in(llr + (size_t)f * N, N, in);
+        rec_node(&r, 0, G, in, 1);
+        for (int i = 0; i < N; i++) xhat[(size_t)f * N + i] = (uint8_t)((x[i / PAR] >> (i % PAR)) & 1u);
+    }
+    free(fb); free(type); free(x); free(in);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Encoder x = u . F^{(x)n}, F = [[1,0],[1,1]], natural order             */
+/* ------------------------------------------------------------------------------------ */
+void orc_encode(int N, const uint8_t *u, uint8_t *x, int nframes)
+{
+    for (int f = 0; f < nframes; f++) {
+        uint8_t *v = x + (size_t)f * N;
+        for (int i = 0; i < N; i++) v[i] = u[(size_t)f * N + i] & 1u;
+        for (int h = 1; h < N; h <<= 1)
+            for (int b = 0; b < N; b += 2 * h)
+                for (int j = b; j < b + h; j++) v[j] ^= v[j + h];
+    }
+}
