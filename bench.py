@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded information bits/s of the MI355X SC polar decoder.
+
+Workload (BASELINE.json configs[1], "C2"): N=1024, K=512 (Frozen_Bit_Tab/FB_N1024_K512.txt),
+65536 AWGN frames per GPU (Eb/N0 = 2.5 dB, seed 0xF0 as in src/testbench/main.cpp:86-104),
+int8 LLRs already resident in HBM. One step = one decode of the whole per-GPU batch.
+
+Multi-GPU (torchrun, one process per GPU, RCCL): every rank generates and decodes its own
+shard of frames (weak scaling, no data-path collective); timing is max over ranks.
+
+Prints ONE JSON line (rank 0). Extra fields:
+  roofline     -- HBM roofline of the decode kernel: algorithmic bytes per launch
+                  (1.125 N bytes per frame: N int8 LLRs in + N/8 bytes of x^ out) / mean
+                  kernel duration (HIP events on the launch stream)
+  cpu_baseline -- the CPU oracle (literal C restatement of my_module::do_action, one thread)
+                  timed on a bounded sample on this host, rank 0 / N=1 only
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (mask fixture, per-GPU frames at N=1 semantics, description)
+    "c1": ("FB_N128_K64", 1, "N=128 K=64 single frame (plumbing)"),
+    "c2": ("FB_N1024_K512", 65536, "N=1024 K=512, 65536-frame batch per GPU"),
+    "c3": ("frozen_n_65536_k_32768", 4096, "N=65536 K=32768, 4096-frame batch per GPU"),
+    "c4": ("FB_N1024_K512", None, "N=1024 K=512, 2^20 frames sharded over the GPUs"),
+    "c5": ("frozen_n_262144_k_131072", None, "N=262144 K=131072, 512 frames sharded over the GPUs"),
+}
+
+
+def gen_frames_torch(torch, mask, batch, ebn0_db, seed, device):
+    """Synthetic AWGN frames on the GPU (reference C-sim chain semantics)."""
+    N = mask.size
+    K = int(mask.sum())
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    m = torch.from_numpy(mask.astype(np.uint8)).to(device)
+    u = torch.randint(0, 2, (batch, N), generator=g, device=device, dtype=torch.uint8) & m
+    x = u.clone()
+    h = 1
+    while h < N:
+        v = x.view(batch, N // (2 * h), 2, h)
+        v[:, :, 0, :] ^= v[:, :, 1, :]
+        h *= 2
+    sigma = 1.0 / np.sqrt(2.0 * (K / N) * 10.0 ** (ebn0_db / 10.0))
+    y = (1.0 - 2.0 * x.float()) + sigma * torch.randn((batch, N), generator=g, device=device)
+    llr = torch.clamp(torch.trunc(4.0 * y), -31, 31).to(torch.int8).contiguous()
+    return llr, x
+
+
+def cpu_baseline(mask, seconds, ebn0_db):
+    """Time the CPU oracle (single thread) on a bounded sample; returns a dict."""
+    from oracle import oracle
+    import util
+    oracle.build()
+    N, K = mask.size, int(mask.sum())
+    sample = max(8, min(4096, int(2 ** 22 // N)))
+    llr, _ = util.synth_frames(mask, sample, ebn0_db=ebn0_db, seed=0xF0)
+    oracle.decode_fsm(mask, llr[:2])   # warm
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        oracle.decode_fsm(mask, llr)
+        frames += sample
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    fps = frames / el
+    return {"value": fps * K, "unit": "info_bits/s", "frames_per_sec": fps, "cores": 1,
+            "kind": "port",
+            "sample": "%d frames (N=%d K=%d, Eb/N0=%.1f dB) decoded repeatedly for %.1f s by "
+                      "oracle/polar_oracle.c orc_decode_fsm (literal my_module FSM), 1 thread"
+                      % (sample, N, K, ebn0_db, el)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="override per-GPU frames")
+    ap.add_argument("--ebn0", type=float, default=2.5)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", type=int, default=64, help="frames checked vs the oracle (rank 0)")
+    args = ap.parse_args()
+
+    import torch
+    import sc_polar_decoder_hls_amd as pkg
+    import util
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("--gpus %d needs torchrun with %d processes" % (args.gpus, args.gpus))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    name, per_gpu, desc = CONFIGS[args.config]
+    mask = util.mask(name)
+    N, K = mask.size, int(mask.sum())
+    if args.config == "c4":
+        per_gpu = (1 << 20) // world
+    elif args.config == "c5":
+        per_gpu = max(1, 512 // world)
+    if args.batch:
+        per_gpu = args.batch
+
+    dec = pkg.Decoder(mask)
+    dec.prepare(per_gpu)
+    llr, x = gen_frames_torch(torch, mask, per_gpu, args.ebn0, 0xF0 + 7919 * rank, dev)
+    out = torch.empty((per_gpu, dec.words), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        dec.decode(llr, out, stream)
+    torch.cuda.synchronize()
+
+    # parity spot check (rank 0) vs the CPU oracle on the first frames of the batch
+    check = {}
+    if rank == 0 and args.check > 0:
+        from oracle import oracle
+        nchk = min(args.check, per_gpu)
+        got = pkg.unpack_bits(out[:nchk].cpu().numpy(), N)
+        ref = oracle.decode_fsm(mask, llr[:nchk].cpu().numpy())
+        check = {"frames": nchk, "bit_exact": bool((got == ref).all())}
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        dec.decode(llr, out, stream)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    total_frames = per_gpu * world * args.steps
+    fps = total_frames / elapsed
+    value = fps * K
+
+    # frame error rate of this batch vs the transmitted codewords (informative)
+    xhat = pkg.unpack_bits(out[: min(per_gpu, 4096)].cpu().numpy(), N)
+    fer = float((xhat != x[: xhat.shape[0]].cpu().numpy()).any(axis=1).mean())
+
+    if rank == 0:
+        bytes_per_launch = 1.125 * N * per_gpu
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        res = {
+            "metric": "decoded info bits/sec + frames/sec, N=1024 K=512 batch, 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "info_bits/s",
+            "frames_per_sec": fps,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int16 sign-magnitude (6-bit LLRs, u8 in / bit-packed out)",
+            "data": "synthetic AWGN frames generated on-device (BPSK, Eb/N0=%.1f dB, 4x quantizer, +-31)" % args.ebn0,
+            "config": {"workload": desc, "N": N, "K": K, "frames_per_gpu": per_gpu,
+                       "mask": name, "parallelism": "frames sharded, dp%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "polar_sc_decode_kernel", "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_launch": bytes_per_launch},
+            "frame_error_rate": fer,
+            "parity_check": check,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(mask, args.cpu_seconds, args.ebn0)
+        print(json.dumps(res))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

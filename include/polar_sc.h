@@ -1,0 +1,170 @@
+/*
+ * polar_sc.h -- C ABI of the MI355X-native batched SC polar decoder (libpolar_sc.so).
+ *
+ * Drop-in boundary for the hot path of ydelomier/SC_Polar_decoder_HLS: the decoder core
+ * SC_MODULE(my_module) (src/module/my_module.h:15-36) plus its stream adapters
+ * wrapper_in (src/module/wrapper_in.h:26-44) and wrapper_out (src/module/wrapper_out.h:26-36),
+ * i.e. the testbench-level contract
+ *
+ *     decode(llr_in, frozen_bits) -> hard_bits
+ *
+ * where llr_in is the quantizer's stream of 6-bit two's-complement LLRs
+ * (src/testbench/sc_quantizer/sc_quantizer.h:69-81), frozen_bits is the frozen-bit table
+ * (FB port, my_module.h:33; bit = 1 -> information bit) and hard_bits is the estimated
+ * codeword x^ (bit_mem_1 streamed out by END, my_module.h:1859-1866), natural order.
+ *
+ * Plain pointers and sizes only; no HIP, torch or C++ types cross this boundary. Every
+ * function returns 0 on success or a negative errno value (-EINVAL, -ENOMEM, -ENOTSUP,
+ * -ENOENT, -EIO for a HIP runtime failure); polar_sc_strerror() names it.
+ */
+#ifndef POLAR_SC_H
+#define POLAR_SC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define POLAR_SC_ABI_VERSION 1
+#define POLAR_SC_PAR 16
+
+/*
+ * Decoder configuration. Mirrors the compile-time switches of the reference's
+ * src/module/config.h:2-30 (+ PAR from polar_parameters.h:8). The reference ships ONE
+ * configuration and parity is defined for exactly that one; it is the default
+ * (polar_sc_default_config). Any other value is rejected with -ENOTSUP in this version.
+ */
+typedef struct polar_sc_config {
+    int32_t llr_bits;       /* LLR_BITS            (config.h:2)      default 6  */
+    int32_t par;            /* PAR                 (polar_parameters.h:8) 16    */
+    int32_t sigmag;         /* SIGMAG=1 / CA2=0    (config.h:11)     default 1  */
+    int32_t extended;       /* EXTENDED            (config.h:14)     default 1  */
+    int32_t pruning_level;  /* PRUNING_LEVEL       (config.h:16)     default 2  */
+    int32_t elag_r1;        /* ELAG_R1             (config.h:19)     default 1  */
+    int32_t elag_rep;       /* ELAG_REP            (config.h:20)     default 1  */
+    int32_t elag_spc;       /* ELAG_SPC            (config.h:21)     default 1  */
+    int32_t elag_rep2;      /* ELAG_REP2           (config.h:22)     default 0  */
+    int32_t elag_spc2;      /* ELAG_SPC2           (config.h:23)     default 0  */
+    int32_t elag_rare;      /* ELAG_RARE           (config.h:26)     default 0  */
+    int32_t elag_h0;        /* ELAG_H0             (config.h:28)     default 1  */
+    int32_t strict_llr;     /* 0: LLRs are taken modulo 2^6 like the reference's
+                               sc_bigint<6> LLR (config.h:6); 1: polar_sc_decode_host
+                               rejects |llr| > 31 with -EINVAL (the device entry point
+                               never validates).                           default 0 */
+} polar_sc_config;
+
+/* Immutable decode plan: N, config, frozen mask, compiled decode schedule and its device
+ * copy. Safe to share read-only between threads; decode calls on different streams may
+ * overlap (each call owns its scratch, see polar_sc_decode). */
+typedef struct polar_sc_plan polar_sc_plan;
+
+/* One step of the compiled, data-independent decode schedule (introspection only; the
+ * device consumes the same records). Replaces the FSM walk of my_module::do_action. */
+typedef struct polar_sc_op {
+    int32_t code;   /* POLAR_OP_* */
+    int32_t level;  /* source stage level (0 = channel LLRs, k = node of N/16 >> k words) */
+    int32_t n;      /* words (16 LLRs / 16 bits) per operand half */
+    int32_t pos;    /* first bit_mem word written (or combined, for H/H0) */
+    int32_t upos;   /* first bit_mem word of partial sums for G-type ops, -1 = zero (H0 route) */
+    uint32_t fb;    /* 16-bit frozen pattern of the group, leaf ops only */
+    int32_t reserved[2];
+} polar_sc_op;
+
+enum {
+    POLAR_OP_F = 1,      /* f_loop of F_STATE        (my_module.h:373-445)  */
+    POLAR_OP_G = 2,      /* g_loop of G_STATE        (my_module.h:704-781)  */
+    POLAR_OP_FLEAF = 3,  /* F with NB_ITER=1 + R_STATE leaf (my_module.h:595) */
+    POLAR_OP_GLEAF = 4,  /* G with NB_ITER=1 + R_STATE leaf                  */
+    POLAR_OP_REP = 5,    /* F_REP_STATE              (my_module.h:1292-1390) */
+    POLAR_OP_R1 = 6,     /* G_R1_STATE               (my_module.h:1571-1642) */
+    POLAR_OP_SPC = 7,    /* G_SPC_STATE              (my_module.h:1737-1842) */
+    POLAR_OP_H = 8,      /* H_STATE                  (my_module.h:881-998)   */
+    POLAR_OP_H0 = 9,     /* H0_STATE                 (my_module.h:1002-1104) */
+    POLAR_OP_END = 10    /* END                      (my_module.h:1848-1869) */
+};
+
+typedef struct polar_sc_plan_stats {
+    uint32_t N, K, groups;            /* N, information bits, N/16                    */
+    uint32_t n_r0, n_r1, n_rep, n_spc, n_rn;   /* do_prunning group census          */
+    uint32_t n_ops;                   /* schedule length (incl. END)                   */
+    uint32_t op_count[16];            /* per POLAR_OP_* code                           */
+    uint64_t word_ops;                /* sum over ops of processed words (F/G-type)    */
+    uint32_t storage;                 /* 0 = LDS-resident stages, 1 = HBM scratch      */
+    uint32_t lds_bytes_per_wave;      /* LDS footprint of one wave (8 frames)          */
+    uint64_t scratch_bytes_per_wave;  /* HBM scratch of one wave when storage == 1     */
+} polar_sc_plan_stats;
+
+/* Fill *cfg with the reference configuration (config.h as shipped). */
+int polar_sc_default_config(polar_sc_config *cfg);
+
+/* Compile a plan. N: power of two, 32 <= N <= 2^20 (INIT needs N/16 >= 2 words,
+ * my_module.h:294-309). info_mask: N bytes, nonzero = information bit (frozen table
+ * bit = 1, Frozen_Bit_Generator/src/Writer.h:86-93). cfg: NULL -> reference default.
+ * Replaces do_prunning (my_module.h:61-166) + the FB FIFO load. Host-only: it does not
+ * touch the GPU (the schedule is uploaded on the first device decode). */
+int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_mask,
+                         const polar_sc_config *cfg);
+int polar_sc_plan_destroy(polar_sc_plan *plan);
+
+/* Decode `batch` frames already resident on the current HIP device.
+ *   llr_dev:       [batch][N] int8 two's-complement LLRs (wrapper_in input stream order)
+ *   hard_bits_dev: [batch][ceil(N/64)] uint64, bit i of word j = x^[64 j + i]
+ *                  (for N = 32 the high half of each frame's single word is zero)
+ *   stream:        hipStream_t (NULL = default stream); the call is asynchronous.
+ * Replaces one INIT..END pass of my_module::do_action per frame (my_module.h:174-1877).
+ * The first call on a device uploads the schedule (synchronously); for graph capture,
+ * call polar_sc_plan_prepare first. */
+int polar_sc_decode(const polar_sc_plan *plan, const int8_t *llr_dev, uint64_t *hard_bits_dev,
+                    size_t batch, void *stream);
+
+/* Same, with the output as [batch][N/16] uint16 words (bit i of word j = x^[16 j + i]),
+ * which is exactly the sequence of TYPE_BITS tokens my_module writes to its `s` port. */
+int polar_sc_decode_u16(const polar_sc_plan *plan, const int8_t *llr_dev, uint16_t *bits_dev,
+                        size_t batch, void *stream);
+
+/* Upload the schedule and reserve device scratch for up to max_batch frames on the
+ * current device, so that later polar_sc_decode calls allocate nothing. */
+int polar_sc_plan_prepare(const polar_sc_plan *plan, size_t max_batch);
+
+/* Host-pointer convenience: copies in, decodes, copies out, synchronises.
+ * hard_bits: [batch][ceil(N/64)] uint64 as for polar_sc_decode. */
+int polar_sc_decode_host(const polar_sc_plan *plan, const int8_t *llr, uint64_t *hard_bits,
+                         size_t batch);
+
+/* Frozen_Bit_Tab/FB_N{N}_K{K}.txt reader (Writer.h:35-93, Input=0): line 1 = table size,
+ * lines 2-3 ignored, line 4 = reliability order (most reliable first). Indices >= N are
+ * dropped, the first K remaining are information bits. N = 0 -> the table's own size.
+ * mask_out: capacity `cap` bytes; *N_out receives N. */
+int polar_load_frozen_tab(const char *path, uint32_t N, uint32_t K, uint8_t *mask_out,
+                          uint32_t cap, uint32_t *N_out);
+
+/* Generated_Frozen_Bit/frozen_n_{N}_k_{K}.txt reader (Writer.h:95-105, Input=1):
+ * whitespace-separated 0/1 tokens, 1 = information bit. */
+int polar_load_mask_file(const char *path, uint8_t *mask_out, uint32_t cap, uint32_t *N_out);
+
+/* u^ = x^ . F^{(x)n} (F = [[1,0],[1,1]], self-inverse), keep the information positions.
+ * xhat: [batch][ceil(N/64)] uint64 host array; info_out: [batch][K] bytes (0/1). Host-side. */
+int polar_codeword_to_info(const polar_sc_plan *plan, const uint64_t *xhat, uint8_t *info_out,
+                           size_t batch);
+
+int polar_sc_plan_get_stats(const polar_sc_plan *plan, polar_sc_plan_stats *stats);
+
+/* Copy the compiled schedule (at most cap ops) and its length. */
+int polar_sc_plan_get_schedule(const polar_sc_plan *plan, polar_sc_op *ops, uint32_t cap,
+                               uint32_t *count);
+
+/* GPU self-test of the cross-lane (DPP) exchange patterns the kernels rely on.
+ * out_dev: 4*64 uint32 on the device; entry [h][lane] = source lane seen by `lane` for
+ * partner distance 1<<h. Synchronous. */
+int polar_sc_selftest_lanes(uint32_t *out_dev);
+
+const char *polar_sc_strerror(int err);
+int polar_sc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* POLAR_SC_H */

@@ -1,0 +1,291 @@
+"""sc_polar_decoder_hls_amd -- MI355X-native batched SC polar decoder.
+
+Host-side mirror of the reference decoder's interface (ydelomier/SC_Polar_decoder_HLS,
+SC_MODULE my_module, src/module/my_module.h:15-36, fed by wrapper_in/wrapper_out):
+
+  * the frozen-bit table goes in once (the `FB` port, read by do_prunning,
+    my_module.h:61-166)           -> Decoder(info_mask) / Decoder.load_frozen_bits()
+  * frames of 6-bit two's-complement LLRs go in (`e` port via wrapper_in.h:26-44) and the
+    estimated codeword x^ comes out (`s` port via wrapper_out.h:26-36)
+                                  -> Decoder.decode(llr) -> hard bits
+
+Everything above is a thin ctypes layer over the C ABI of libpolar_sc.so
+(include/polar_sc.h); the decode itself runs only as HIP kernels on gfx950. There is no CPU
+fallback: if the library is missing or no GPU is visible, decode raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _build
+
+__all__ = [
+    "Decoder", "PolarError", "load_frozen_tab", "load_mask_file", "unpack_bits", "pack_bits",
+    "default_config", "lib", "selftest_lanes", "OPS", "build",
+]
+
+build = _build.build
+
+OPS = {1: "F", 2: "G", 3: "FLEAF", 4: "GLEAF", 5: "REP", 6: "R1", 7: "SPC", 8: "H", 9: "H0", 10: "END"}
+
+_ERRNO = {22: "EINVAL", 12: "ENOMEM", 95: "ENOTSUP", 2: "ENOENT", 5: "EIO"}
+
+
+class PolarError(RuntimeError):
+    def __init__(self, fn, rc):
+        msg = "%s failed: %d (%s)" % (fn, rc, _ERRNO.get(-rc, "?"))
+        try:
+            msg += " - " + lib().polar_sc_strerror(rc).decode()
+        except Exception:
+            pass
+        super().__init__(msg)
+        self.rc = rc
+
+
+class polar_sc_config(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "llr_bits", "par", "sigmag", "extended", "pruning_level", "elag_r1", "elag_rep",
+        "elag_spc", "elag_rep2", "elag_spc2", "elag_rare", "elag_h0", "strict_llr")]
+
+
+class polar_sc_op(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int32), ("level", ctypes.c_int32), ("n", ctypes.c_int32),
+                ("pos", ctypes.c_int32), ("upos", ctypes.c_int32), ("fb", ctypes.c_uint32),
+                ("reserved", ctypes.c_int32 * 2)]
+
+
+class polar_sc_plan_stats(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_uint32), ("K", ctypes.c_uint32), ("groups", ctypes.c_uint32),
+                ("n_r0", ctypes.c_uint32), ("n_r1", ctypes.c_uint32), ("n_rep", ctypes.c_uint32),
+                ("n_spc", ctypes.c_uint32), ("n_rn", ctypes.c_uint32), ("n_ops", ctypes.c_uint32),
+                ("op_count", ctypes.c_uint32 * 16), ("word_ops", ctypes.c_uint64),
+                ("storage", ctypes.c_uint32), ("lds_bytes_per_wave", ctypes.c_uint32),
+                ("scratch_bytes_per_wave", ctypes.c_uint64)]
+
+
+# exported symbols of include/polar_sc.h (tests check that the library exports all of them)
+EXPORTS = (
+    "polar_sc_default_config", "polar_sc_plan_create", "polar_sc_plan_destroy", "polar_sc_decode",
+    "polar_sc_decode_u16", "polar_sc_plan_prepare", "polar_sc_decode_host", "polar_load_frozen_tab",
+    "polar_load_mask_file", "polar_codeword_to_info", "polar_sc_plan_get_stats",
+    "polar_sc_plan_get_schedule", "polar_sc_selftest_lanes", "polar_sc_strerror",
+    "polar_sc_abi_version",
+)
+
+_lib = None
+
+
+def lib():
+    """Load libpolar_sc.so (built in-tree by build()). Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_build.LIB):
+        raise RuntimeError("libpolar_sc.so is not built (%s); run sc_polar_decoder_hls_amd.build() "
+                           "or __graft_entry__.build()" % _build.LIB)
+    L = ctypes.CDLL(_build.LIB)
+    p, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "polar_sc_default_config": [p],
+        "polar_sc_plan_create": [ctypes.POINTER(p), u32, p, p],
+        "polar_sc_plan_destroy": [p],
+        "polar_sc_decode": [p, p, p, sz, p],
+        "polar_sc_decode_u16": [p, p, p, sz, p],
+        "polar_sc_plan_prepare": [p, sz],
+        "polar_sc_decode_host": [p, p, p, sz],
+        "polar_load_frozen_tab": [ctypes.c_char_p, u32, u32, p, u32, ctypes.POINTER(u32)],
+        "polar_load_mask_file": [ctypes.c_char_p, p, u32, ctypes.POINTER(u32)],
+        "polar_codeword_to_info": [p, p, p, sz],
+        "polar_sc_plan_get_stats": [p, p],
+        "polar_sc_plan_get_schedule": [p, p, u32, ctypes.POINTER(u32)],
+        "polar_sc_selftest_lanes": [p],
+        "polar_sc_strerror": [i32],
+        "polar_sc_abi_version": [],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = ctypes.c_char_p if name == "polar_sc_strerror" else i32
+    _lib = L
+    return L
+
+
+def _check(fn, rc):
+    if rc != 0:
+        raise PolarError(fn, rc)
+
+
+def default_config():
+    c = polar_sc_config()
+    _check("polar_sc_default_config", lib().polar_sc_default_config(ctypes.byref(c)))
+    return c
+
+
+def _np_ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def load_frozen_tab(path, K, N=0):
+    """Frozen_Bit_Tab/FB_N*_K*.txt -> information mask (uint8, 1 = info). Writer.h:35-93."""
+    cap = 1 << 21
+    buf = np.zeros(cap, dtype=np.uint8)
+    n = ctypes.c_uint32(0)
+    _check("polar_load_frozen_tab",
+           lib().polar_load_frozen_tab(os.fsencode(path), N, K, _np_ptr(buf), cap, ctypes.byref(n)))
+    return buf[:n.value].copy()
+
+
+def load_mask_file(path):
+    """Generated_Frozen_Bit/frozen_n_*_k_*.txt -> information mask. Writer.h:95-105."""
+    cap = 1 << 21
+    buf = np.zeros(cap, dtype=np.uint8)
+    n = ctypes.c_uint32(0)
+    _check("polar_load_mask_file",
+           lib().polar_load_mask_file(os.fsencode(path), _np_ptr(buf), cap, ctypes.byref(n)))
+    return buf[:n.value].copy()
+
+
+def unpack_bits(words, N):
+    """[B, ceil(N/64)] uint64/int64 (bit i of word j = x[64j+i]) -> [B, N] uint8."""
+    w = np.ascontiguousarray(np.asarray(words)).view(np.uint8)
+    w = w.reshape(w.shape[0], -1) if w.ndim > 1 else w.reshape(1, -1)
+    return np.unpackbits(w, axis=1, bitorder="little")[:, :N]
+
+
+def pack_bits(bits):
+    """[B, N] 0/1 -> [B, ceil(N/64)] uint64 (inverse of unpack_bits)."""
+    b = np.atleast_2d(np.asarray(bits, dtype=np.uint8))
+    B, N = b.shape
+    W = (N + 63) // 64
+    pad = np.zeros((B, W * 64), dtype=np.uint8)
+    pad[:, :N] = b
+    return np.packbits(pad, axis=1, bitorder="little").view(np.uint64).reshape(B, W)
+
+
+def _torch():
+    import torch  # plumbing only: device memory and streams
+    return torch
+
+
+class Decoder:
+    """A compiled decode plan for one frozen-bit table (== my_module after do_prunning).
+
+    info_mask: (N,) array, nonzero = information bit (frozen-table bit 1).
+    config:    polar_sc_config or None (reference config.h); other configs -> ENOTSUP.
+    """
+
+    def __init__(self, info_mask=None, config=None):
+        self._plan = ctypes.c_void_p(None)
+        self.N = 0
+        if info_mask is not None:
+            self.load_frozen_bits(info_mask, config)
+
+    # -- FB port ---------------------------------------------------------------------------
+    def load_frozen_bits(self, info_mask, config=None):
+        mask = np.ascontiguousarray(np.asarray(info_mask).astype(np.uint8) != 0, dtype=np.uint8)
+        if mask.ndim != 1:
+            raise ValueError("info_mask must be 1-D")
+        self.close()
+        plan = ctypes.c_void_p(None)
+        cfg = ctypes.byref(config) if config is not None else None
+        _check("polar_sc_plan_create",
+               lib().polar_sc_plan_create(ctypes.byref(plan), int(mask.size), _np_ptr(mask), cfg))
+        self._plan = plan
+        self.mask = mask
+        self.N = int(mask.size)
+        self.K = int(mask.sum())
+        self.words = (self.N + 63) // 64
+        return self
+
+    def close(self):
+        if getattr(self, "_plan", None) is not None and self._plan.value:
+            lib().polar_sc_plan_destroy(self._plan)
+        self._plan = ctypes.c_void_p(None)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- introspection ----------------------------------------------------------------------
+    @property
+    def stats(self):
+        s = polar_sc_plan_stats()
+        _check("polar_sc_plan_get_stats", lib().polar_sc_plan_get_stats(self._plan, ctypes.byref(s)))
+        d = {f: getattr(s, f) for f, _ in polar_sc_plan_stats._fields_ if f != "op_count"}
+        d["op_count"] = {OPS[c]: int(s.op_count[c]) for c in OPS if s.op_count[c]}
+        return d
+
+    def schedule(self):
+        """The compiled op list as a list of dicts (code name, level, n, pos, upos, fb)."""
+        n = ctypes.c_uint32(0)
+        _check("polar_sc_plan_get_schedule", lib().polar_sc_plan_get_schedule(self._plan, None, 0, ctypes.byref(n)))
+        arr = (polar_sc_op * n.value)()
+        _check("polar_sc_plan_get_schedule", lib().polar_sc_plan_get_schedule(self._plan, arr, n.value, ctypes.byref(n)))
+        return [dict(op=OPS.get(o.code, o.code), level=o.level, n=o.n, pos=o.pos, upos=o.upos, fb=o.fb)
+                for o in arr]
+
+    def prepare(self, max_batch):
+        _check("polar_sc_plan_prepare", lib().polar_sc_plan_prepare(self._plan, int(max_batch)))
+
+    # -- e -> s ports -----------------------------------------------------------------------
+    def decode(self, llr, out=None, stream=None):
+        """Decode frames resident on the GPU.
+
+        llr: torch.int8 CUDA tensor [B, N] (contiguous). Returns (or fills `out`) a torch.int64
+        CUDA tensor [B, ceil(N/64)] whose bits are x^ (bit i of word j = x^[64j+i]).
+        Asynchronous on `stream` (default: torch's current stream).
+        """
+        torch = _torch()
+        if not (isinstance(llr, torch.Tensor) and llr.is_cuda and llr.dtype == torch.int8):
+            raise TypeError("llr must be a CUDA int8 tensor")
+        if llr.dim() != 2 or llr.shape[1] != self.N or not llr.is_contiguous():
+            raise ValueError("llr must be contiguous [B, %d]" % self.N)
+        B = llr.shape[0]
+        if out is None:
+            out = torch.empty((B, self.words), dtype=torch.int64, device=llr.device)
+        elif out.shape != (B, self.words) or out.dtype != torch.int64 or not out.is_contiguous():
+            raise ValueError("out must be contiguous int64 [B, %d]" % self.words)
+        s = stream if stream is not None else torch.cuda.current_stream(llr.device)
+        _check("polar_sc_decode", lib().polar_sc_decode(
+            self._plan, ctypes.c_void_p(llr.data_ptr()), ctypes.c_void_p(out.data_ptr()), B,
+            ctypes.c_void_p(s.cuda_stream)))
+        return out
+
+    def decode_u16(self, llr, out=None, stream=None):
+        """As decode(), output int16 [B, N/16]: the TYPE_BITS tokens of my_module's `s` port."""
+        torch = _torch()
+        B = llr.shape[0]
+        if out is None:
+            out = torch.empty((B, self.N // 16), dtype=torch.int16, device=llr.device)
+        s = stream if stream is not None else torch.cuda.current_stream(llr.device)
+        _check("polar_sc_decode_u16", lib().polar_sc_decode_u16(
+            self._plan, ctypes.c_void_p(llr.data_ptr()), ctypes.c_void_p(out.data_ptr()), B,
+            ctypes.c_void_p(s.cuda_stream)))
+        return out
+
+    def decode_host(self, llr):
+        """Host arrays in/out (synchronous): int8 [B, N] -> uint64 [B, ceil(N/64)]."""
+        a = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
+        if a.shape[1] != self.N:
+            raise ValueError("llr must be [B, %d]" % self.N)
+        out = np.zeros((a.shape[0], self.words), dtype=np.uint64)
+        _check("polar_sc_decode_host", lib().polar_sc_decode_host(self._plan, _np_ptr(a), _np_ptr(out), a.shape[0]))
+        return out
+
+    def codeword_to_info(self, xhat):
+        """x^ words [B, ceil(N/64)] (host) -> information bits [B, K] (u^ = x^ F^(x)n)."""
+        x = np.ascontiguousarray(np.atleast_2d(np.asarray(xhat)).view(np.uint64))
+        out = np.zeros((x.shape[0], self.K), dtype=np.uint8)
+        _check("polar_codeword_to_info", lib().polar_codeword_to_info(self._plan, _np_ptr(x), _np_ptr(out), x.shape[0]))
+        return out
+
+
+def selftest_lanes():
+    """Run the DPP row-exchange self-test on the current GPU; returns [4, 64] source lanes."""
+    torch = _torch()
+    buf = torch.zeros(4 * 64, dtype=torch.int32, device="cuda")
+    _check("polar_sc_selftest_lanes", lib().polar_sc_selftest_lanes(ctypes.c_void_p(buf.data_ptr())))
+    return buf.view(4, 64).cpu().numpy()

@@ -1,0 +1,43 @@
+"""Build libpolar_sc.so in-tree with hipcc for gfx950 (no JIT cache, no pip install).
+
+The shared library is the product: HIP kernels (csrc/polar_sc_kernels.hip) + host plan /
+schedule compiler / C ABI (csrc/polar_sc_host.cpp) behind include/polar_sc.h.
+"""
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB = os.path.join(PKG, "lib", "libpolar_sc.so")
+SOURCES = [os.path.join(PKG, "csrc", "polar_sc_kernels.hip"), os.path.join(PKG, "csrc", "polar_sc_host.cpp")]
+HEADERS = [os.path.join(ROOT, "include", "polar_sc.h")]
+ARCH = os.environ.get("POLAR_SC_ARCH", "gfx950")
+
+
+def hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if cand and (os.path.sep not in cand or os.path.exists(cand)):
+            return cand
+    return "hipcc"
+
+
+def needs_build():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(s) > t for s in SOURCES + HEADERS)
+
+
+def build(force=False, verbose=False):
+    """Compile the library if stale; returns its path. Raises on compiler errors."""
+    if not force and not needs_build():
+        return LIB
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    tmp = LIB + ".tmp.%d" % os.getpid()
+    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-I" + os.path.join(ROOT, "include")] + SOURCES + ["-o", tmp]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
+    return LIB

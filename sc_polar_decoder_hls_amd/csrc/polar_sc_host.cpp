@@ -1,0 +1,465 @@
+// polar_sc_host.cpp -- host side of libpolar_sc.so: plan / schedule compiler / table
+// loaders / C ABI (include/polar_sc.h).
+//
+// The reference decoder (SC_MODULE my_module, src/module/my_module.h) walks the polar code
+// tree with an FSM whose sequence of states, sizes and addresses depends only on the
+// frozen-bit table (my_module.h:61-166 classifies 16-bit groups, then every transition is
+// a function of those classes). This file "compiles" that walk once per table into a flat
+// op list (polar_sc_op); the GPU kernel interprets the list with wave-uniform control.
+#include "../../include/polar_sc.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out, const void *ops,
+                                      uint32_t *scratch, int N, long batch, int out_stride,
+                                      int waves_per_block, int wave_dwords, void *stream);
+extern "C" int polar_sc_launch_selftest(uint32_t *out_dev);
+
+namespace {
+
+// node codes of shared/src/library.h:34-40
+constexpr uint32_t NODE_R0 = 0x00, NODE_R1 = 0x0F, NODE_REP = 0x02, NODE_SPC = 0x04, NODE_RN = 0x08;
+
+// largest per-wave LDS footprint kept on chip; above it stages go to HBM scratch
+constexpr uint32_t LDS_WAVE_LIMIT = 80u * 1024u;
+
+struct DevState {
+    void *ops = nullptr;
+    uint32_t *scratch = nullptr;
+    size_t scratch_bytes = 0;
+};
+
+}  // namespace
+
+struct polar_sc_plan {
+    uint32_t N = 0, G = 0, K = 0;
+    polar_sc_config cfg{};
+    std::vector<uint8_t> mask;       // N, 1 = information
+    std::vector<uint16_t> fb;        // G, Bit_Frozen (bit k = mask[16g+k])
+    std::vector<uint8_t> type;       // G, Node_Type
+    std::vector<polar_sc_op> ops;
+    polar_sc_plan_stats stats{};
+    int gmem = 0;
+    int wave_dwords = 0;             // per-wave storage, dwords (stage slots + bit dwords) * 64
+    int waves_per_block = 1;
+    mutable std::mutex mu;
+    mutable std::map<int, DevState> dev;
+};
+
+namespace {
+
+// do_prunning (my_module.h:75-155): group class, priority R0 > R1 > REP > SPC > RN
+uint32_t classify_group(uint32_t fb)
+{
+    if (fb == 0u) return NODE_R0;
+    if (fb == 0xFFFFu) return NODE_R1;
+    if (fb == 0x8000u) return NODE_REP;
+    if (fb == 0xFFFEu) return NODE_SPC;
+    return NODE_RN;
+}
+
+// Node class of a multi-group node as aggregated in the F/G loops
+// (my_module.h:403-471, 739-806): all R0 -> R0; all R1 -> R1; all R0 but a REP last group
+// -> REP; an SPC first group then all R1 -> SPC; otherwise RN.
+uint32_t node_class(const polar_sc_plan &p, uint32_t g0, uint32_t cnt)
+{
+    uint32_t R0 = 0, R1 = 0x0F;
+    bool r0_but_last = true, r1_but_first = true;
+    for (uint32_t t = 0; t < cnt; t++) {
+        uint32_t T = p.type[g0 + t];
+        R0 |= T;
+        R1 &= T;
+        if (t + 1 < cnt && T != NODE_R0) r0_but_last = false;
+        if (t > 0 && T != NODE_R1) r1_but_first = false;
+    }
+    if (R0 == NODE_R0) return NODE_R0;
+    if (R1 == NODE_R1) return NODE_R1;
+    if (r0_but_last && p.type[g0 + cnt - 1] == NODE_REP) return NODE_REP;
+    if (r1_but_first && p.type[g0] == NODE_SPC) return NODE_SPC;
+    return NODE_RN;
+}
+
+void emit(polar_sc_plan &p, int code, int level, int n, int pos, int upos, uint32_t fb)
+{
+    polar_sc_op o{};
+    o.code = code;
+    o.level = level;
+    o.n = n;
+    o.pos = pos;
+    o.upos = upos;
+    o.fb = fb;
+    p.ops.push_back(o);
+}
+
+// Decode the children of the node at `level` covering groups [g0, g0+cnt) (cnt >= 2) whose
+// LLR words are in stage buffer `level`. Mirrors the F/G/R/H/H0/F_REP/G_R1/G_SPC
+// transitions of my_module::do_action:
+//  * left child R0  -> "H0 route" (my_module.h:481-507): no F, G with sa = 0, then H0
+//  * left child REP -> F_REP_STATE (my_module.h:1292-1390)
+//  * right child R1 -> G_R1_STATE, SPC -> G_SPC_STATE (selected from the node-type stack,
+//    my_module.h:614-664, 939-997)
+//  * the root's children are never pruned: INIT pushes (RN,RN) (my_module.h:328)
+void compile_node(polar_sc_plan &p, int level, uint32_t g0, uint32_t cnt, bool is_root)
+{
+    const uint32_t h = cnt / 2;
+    const uint32_t tl = is_root ? NODE_RN : node_class(p, g0, h);
+    const uint32_t tr = is_root ? NODE_RN : node_class(p, g0 + h, h);
+    bool left_zero = false;
+    if (tl == NODE_R0) {
+        left_zero = true;
+    } else if (tl == NODE_REP) {
+        emit(p, POLAR_OP_REP, level, (int)h, (int)g0, -1, 0);
+    } else if (h == 1) {
+        emit(p, POLAR_OP_FLEAF, level, 1, (int)g0, -1, p.fb[g0]);
+    } else {
+        emit(p, POLAR_OP_F, level, (int)h, (int)g0, -1, 0);
+        compile_node(p, level + 1, g0, h, false);
+    }
+    const int upos = left_zero ? -1 : (int)g0;
+    if (tr == NODE_R1) {
+        emit(p, POLAR_OP_R1, level, (int)h, (int)(g0 + h), upos, 0);
+    } else if (tr == NODE_SPC) {
+        emit(p, POLAR_OP_SPC, level, (int)h, (int)(g0 + h), upos, 0);
+    } else if (h == 1) {
+        emit(p, POLAR_OP_GLEAF, level, 1, (int)(g0 + h), upos, p.fb[g0 + h]);
+    } else {
+        emit(p, POLAR_OP_G, level, (int)h, (int)(g0 + h), upos, 0);
+        compile_node(p, level + 1, g0 + h, h, false);
+    }
+    emit(p, left_zero ? POLAR_OP_H0 : POLAR_OP_H, level, (int)h, (int)g0, -1, 0);
+}
+
+bool config_supported(const polar_sc_config &c)
+{
+    polar_sc_config d;
+    polar_sc_default_config(&d);
+    return c.llr_bits == d.llr_bits && c.par == d.par && c.sigmag == d.sigmag &&
+           c.extended == d.extended && c.pruning_level == d.pruning_level &&
+           c.elag_r1 == d.elag_r1 && c.elag_rep == d.elag_rep && c.elag_spc == d.elag_spc &&
+           c.elag_rep2 == d.elag_rep2 && c.elag_spc2 == d.elag_spc2 &&
+           c.elag_rare == d.elag_rare && c.elag_h0 == d.elag_h0 &&
+           (c.strict_llr == 0 || c.strict_llr == 1);
+}
+
+int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
+
+// device state for the current device: schedule upload (+ scratch for `batch` frames)
+int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -EIO;
+    std::lock_guard<std::mutex> lk(p->mu);
+    DevState &st = p->dev[dev];
+    if (!st.ops) {
+        size_t bytes = p->ops.size() * sizeof(polar_sc_op);
+        if (hipMalloc(&st.ops, bytes) != hipSuccess) return -ENOMEM;
+        if (hipMemcpy(st.ops, p->ops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+    }
+    if (p->gmem) {
+        size_t waves = (batch + 7) / 8;
+        size_t need = waves * (size_t)p->wave_dwords * 4u;
+        if (need > st.scratch_bytes) {
+            if (st.scratch) {
+                if (hipDeviceSynchronize() != hipSuccess) return -EIO;
+                (void)hipFree(st.scratch);
+                st.scratch = nullptr;
+                st.scratch_bytes = 0;
+            }
+            if (hipMalloc((void **)&st.scratch, need) != hipSuccess) return -ENOMEM;
+            st.scratch_bytes = need;
+        }
+    }
+    *out = &st;
+    return 0;
+}
+
+int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size_t batch,
+                  int out_stride, void *stream)
+{
+    if (!p || (batch > 0 && (!llr || !out))) return -EINVAL;
+    if (batch == 0) return 0;
+    if (batch > (size_t)0x7FFFFFF8) return -EINVAL;
+    DevState *st = nullptr;
+    int rc = ensure_device(p, batch, &st);
+    if (rc) return rc;
+    rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, st->scratch, (int)p->N, (long)batch,
+                                out_stride, p->waves_per_block, p->wave_dwords, stream);
+    return rc ? -EIO : 0;
+}
+
+bool read_text(const char *path, std::string &s)
+{
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    std::stringstream ss;
+    ss << f.rdbuf();
+    s = ss.str();
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int polar_sc_abi_version(void) { return POLAR_SC_ABI_VERSION; }
+
+const char *polar_sc_strerror(int err)
+{
+    switch (err) {
+    case 0: return "success";
+    case -EINVAL: return "invalid argument";
+    case -ENOMEM: return "out of memory";
+    case -ENOTSUP: return "configuration not supported (only the reference config.h)";
+    case -ENOENT: return "file not found";
+    case -EIO: return "HIP runtime error";
+    default: return "unknown error";
+    }
+}
+
+int polar_sc_default_config(polar_sc_config *cfg)
+{
+    if (!cfg) return -EINVAL;
+    cfg->llr_bits = 6;
+    cfg->par = 16;
+    cfg->sigmag = 1;
+    cfg->extended = 1;
+    cfg->pruning_level = 2;
+    cfg->elag_r1 = 1;
+    cfg->elag_rep = 1;
+    cfg->elag_spc = 1;
+    cfg->elag_rep2 = 0;
+    cfg->elag_spc2 = 0;
+    cfg->elag_rare = 0;
+    cfg->elag_h0 = 1;
+    cfg->strict_llr = 0;
+    return 0;
+}
+
+int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_mask,
+                         const polar_sc_config *cfg)
+{
+    if (!out || !info_mask) return -EINVAL;
+    *out = nullptr;
+    if (N < 32 || N > (1u << 20) || (N & (N - 1)) != 0) return -EINVAL;
+    polar_sc_config c;
+    if (cfg) c = *cfg; else polar_sc_default_config(&c);
+    if (!config_supported(c)) return -ENOTSUP;
+
+    polar_sc_plan *p = new (std::nothrow) polar_sc_plan();
+    if (!p) return -ENOMEM;
+    p->N = N;
+    p->G = N / POLAR_SC_PAR;
+    p->cfg = c;
+    p->mask.resize(N);
+    p->fb.resize(p->G);
+    p->type.resize(p->G);
+    for (uint32_t i = 0; i < N; i++) {
+        p->mask[i] = info_mask[i] ? 1 : 0;
+        p->K += p->mask[i];
+    }
+    polar_sc_plan_stats &s = p->stats;
+    for (uint32_t g = 0; g < p->G; g++) {
+        uint32_t t = 0;
+        for (uint32_t k = 0; k < POLAR_SC_PAR; k++) t |= (uint32_t)p->mask[g * 16 + k] << k;
+        p->fb[g] = (uint16_t)t;
+        p->type[g] = (uint8_t)classify_group(t);
+        switch (p->type[g]) {
+        case NODE_R0: s.n_r0++; break;
+        case NODE_R1: s.n_r1++; break;
+        case NODE_REP: s.n_rep++; break;
+        case NODE_SPC: s.n_spc++; break;
+        default: s.n_rn++; break;
+        }
+    }
+    compile_node(*p, 0, 0, p->G, true);
+    emit(*p, POLAR_OP_END, 0, 0, 0, -1, 0);
+
+    s.N = N;
+    s.K = p->K;
+    s.groups = p->G;
+    s.n_ops = (uint32_t)p->ops.size();
+    for (const polar_sc_op &o : p->ops) {
+        s.op_count[o.code & 15]++;
+        if (o.code <= POLAR_OP_SPC) s.word_ops += (uint64_t)o.n;
+    }
+    const uint32_t nslot = p->G - 1, nbd = (p->G + 15) / 16;
+    p->wave_dwords = (int)((nslot + nbd) * 64u);
+    const uint64_t wave_bytes = (uint64_t)p->wave_dwords * 4u;
+    p->gmem = wave_bytes > LDS_WAVE_LIMIT ? 1 : 0;
+    p->waves_per_block = 1;
+    s.storage = (uint32_t)p->gmem;
+    s.lds_bytes_per_wave = p->gmem ? 0u : (uint32_t)wave_bytes;
+    s.scratch_bytes_per_wave = p->gmem ? wave_bytes : 0u;
+    *out = p;
+    return 0;
+}
+
+int polar_sc_plan_destroy(polar_sc_plan *p)
+{
+    if (!p) return -EINVAL;
+    int cur = 0;
+    bool have_dev = hipGetDevice(&cur) == hipSuccess;
+    for (auto &kv : p->dev) {
+        if (have_dev) (void)hipSetDevice(kv.first);
+        if (kv.second.ops) (void)hipFree(kv.second.ops);
+        if (kv.second.scratch) (void)hipFree(kv.second.scratch);
+    }
+    if (have_dev && !p->dev.empty()) (void)hipSetDevice(cur);
+    delete p;
+    return 0;
+}
+
+int polar_sc_plan_prepare(const polar_sc_plan *p, size_t max_batch)
+{
+    if (!p) return -EINVAL;
+    DevState *st = nullptr;
+    return ensure_device(p, max_batch ? max_batch : 1, &st);
+}
+
+int polar_sc_decode(const polar_sc_plan *p, const int8_t *llr_dev, uint64_t *hard_bits_dev,
+                    size_t batch, void *stream)
+{
+    if (!p) return -EINVAL;
+    const int stride16 = (int)(4 * ((p->G + 3) / 4));
+    return decode_common(p, llr_dev, (uint16_t *)hard_bits_dev, batch, stride16, stream);
+}
+
+int polar_sc_decode_u16(const polar_sc_plan *p, const int8_t *llr_dev, uint16_t *bits_dev,
+                        size_t batch, void *stream)
+{
+    if (!p) return -EINVAL;
+    return decode_common(p, llr_dev, bits_dev, batch, (int)p->G, stream);
+}
+
+int polar_sc_decode_host(const polar_sc_plan *p, const int8_t *llr, uint64_t *hard_bits, size_t batch)
+{
+    if (!p || (batch > 0 && (!llr || !hard_bits))) return -EINVAL;
+    if (batch == 0) return 0;
+    if (p->cfg.strict_llr) {
+        const size_t total = batch * (size_t)p->N;
+        for (size_t i = 0; i < total; i++)
+            if (llr[i] > 31 || llr[i] < -31) return -EINVAL;
+    }
+    const size_t words = (p->N + 63) / 64;
+    const size_t in_bytes = batch * (size_t)p->N, out_bytes = batch * words * 8u;
+    int8_t *d_llr = nullptr;
+    uint64_t *d_out = nullptr;
+    int rc = 0;
+    if (hipMalloc((void **)&d_llr, in_bytes) != hipSuccess) return -ENOMEM;
+    if (hipMalloc((void **)&d_out, out_bytes) != hipSuccess) { (void)hipFree(d_llr); return -ENOMEM; }
+    rc = hip_err(hipMemcpy(d_llr, llr, in_bytes, hipMemcpyHostToDevice));
+    if (!rc) rc = polar_sc_decode(p, d_llr, d_out, batch, nullptr);
+    if (!rc) rc = hip_err(hipDeviceSynchronize());
+    if (!rc) rc = hip_err(hipMemcpy(hard_bits, d_out, out_bytes, hipMemcpyDeviceToHost));
+    (void)hipFree(d_llr);
+    (void)hipFree(d_out);
+    return rc;
+}
+
+int polar_load_frozen_tab(const char *path, uint32_t N, uint32_t K, uint8_t *mask_out, uint32_t cap,
+                          uint32_t *N_out)
+{
+    if (!path || !mask_out) return -EINVAL;
+    std::string txt;
+    if (!read_text(path, txt)) return -ENOENT;
+    std::istringstream in(txt);
+    std::string l1, l2, l3, l4;
+    if (!std::getline(in, l1) || !std::getline(in, l2) || !std::getline(in, l3) || !std::getline(in, l4))
+        return -EINVAL;
+    long tabN = std::strtol(l1.c_str(), nullptr, 10);
+    if (tabN <= 0) return -EINVAL;
+    if (N == 0) N = (uint32_t)tabN;
+    if (N > cap || K > N) return -EINVAL;
+    std::istringstream ch(l4);
+    std::vector<uint32_t> order;
+    long v;
+    while (ch >> v) {
+        if (v >= 0 && (uint32_t)v < N) order.push_back((uint32_t)v);   // Writer.h:61-69
+    }
+    if (order.size() < K) return -EINVAL;
+    std::vector<uint8_t> seen(N, 0);
+    for (uint32_t i = 0; i < N; i++) mask_out[i] = 0;
+    for (uint32_t i = 0; i < K; i++) {
+        if (seen[order[i]]) return -EINVAL;
+        seen[order[i]] = 1;
+        mask_out[order[i]] = 1;                                          // Writer.h:84-86
+    }
+    if (N_out) *N_out = N;
+    return 0;
+}
+
+int polar_load_mask_file(const char *path, uint8_t *mask_out, uint32_t cap, uint32_t *N_out)
+{
+    if (!path || !mask_out) return -EINVAL;
+    std::string txt;
+    if (!read_text(path, txt)) return -ENOENT;
+    uint32_t n = 0;
+    for (char ch : txt) {
+        if (ch == '0' || ch == '1') {
+            if (n >= cap) return -EINVAL;
+            mask_out[n++] = (uint8_t)(ch - '0');
+        } else if (!(ch == ' ' || ch == '\t' || ch == '\r' || ch == '\n')) {
+            return -EINVAL;
+        }
+    }
+    if (n == 0) return -EINVAL;
+    if (N_out) *N_out = n;
+    return 0;
+}
+
+int polar_codeword_to_info(const polar_sc_plan *p, const uint64_t *xhat, uint8_t *info_out, size_t batch)
+{
+    if (!p || (batch > 0 && (!xhat || !info_out))) return -EINVAL;
+    const uint32_t N = p->N;
+    const size_t words = (N + 63) / 64;
+    std::vector<uint8_t> v(N);
+    for (size_t f = 0; f < batch; f++) {
+        const uint64_t *x = xhat + f * words;
+        for (uint32_t i = 0; i < N; i++) v[i] = (uint8_t)((x[i >> 6] >> (i & 63)) & 1u);
+        for (uint32_t h = 1; h < N; h <<= 1)           // u = x F^{(x)n}
+            for (uint32_t b = 0; b < N; b += 2 * h)
+                for (uint32_t j = b; j < b + h; j++) v[j] ^= v[j + h];
+        uint8_t *o = info_out + f * p->K;
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < N; i++)
+            if (p->mask[i]) o[k++] = v[i];
+    }
+    return 0;
+}
+
+int polar_sc_plan_get_stats(const polar_sc_plan *p, polar_sc_plan_stats *s)
+{
+    if (!p || !s) return -EINVAL;
+    *s = p->stats;
+    return 0;
+}
+
+int polar_sc_plan_get_schedule(const polar_sc_plan *p, polar_sc_op *ops, uint32_t cap, uint32_t *count)
+{
+    if (!p || !count) return -EINVAL;
+    *count = (uint32_t)p->ops.size();
+    if (ops) {
+        uint32_t n = cap < *count ? cap : *count;
+        std::memcpy(ops, p->ops.data(), n * sizeof(polar_sc_op));
+    }
+    return 0;
+}
+
+int polar_sc_selftest_lanes(uint32_t *out_dev)
+{
+    if (!out_dev) return -EINVAL;
+    return polar_sc_launch_selftest(out_dev) ? -EIO : 0;
+}
+
+}  // extern "C"

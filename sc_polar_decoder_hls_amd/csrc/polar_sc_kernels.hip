@@ -1,0 +1,573 @@
+// polar_sc_kernels.hip -- CDNA4 (gfx950) batched SC polar decoder kernels.
+//
+// Execution model:
+//   * One wave64 decodes 8 frames. The wave is 4 DPP rows of 16 lanes; lane `pl` of row `r`
+//     owns PAR-lane `pl` (LLR 16w+pl of every word w) of frames f0+r (low 16-bit half of
+//     every register) and f0+4+r (high half). PAR = 16 of the reference (my_module.h works
+//     on one 16-LLR word per cycle) == one DPP row here, so the F/G/H word loops of
+//     my_module::do_action are lane-private and the only cross-lane traffic is the leaf
+//     (Spec_PolarDec_16), the REP adder tree, the SPC min/parity trees and output packing,
+//     all done with DPP row ops.
+//   * LLRs are sign-magnitude in packed 16-bit halves (bit 15 = sign, bits 0..14 =
+//     magnitude): "SM16". All arithmetic is v_pk_* on two frames at once.
+//   * The control flow of the reference FSM does not depend on LLR values, so the host
+//     compiles it once per frozen mask into a flat op list (polar_sc_host.cpp); the kernel
+//     interprets it with wave-uniform (scalar) control.
+//   * Per wave, stage LLRs of the current tree path live in LDS (slot s, lane L at dword
+//     s*64+L: conflict-free ds_read_b32) or, for large N, in an HBM scratch area with the
+//     same layout (one 256-byte coalesced access per wave per slot). Partial sums
+//     (bit_mem_1 of the reference) are per lane: dword d holds words 16d..16d+15, low 16
+//     bits = low-half frame, high 16 bits = high-half frame.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace polar {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+constexpr uint32_t SGN = 0x80008000u;   // sign flags of both halves
+constexpr uint32_t MAG = 0x7FFF7FFFu;   // magnitudes of both halves
+
+enum : int {
+    OP_F = 1, OP_G = 2, OP_FLEAF = 3, OP_GLEAF = 4, OP_REP = 5, OP_R1 = 6, OP_SPC = 7,
+    OP_H = 8, OP_H0 = 9, OP_END = 10
+};
+
+struct Op {            // == polar_sc_op (include/polar_sc.h)
+    int32_t code, level, n, pos, upos;
+    uint32_t fb;
+    int32_t r0, r1;
+};
+
+// ---------------------------------------------------------------------------------------
+// packed 16-bit helpers
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t U(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ u16x2 V(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) { return U(__builtin_elementwise_min(V(a), V(b))); }
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return U(V(a) + V(b)); }
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) { return U(V(a) - V(b)); }
+__device__ __forceinline__ uint32_t pk_sra15(uint32_t a)
+{
+    i16x2 x = __builtin_bit_cast(i16x2, a);
+    x = x >> (short)15;
+    return __builtin_bit_cast(uint32_t, x);
+}
+__device__ __forceinline__ uint32_t pk_abs_i16(uint32_t a)
+{
+    i16x2 x = __builtin_bit_cast(i16x2, a);
+    i16x2 y = -x;
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
+}
+// bitwise select: m ? a : b
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+
+// F_function_SM (shared/src/functions.h:124-145): sign xor, magnitude min, no saturation.
+__device__ __forceinline__ uint32_t F_sm(uint32_t a, uint32_t b)
+{
+    return pk_min(a & MAG, b & MAG) | ((a ^ b) & SGN);
+}
+
+// qfull_add_sub_sm (shared/src/scalar.h:196-225) on SM16, followed by an optional clamp:
+//   a' = a with sign ^ u; same signs -> |a|+|b|, else ||a|-|b||;
+//   sign = |a| < |b| ? sign(b) : sign(a')      (ties -> sign(a'), may produce -0)
+// SAT = 15 : G_function_SM, VECTOR_SAT_SM<P,Q-1> clamp (functions.h:186-194, scalar.h:94-99)
+// SAT = 511: qfull_adder_sat_sm<11> of the REP accumulator (scalar.h:164-194)
+// SAT = 0  : G_extended_SM / qfull_adder_sm (exact; leaves and the REP pair tree)
+// u holds sign-flip flags at bit positions 15/31 only.
+template <int SAT>
+__device__ __forceinline__ uint32_t G_sm(uint32_t a, uint32_t b, uint32_t u)
+{
+    uint32_t a2 = a ^ u;
+    uint32_t ma = a & MAG, mb = b & MAG;
+    uint32_t d = pk_sub(ma, mb);              // bit 15 set iff |a| < |b|
+    uint32_t sum = pk_add(ma, mb);
+    uint32_t dif = pk_abs_i16(d);
+    uint32_t dm = pk_sra15(a2 ^ b);           // 0xFFFF where signs differ
+    uint32_t m = bsel(dm, dif, sum);
+    if constexpr (SAT != 0) m = pk_min(m, (uint32_t)SAT * 0x00010001u);
+    uint32_t s = bsel(d, b, a2) & SGN;        // only bits 15/31 of the selector matter
+    return s | m;
+}
+
+// ---------------------------------------------------------------------------------------
+// cross-lane exchange inside a 16-lane DPP row: value of lane (l ^ H)
+// ---------------------------------------------------------------------------------------
+template <int H>
+__device__ __forceinline__ uint32_t xorlane(uint32_t v)
+{
+    if constexpr (H == 1) {
+        return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    } else if constexpr (H == 2) {
+        return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    } else if constexpr (H == 4) {
+        uint32_t t = __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);  // row_half_mirror: l^7
+        return __builtin_amdgcn_mov_dpp(t, 0x1B, 0xF, 0xF, false);        // quad_perm [3,2,1,0]: ^3
+    } else {
+        static_assert(H == 8, "row partner distance");
+        return __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    }
+}
+
+// per-lane constants: all-ones where the lane is the lower ("a") member of its pair at
+// distance H
+struct Lanes {
+    uint32_t a1, a2, a4, a8;   // lane masks
+    uint32_t pl;               // PAR lane 0..15
+    uint32_t br;               // bitrev4(pl)
+    template <int H> __device__ __forceinline__ uint32_t amask() const
+    {
+        if constexpr (H == 1) return a1;
+        else if constexpr (H == 2) return a2;
+        else if constexpr (H == 4) return a4;
+        else return a8;
+    }
+};
+
+// ---------------------------------------------------------------------------------------
+// Leaf: Spec_PolarDec_16 -> Spec_P16_ext<6> (functions.h:521-546, 413-492, 366-384):
+// exact SC over the 16 LLRs of one word, F (min) + G_extended (exact, width grows).
+// Executed by all 16 lanes of each row (4 rows x 2 halves = 8 frames at once).
+// Returns x (the 16 encoded bits) as sign-position flags per lane.
+// Blocks whose frozen pattern is all-frozen return 0; all-information blocks return the
+// hard decisions of their LLRs, which is what the recursion computes for them
+// (induction on G with u = x_a: sign(a') = sign(b)).
+// ---------------------------------------------------------------------------------------
+template <int B, int W>
+__device__ __forceinline__ uint32_t leaf_rec(uint32_t L, uint32_t fb, uint32_t fbm, const Lanes &ln)
+{
+    constexpr uint32_t bm = ((1u << W) - 1u) << B;
+    const uint32_t sub = fb & bm;
+    if (sub == 0u) return 0u;
+    if (sub == bm) return L & SGN;
+    if constexpr (W == 2) {
+        // Spec_P2 (functions.h:366-384): lane B = a, lane B+1 = b
+        uint32_t P = xorlane<1>(L);
+        uint32_t u0 = (L ^ P) & fbm;                   // F_simplified & fb[B]   (valid on a)
+        uint32_t u0p = xorlane<1>(u0);
+        uint32_t d = pk_sub(P & MAG, L & MAG);         // |a| < |b|              (on b)
+        uint32_t u1 = bsel(d, L, P ^ u0p) & fbm;       // G_simplified & fb[B+1] (valid on b)
+        uint32_t u1p = xorlane<1>(u1);
+        return bsel(ln.a1, u0 ^ u1p, u1);
+    } else {
+        constexpr int H = W / 2;
+        uint32_t P = xorlane<H>(L);
+        uint32_t La = F_sm(L, P);                             // valid on a-lanes
+        uint32_t xa = leaf_rec<B, H>(La, fb, fbm, ln);
+        uint32_t Lb = G_sm<0>(P, L, xorlane<H>(xa));          // valid on b-lanes
+        uint32_t xb = leaf_rec<B + H, H>(Lb, fb, fbm, ln);
+        return bsel(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
+    }
+}
+
+__device__ __forceinline__ uint32_t leaf16(uint32_t L, uint32_t fb, const Lanes &ln)
+{
+    uint32_t fbm = ((fb >> ln.pl) & 1u) ? SGN : 0u;
+    return leaf_rec<0, 16>(L, fb, fbm, ln);
+}
+
+// ---------------------------------------------------------------------------------------
+// Row reductions
+// ---------------------------------------------------------------------------------------
+// ADD_TREE_16_SM (functions.h:3036-3083): pair (j, j+8), then (j, j+4) ... with the lower
+// lane as operand a. Butterfly form: both partners compute combine(lower, upper), so every
+// lane ends with the row total (same pairing and operand order as the reference tree).
+__device__ __forceinline__ uint32_t row_add_tree(uint32_t v, const Lanes &ln)
+{
+    uint32_t p;
+    p = xorlane<8>(v); v = G_sm<0>(bsel(ln.a8, v, p), bsel(ln.a8, p, v), 0u);
+    p = xorlane<4>(v); v = G_sm<0>(bsel(ln.a4, v, p), bsel(ln.a4, p, v), 0u);
+    p = xorlane<2>(v); v = G_sm<0>(bsel(ln.a2, v, p), bsel(ln.a2, p, v), 0u);
+    p = xorlane<1>(v); v = G_sm<0>(bsel(ln.a1, v, p), bsel(ln.a1, p, v), 0u);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v)
+{
+    v = min(v, xorlane<8>(v));
+    v = min(v, xorlane<4>(v));
+    v = min(v, xorlane<2>(v));
+    v = min(v, xorlane<1>(v));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t row_xor(uint32_t v)
+{
+    v ^= xorlane<8>(v);
+    v ^= xorlane<4>(v);
+    v ^= xorlane<2>(v);
+    v ^= xorlane<1>(v);
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// Channel LLR -> SM16: wrapper_in + Adapt_format/qconv_format (wrapper_in.h:34,
+// library.h:18-28, scalar.h:229-239). The LLR is the low 6 bits (sc_bigint<6>); -32 -> +0.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t conv_half(int c)
+{
+    int t = (int)((uint32_t)c << 26) >> 26;      // sign-extend 6 bits
+    uint32_t m = (uint32_t)(t < 0 ? -t : t) & 31u;
+    uint32_t s = (t < 0 && m != 0u) ? 0x8000u : 0u;
+    return m | s;
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-wave storage: LDS (small N) or HBM scratch (large N). `base` already includes the
+// lane offset; slot / bit-dword indices are wave-uniform.
+// ---------------------------------------------------------------------------------------
+struct Ctx {
+    uint32_t *base;        // stage slots [0, nslot), then bits dwords
+    uint32_t nslot;        // G - 1
+    int G;
+    const int8_t *llr_lo, *llr_hi;   // frame rows (lane offset included)
+    Lanes ln;
+    __device__ __forceinline__ uint32_t ld(int slot) const { return base[slot * 64]; }
+    __device__ __forceinline__ void st(int slot, uint32_t v) const { base[slot * 64] = v; }
+    __device__ __forceinline__ uint32_t bld(int d) const { return base[(nslot + d) * 64]; }
+    __device__ __forceinline__ void bst(int d, uint32_t v) const { base[(nslot + d) * 64] = v; }
+    __device__ __forceinline__ int lvl_off(int k) const { return G - (G >> (k - 1)); }  // k >= 1
+    __device__ __forceinline__ uint32_t chan(int w) const
+    {
+        int lo = llr_lo[16 * w];
+        int hi = llr_hi[16 * w];
+        return conv_half(lo) | (conv_half(hi) << 16);
+    }
+    // source word i of a level-k node (k = 0: channel)
+    __device__ __forceinline__ uint32_t src(int k, int i) const
+    {
+        return (k == 0) ? chan(i) : ld(lvl_off(k) + i);
+    }
+};
+
+// partial-sum flags (bits 15/31) of bit_mem word q
+__device__ __forceinline__ uint32_t ubit(uint32_t dword, int q) { return (dword << (15 - (q & 15))) & SGN; }
+
+// write n (< 16, aligned) words of hard-decision flags packed in `acc` (bit j = word pos+j)
+__device__ __forceinline__ void bits_put_small(const Ctx &c, int pos, int n, uint32_t acc)
+{
+    uint32_t mlo = ((1u << n) - 1u) << (pos & 15);
+    uint32_t m = mlo | (mlo << 16);
+    uint32_t d = c.bld(pos >> 4);
+    c.bst(pos >> 4, (d & ~m) | (acc & m));
+}
+
+// ---------------------------------------------------------------------------------------
+// Ops
+// ---------------------------------------------------------------------------------------
+// F_STATE / G_STATE word loops (my_module.h:373-445, 704-781) for n >= 2 output words:
+// dst[i] = F(src[i], src[n+i]) or G(src[i], src[n+i], bit_mem[upos+i]).
+template <bool ISG>
+__device__ __forceinline__ void op_fg(const Ctx &c, int k, int n, int upos)
+{
+    const int dst = c.lvl_off(k + 1);
+    uint32_t ud = 0;
+    if (k == 0) {
+        for (int i = 0; i < n; i++) {
+            uint32_t a = c.chan(i), b = c.chan(n + i);
+            uint32_t r;
+            if constexpr (ISG) {
+                uint32_t u = 0;
+                if (upos >= 0) {
+                    if (((upos + i) & 15) == 0 || i == 0) ud = c.bld((upos + i) >> 4);
+                    u = ubit(ud, upos + i);
+                }
+                r = G_sm<15>(a, b, u);
+            } else {
+                r = F_sm(a, b);
+            }
+            c.st(dst + i, r);
+        }
+        return;
+    }
+    const int s0 = c.lvl_off(k);
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {
+        uint32_t a0 = c.ld(s0 + i), a1 = c.ld(s0 + i + 1), a2 = c.ld(s0 + i + 2), a3 = c.ld(s0 + i + 3);
+        uint32_t b0 = c.ld(s0 + n + i), b1 = c.ld(s0 + n + i + 1), b2 = c.ld(s0 + n + i + 2), b3 = c.ld(s0 + n + i + 3);
+        uint32_t r0, r1, r2, r3;
+        if constexpr (ISG) {
+            uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
+            if (upos >= 0) {
+                if (((upos + i) & 15) == 0 || i == 0) ud = c.bld((upos + i) >> 4);
+                u0 = ubit(ud, upos + i); u1 = ubit(ud, upos + i + 1);
+                u2 = ubit(ud, upos + i + 2); u3 = ubit(ud, upos + i + 3);
+            }
+            r0 = G_sm<15>(a0, b0, u0); r1 = G_sm<15>(a1, b1, u1);
+            r2 = G_sm<15>(a2, b2, u2); r3 = G_sm<15>(a3, b3, u3);
+        } else {
+            r0 = F_sm(a0, b0); r1 = F_sm(a1, b1); r2 = F_sm(a2, b2); r3 = F_sm(a3, b3);
+        }
+        c.st(dst + i, r0); c.st(dst + i + 1, r1); c.st(dst + i + 2, r2); c.st(dst + i + 3, r3);
+    }
+    for (; i < n; i++) {
+        uint32_t a = c.ld(s0 + i), b = c.ld(s0 + n + i);
+        uint32_t r;
+        if constexpr (ISG) {
+            uint32_t u = 0;
+            if (upos >= 0) {
+                if (((upos + i) & 15) == 0 || i == 0) ud = c.bld((upos + i) >> 4);
+                u = ubit(ud, upos + i);
+            }
+            r = G_sm<15>(a, b, u);
+        } else {
+            r = F_sm(a, b);
+        }
+        c.st(dst + i, r);
+    }
+}
+
+// F/G with NB_ITER = 1 followed by R_STATE: Spec_Polar_Decoder on reg_result
+// (my_module.h:544-612)
+template <bool ISG>
+__device__ __forceinline__ void op_leaf(const Ctx &c, int k, int pos, int upos, uint32_t fb)
+{
+    uint32_t a = c.src(k, 0), b = c.src(k, 1);
+    uint32_t L;
+    if constexpr (ISG) {
+        uint32_t u = (upos >= 0) ? ubit(c.bld(upos >> 4), upos) : 0u;
+        L = G_sm<15>(a, b, u);
+    } else {
+        L = F_sm(a, b);
+    }
+    uint32_t x = leaf16(L, fb, c.ln);
+    int b4 = pos & 15;
+    uint32_t m = 0x10001u << b4;
+    uint32_t d = c.bld(pos >> 4);
+    c.bst(pos >> 4, (d & ~m) | (x >> (15 - b4)));
+}
+
+// F_REP_STATE (my_module.h:1292-1390): lambda = F(parent); per word the 16-lane exact SM
+// adder tree, accumulated over words in order by the 11-bit saturating SM adder
+// (ADDER_TREE_16, functions.h:3190-3205); x = all sign(acc).
+__device__ __forceinline__ void op_rep(const Ctx &c, int k, int n, int pos)
+{
+    const int s0 = c.lvl_off(k);
+    uint32_t acc = 0;
+    for (int i = 0; i < n; i++) {
+        uint32_t lam = F_sm(c.ld(s0 + i), c.ld(s0 + n + i));
+        uint32_t t = row_add_tree(lam, c.ln);
+        acc = G_sm<511>(t, acc, 0u);
+    }
+    uint32_t dflags = acc & SGN;
+    uint32_t full = ((dflags & 0x8000u) ? 0x0000FFFFu : 0u) | ((dflags & 0x80000000u) ? 0xFFFF0000u : 0u);
+    if (n >= 16) {
+        for (int j = 0; j < n / 16; j++) c.bst((pos >> 4) + j, full);
+    } else {
+        bits_put_small(c, pos, n, full);
+    }
+}
+
+// G_R1_STATE (my_module.h:1571-1642) and G_SPC_STATE (my_module.h:1737-1842):
+// lambda = G(parent, bits[upos..]); x = sign(lambda); SPC additionally flips the first
+// minimum-|lambda| position (lexicographic (|l|, word, bitrev4(lane)) == Min_Mask_16_SM
+// tournament + strict '<' across words) when the parity of x is odd.
+template <bool SPC>
+__device__ __forceinline__ void op_r1spc(const Ctx &c, int k, int n, int upos, int pos)
+{
+    const int s0 = c.lvl_off(k);
+    uint32_t ud = 0, acc = 0, par = 0;
+    uint32_t key_lo = 0xFFFFFFFFu, key_hi = 0xFFFFFFFFu;
+    for (int i = 0; i < n; i++) {
+        uint32_t u = 0;
+        if (upos >= 0) {
+            if (((upos + i) & 15) == 0 || i == 0) ud = c.bld((upos + i) >> 4);
+            u = ubit(ud, upos + i);
+        }
+        uint32_t lam = G_sm<15>(c.ld(s0 + i), c.ld(s0 + n + i), u);
+        uint32_t h = lam & SGN;
+        int q = (pos + i) & 15;
+        acc |= h >> (15 - q);
+        if (n >= 16 && q == 15) { c.bst((pos + i) >> 4, acc); acc = 0; }
+        if constexpr (SPC) {
+            par ^= h;
+            uint32_t klo = ((lam & 0x1Fu) << 24) | ((uint32_t)i << 4);
+            uint32_t khi = (((lam >> 16) & 0x1Fu) << 24) | ((uint32_t)i << 4);
+            key_lo = min(key_lo, klo);
+            key_hi = min(key_hi, khi);
+        }
+    }
+    if (n < 16) bits_put_small(c, pos, n, acc);
+    if constexpr (SPC) {
+        par = row_xor(par);
+        key_lo = row_min_u32(key_lo | c.ln.br);
+        key_hi = row_min_u32(key_hi | c.ln.br);
+        uint32_t flip_lo = ((par & 0x8000u) && (key_lo & 15u) == c.ln.br) ? 1u : 0u;
+        uint32_t flip_hi = ((par & 0x80000000u) && (key_hi & 15u) == c.ln.br) ? 1u : 0u;
+        if (flip_lo) {
+            int w = pos + (int)((key_lo >> 4) & 0xFFFFFu);
+            c.bst(w >> 4, c.bld(w >> 4) ^ (1u << (w & 15)));
+        }
+        if (flip_hi) {
+            int w = pos + (int)((key_hi >> 4) & 0xFFFFFu);
+            c.bst(w >> 4, c.bld(w >> 4) ^ (0x10000u << (w & 15)));
+        }
+    }
+}
+
+// H_STATE / H0_STATE (my_module.h:903-932, 1020-1042):
+// bits[pos..pos+n) = bits[pos..pos+n) ^ bits[pos+n..pos+2n)   (H)
+//                  = bits[pos+n..pos+2n)                      (H0)
+template <bool H0>
+__device__ __forceinline__ void op_h(const Ctx &c, int pos, int n)
+{
+    if (n >= 16) {
+        const int da = pos >> 4, db = (pos + n) >> 4;
+        for (int j = 0; j < n / 16; j++) {
+            uint32_t b = c.bld(db + j);
+            c.bst(da + j, H0 ? b : (c.bld(da + j) ^ b));
+        }
+    } else {
+        uint32_t mlo = ((1u << n) - 1u) << (pos & 15);
+        uint32_t m = mlo | (mlo << 16);
+        uint32_t d = c.bld(pos >> 4);
+        uint32_t sh = (d >> n) & m;
+        c.bst(pos >> 4, H0 ? ((d & ~m) | sh) : (d ^ sh));
+    }
+}
+
+// 16x16 bit transpose inside a row on both 16-bit halves: lane l bit j <- lane j bit l.
+__device__ __forceinline__ uint32_t row_transpose16(uint32_t v, const Lanes &ln)
+{
+    uint32_t p;
+    p = xorlane<8>(v); v = bsel(ln.a8, (v & 0x00FF00FFu) | ((p & 0x00FF00FFu) << 8), ((p >> 8) & 0x00FF00FFu) | (v & 0xFF00FF00u));
+    p = xorlane<4>(v); v = bsel(ln.a4, (v & 0x0F0F0F0Fu) | ((p & 0x0F0F0F0Fu) << 4), ((p >> 4) & 0x0F0F0F0Fu) | (v & 0xF0F0F0F0u));
+    p = xorlane<2>(v); v = bsel(ln.a2, (v & 0x33333333u) | ((p & 0x33333333u) << 2), ((p >> 2) & 0x33333333u) | (v & 0xCCCCCCCCu));
+    p = xorlane<1>(v); v = bsel(ln.a1, (v & 0x55555555u) | ((p & 0x55555555u) << 1), ((p >> 1) & 0x55555555u) | (v & 0xAAAAAAAAu));
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// The decode kernel: one wave = 8 frames; `ops` is the compiled schedule.
+//   llr:  [batch][N] int8;   out: [batch][out_stride] uint16 (bit_mem_1 words, END order)
+// ---------------------------------------------------------------------------------------
+template <bool GMEM>
+__global__ void __launch_bounds__(256) polar_sc_decode_kernel(
+    const int8_t *__restrict__ llr, uint16_t *__restrict__ out, const Op *__restrict__ ops,
+    uint32_t *__restrict__ scratch, int N, int batch, int out_stride, int waves_per_block,
+    int wave_dwords)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    const long wave = (long)blockIdx.x * waves_per_block + wib;
+    const int G = N >> 4;
+    const int row = lane >> 4;
+    const int pl = lane & 15;
+
+    Ctx c;
+    c.G = G;
+    c.nslot = (uint32_t)(G - 1);
+    if constexpr (GMEM) {
+        c.base = scratch + (size_t)wave * (size_t)wave_dwords + lane;
+    } else {
+        c.base = smem + (size_t)wib * (size_t)wave_dwords + lane;
+    }
+    long f_lo = wave * 8 + row, f_hi = wave * 8 + 4 + row;
+    const long f_lo_c = f_lo < batch ? f_lo : (long)batch - 1;
+    const long f_hi_c = f_hi < batch ? f_hi : (long)batch - 1;
+    c.llr_lo = llr + (size_t)f_lo_c * (size_t)N + pl;
+    c.llr_hi = llr + (size_t)f_hi_c * (size_t)N + pl;
+    c.ln.pl = (uint32_t)pl;
+    c.ln.br = (uint32_t)(((pl & 1) << 3) | ((pl & 2) << 1) | ((pl & 4) >> 1) | ((pl & 8) >> 3));
+    c.ln.a1 = (pl & 1) ? 0u : 0xFFFFFFFFu;
+    c.ln.a2 = (pl & 2) ? 0u : 0xFFFFFFFFu;
+    c.ln.a4 = (pl & 4) ? 0u : 0xFFFFFFFFu;
+    c.ln.a8 = (pl & 8) ? 0u : 0xFFFFFFFFu;
+
+    if (wave * 8 >= batch) return;   // whole wave idle (uniform)
+
+    // clear partial-sum memory (H0 may read words the H0 route never wrote)
+    const int nbd = (G + 15) >> 4;
+    for (int d = 0; d < nbd; d++) c.bst(d, 0u);
+
+    for (int oi = 0;; oi++) {
+        const int code = __builtin_amdgcn_readfirstlane(ops[oi].code);
+        if (code == OP_END) break;
+        const int k = __builtin_amdgcn_readfirstlane(ops[oi].level);
+        const int n = __builtin_amdgcn_readfirstlane(ops[oi].n);
+        const int pos = __builtin_amdgcn_readfirstlane(ops[oi].pos);
+        const int upos = __builtin_amdgcn_readfirstlane(ops[oi].upos);
+        const uint32_t fb = (uint32_t)__builtin_amdgcn_readfirstlane((int)ops[oi].fb);
+        switch (code) {
+        case OP_F: op_fg<false>(c, k, n, -1); break;
+        case OP_G: op_fg<true>(c, k, n, upos); break;
+        case OP_FLEAF: op_leaf<false>(c, k, pos, -1, fb); break;
+        case OP_GLEAF: op_leaf<true>(c, k, pos, upos, fb); break;
+        case OP_REP: op_rep(c, k, n, pos); break;
+        case OP_R1: op_r1spc<false>(c, k, n, upos, pos); break;
+        case OP_SPC: op_r1spc<true>(c, k, n, upos, pos); break;
+        case OP_H: op_h<false>(c, pos, n); break;
+        case OP_H0: op_h<true>(c, pos, n); break;
+        default: break;
+        }
+    }
+
+    // END (my_module.h:1848-1869) + wrapper_out: emit bit_mem words in natural order.
+    const bool st_lo = f_lo < batch, st_hi = f_hi < batch;
+    uint16_t *o_lo = out + (size_t)f_lo * (size_t)out_stride;
+    uint16_t *o_hi = out + (size_t)f_hi * (size_t)out_stride;
+    for (int d = 0; d < nbd; d++) {
+        uint32_t t = row_transpose16(c.bld(d), c.ln);   // lane pl: word 16d+pl, lo | hi<<16
+        int w = 16 * d + pl;
+        if (w < G) {
+            if (st_lo) o_lo[w] = (uint16_t)(t & 0xFFFFu);
+            if (st_hi) o_hi[w] = (uint16_t)(t >> 16);
+        }
+    }
+    for (int w = G + pl; w < out_stride; w += 16) {   // pad words (N = 32 with u64 output)
+        if (st_lo) o_lo[w] = 0;
+        if (st_hi) o_hi[w] = 0;
+    }
+}
+
+// DPP exchange self-test: out[h*64 + lane] = lane id seen through xorlane<1<<h>
+__global__ void polar_sc_lane_selftest_kernel(uint32_t *out)
+{
+    uint32_t l = threadIdx.x;
+    out[0 * 64 + l] = xorlane<1>(l);
+    out[1 * 64 + l] = xorlane<2>(l);
+    out[2 * 64 + l] = xorlane<4>(l);
+    out[3 * 64 + l] = xorlane<8>(l);
+}
+
+}  // namespace polar
+
+// ---------------------------------------------------------------------------------------
+// launch glue (called from polar_sc_host.cpp)
+// ---------------------------------------------------------------------------------------
+extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out, const void *ops,
+                                      uint32_t *scratch, int N, long batch, int out_stride,
+                                      int waves_per_block, int wave_dwords, void *stream)
+{
+    const long waves = (batch + 7) / 8;
+    const long blocks = (waves + waves_per_block - 1) / waves_per_block;
+    dim3 grid((unsigned)blocks), block((unsigned)(64 * waves_per_block));
+    hipStream_t s = (hipStream_t)stream;
+    const polar::Op *o = (const polar::Op *)ops;
+    if (gmem) {
+        hipLaunchKernelGGL(polar::polar_sc_decode_kernel<true>, grid, block, 0, s, llr, out, o,
+                           scratch, N, (int)batch, out_stride, waves_per_block, wave_dwords);
+    } else {
+        size_t lds = (size_t)waves_per_block * (size_t)wave_dwords * 4u;
+        if (lds > 65536) {
+            hipError_t ae = hipFuncSetAttribute((const void *)polar::polar_sc_decode_kernel<false>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (ae != hipSuccess) return -(int)ae - 1000;
+        }
+        hipLaunchKernelGGL(polar::polar_sc_decode_kernel<false>, grid, block, lds, s, llr, out, o,
+                           scratch, N, (int)batch, out_stride, waves_per_block, wave_dwords);
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -(int)e - 1000;
+}
+
+extern "C" int polar_sc_launch_selftest(uint32_t *out_dev)
+{
+    hipLaunchKernelGGL(polar::polar_sc_lane_selftest_kernel, dim3(1), dim3(64), 0, 0, out_dev);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return -(int)e - 1000;
+    e = hipDeviceSynchronize();
+    return e == hipSuccess ? 0 : -(int)e - 1000;
+}

@@ -1,0 +1,169 @@
+"""Shared test helpers: fixtures, synthetic frames, and a numpy interpreter of the compiled
+decode schedule (used to validate the host schedule compiler on CPU, independently of the
+GPU kernel and of the C oracle)."""
+import json
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MASKS_JSON = os.path.join(ROOT, "data", "frozen_masks.json")
+KAT_JSON = os.path.join(ROOT, "tests", "golden", "kat_codewords.json")
+
+_masks = None
+
+
+def masks():
+    global _masks
+    if _masks is None:
+        with open(MASKS_JSON) as f:
+            _masks = json.load(f)["masks"]
+    return _masks
+
+
+def mask(name):
+    m = masks()[name]
+    b = np.frombuffer(bytes.fromhex(m["hex"]), dtype=np.uint8)
+    return np.unpackbits(b, bitorder="little")[: m["N"]].astype(np.uint8)
+
+
+def kat():
+    with open(KAT_JSON) as f:
+        return json.load(f)["codewords"]
+
+
+def encode_np(u):
+    """x = u F^{(x)n} (natural order), vectorised over rows."""
+    x = np.array(u, dtype=np.uint8, copy=True)
+    B, N = x.shape
+    h = 1
+    while h < N:
+        v = x.reshape(B, N // (2 * h), 2, h)
+        v[:, :, 0, :] ^= v[:, :, 1, :]
+        h *= 2
+    return x
+
+
+def synth_frames(info_mask, batch, ebn0_db=2.5, seed=0xF0, rate=None):
+    """The reference C-sim chain: random info bits, x = uF, BPSK
+    (bit1 -> -1, sc_bpsk.h:53), AWGN sigma = 1/sqrt(2 R 10^(EbN0/10)) (main.cpp:91-98),
+    llr = clamp(trunc(4 y), -31, 31) (sc_quantizer.h:77-79). Returns (llr int8, x uint8)."""
+    rng = np.random.default_rng(seed)
+    N = info_mask.size
+    R = rate if rate is not None else max(int(info_mask.sum()), 1) / N
+    u = (rng.integers(0, 2, size=(batch, N), dtype=np.uint8) & info_mask[None, :].astype(np.uint8))
+    x = encode_np(u)
+    sigma = 1.0 / np.sqrt(2.0 * R * 10.0 ** (ebn0_db / 10.0))
+    y = np.where(x == 1, -1.0, 1.0).astype(np.float32) + sigma * rng.standard_normal((batch, N), dtype=np.float32)
+    q = np.trunc(4.0 * y)
+    llr = np.clip(q, -31, 31).astype(np.int8)
+    return llr, x
+
+
+# ----------------------------------------------------------------------------------------
+# numpy SM primitives: values are (s, m) int arrays
+# ----------------------------------------------------------------------------------------
+def sm_from_llr(llr):
+    t = ((llr.astype(np.int32) & 63) ^ 32) - 32          # sign-extend 6 bits
+    m = np.abs(t) & 31
+    s = ((t < 0) & (m != 0)).astype(np.int32)
+    return s, m
+
+
+def F(a, b):
+    return a[0] ^ b[0], np.minimum(a[1], b[1])
+
+
+def G(a, b, u, sat=None):
+    sa2 = a[0] ^ u
+    same = sa2 == b[0]
+    m = np.where(same, a[1] + b[1], np.abs(a[1] - b[1]))
+    s = np.where(a[1] < b[1], b[0], sa2)
+    if sat is not None:
+        m = np.minimum(m, sat)
+    return s, m
+
+
+def leaf(lam, fb):
+    """Spec_P16_ext on lam = (s, m) arrays [B, n]; returns x [B, n] (exact)."""
+    s, m = lam
+    n = s.shape[1]
+    if n == 2:
+        f0, f1 = fb & 1, (fb >> 1) & 1
+        u0 = (s[:, 0] ^ s[:, 1]) & f0
+        sg = np.where(m[:, 0] < m[:, 1], s[:, 1], s[:, 0] ^ u0) & f1
+        return np.stack([u0 ^ sg, sg], axis=1)
+    h = n // 2
+    a = (s[:, :h], m[:, :h])
+    b = (s[:, h:], m[:, h:])
+    xa = leaf(F(a, b), fb & ((1 << h) - 1))
+    xb = leaf(G(a, b, xa), fb >> h)
+    return np.concatenate([xa ^ xb, xb], axis=1)
+
+
+def rep_tree(lam):
+    s, m = lam
+    n = s.shape[1]
+    while n > 1:
+        h = n // 2
+        s, m = G((s[:, :h], m[:, :h]), (s[:, h:n], m[:, h:n]), 0)
+        n = h
+    return s[:, 0], m[:, 0]
+
+
+def run_schedule(ops, N, llr):
+    """Interpret a compiled schedule (list of dicts from Decoder.schedule()) on a batch."""
+    B = llr.shape[0]
+    Gw = N // 16
+    s, m = sm_from_llr(llr)
+    chan = (s.reshape(B, Gw, 16), m.reshape(B, Gw, 16))
+    buf = {0: chan}
+    bits = np.zeros((B, Gw, 16), dtype=np.int32)
+
+    def words(k, lo, hi):
+        return buf[k][0][:, lo:hi], buf[k][1][:, lo:hi]
+
+    def ubits(upos, n):
+        if upos < 0:
+            return 0
+        return bits[:, upos:upos + n]
+
+    for op in ops:
+        code, k, n, pos, upos, fb = op["op"], op["level"], op["n"], op["pos"], op["upos"], op["fb"]
+        if code == "END":
+            break
+        if code in ("F", "G", "FLEAF", "GLEAF", "REP", "R1", "SPC"):
+            a, b = words(k, 0, n), words(k, n, 2 * n)
+        if code == "F":
+            buf[k + 1] = F(a, b)
+        elif code == "G":
+            buf[k + 1] = G(a, b, ubits(upos, n), 15)
+        elif code in ("FLEAF", "GLEAF"):
+            lam = F(a, b) if code == "FLEAF" else G(a, b, ubits(upos, 1), 15)
+            bits[:, pos] = leaf((lam[0][:, 0], lam[1][:, 0]), fb)
+        elif code == "REP":
+            lam = F(a, b)
+            acc = (np.zeros(B, np.int32), np.zeros(B, np.int32))
+            for i in range(n):
+                t = rep_tree((lam[0][:, i], lam[1][:, i]))
+                acc = G(t, acc, 0, 511)
+            bits[:, pos:pos + n] = acc[0][:, None, None]
+        elif code in ("R1", "SPC"):
+            lam = G(a, b, ubits(upos, n), 15)
+            h = lam[0].copy()
+            if code == "SPC":
+                par = h.reshape(B, -1).sum(axis=1) & 1
+                br = np.array([int("{:04b}".format(l)[::-1], 2) for l in range(16)])
+                key = (lam[1] << 24) | (np.arange(n)[None, :, None] << 4) | br[None, None, :]
+                idx = key.reshape(B, -1).argmin(axis=1)
+                fl = np.zeros(B * n * 16, dtype=np.int32)
+                fl[np.arange(B) * n * 16 + idx] = par
+                h ^= fl.reshape(B, n, 16)
+            bits[:, pos:pos + n] = h
+        elif code == "H":
+            bits[:, pos:pos + n] ^= bits[:, pos + n:pos + 2 * n]
+        elif code == "H0":
+            bits[:, pos:pos + n] = bits[:, pos + n:pos + 2 * n]
+        else:
+            raise ValueError(code)
+    return bits.reshape(B, N).astype(np.uint8)
