@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Decode-only driver for rocprofv3 runs: generates frames once, then launches the decode
+kernel `--reps` times (no other kernels in the loop)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mask", default="FB_N1024_K512")
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--ebn0", type=float, default=2.5)
+    a = ap.parse_args()
+    import torch
+    import bench
+    import sc_polar_decoder_hls_amd as pkg
+    import util
+    mask = util.mask(a.mask)
+    dev = torch.device("cuda", 0)
+    dec = pkg.Decoder(mask)
+    dec.prepare(a.batch)
+    llr, _ = bench.gen_frames_torch(torch, mask, a.batch, a.ebn0, 0xF0, dev)
+    out = torch.empty((a.batch, dec.words), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    for _ in range(a.reps):
+        dec.decode(llr, out)
+    torch.cuda.synchronize()
+    print("decoded %d x %d frames (N=%d)" % (a.reps, a.batch, mask.size))
+
+
+if __name__ == "__main__":
+    main()
