@@ -39,6 +39,12 @@ CONFIGS = {
 }
 
 
+# kernel that carries the decode for each plan storage class (polar_sc_plan_stats.storage)
+KERNEL_NAMES = {0: "polar_sc_decode_kernel<false> (LDS interpreter)",
+                1: "polar_sc_decode_kernel<true> (HBM-scratch interpreter)",
+                2: "polar_sc_mask_kernel (per-mask hipRTC kernel)"}
+
+
 def gen_frames_torch(torch, mask, batch, ebn0_db, seed, device):
     """Synthetic AWGN frames on the GPU (reference C-sim chain semantics)."""
     N = mask.size
@@ -192,7 +198,7 @@ def main():
                        "mask": name, "parallelism": "frames sharded, dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "polar_sc_decode_kernel", "kernel_ms": kern_ms,
+                         "kernel": KERNEL_NAMES[dec.stats["storage"]], "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "frame_error_rate": fer,
             "parity_check": check,

@@ -91,7 +91,10 @@ typedef struct polar_sc_plan_stats {
     uint32_t n_ops;                   /* schedule length (incl. END)                   */
     uint32_t op_count[16];            /* per POLAR_OP_* code                           */
     uint64_t word_ops;                /* sum over ops of processed words (F/G-type)    */
-    uint32_t storage;                 /* 0 = LDS-resident stages, 1 = HBM scratch      */
+    uint32_t storage;                 /* stage LLR storage of the decode kernel:
+                                         0 = LDS (schedule interpreter), 1 = HBM scratch
+                                         (interpreter, large N), 2 = VGPRs (per-mask kernel,
+                                         N <= 1024)                                      */
     uint32_t lds_bytes_per_wave;      /* LDS footprint of one wave (8 frames)          */
     uint64_t scratch_bytes_per_wave;  /* HBM scratch of one wave when storage == 1     */
 } polar_sc_plan_stats;
@@ -154,6 +157,15 @@ int polar_sc_plan_get_stats(const polar_sc_plan *plan, polar_sc_plan_stats *stat
 /* Copy the compiled schedule (at most cap ops) and its length. */
 int polar_sc_plan_get_schedule(const polar_sc_plan *plan, polar_sc_op *ops, uint32_t cap,
                                uint32_t *count);
+
+/* Per-mask kernel (plans with stats.storage == 2, N <= 1024): generate its HIP source and
+ * compile it for gfx950 with hipRTC now (host only, no GPU needed); otherwise it is built
+ * on the first decode. -ENOTSUP for plans that use the schedule interpreter. The
+ * environment variable POLAR_SC_JIT=0 at plan creation selects the interpreter. */
+int polar_sc_plan_compile(const polar_sc_plan *plan);
+
+/* The generated per-mask kernel source (NUL-terminated, truncated to cap); *len = full size. */
+int polar_sc_plan_kernel_source(const polar_sc_plan *plan, char *buf, size_t cap, size_t *len);
 
 /* GPU self-test of the cross-lane (DPP) exchange patterns the kernels rely on.
  * out_dev: 4*64 uint32 on the device; entry [h][lane] = source lane seen by `lane` for

@@ -70,7 +70,7 @@ EXPORTS = (
     "polar_sc_decode_u16", "polar_sc_plan_prepare", "polar_sc_decode_host", "polar_load_frozen_tab",
     "polar_load_mask_file", "polar_codeword_to_info", "polar_sc_plan_get_stats",
     "polar_sc_plan_get_schedule", "polar_sc_selftest_lanes", "polar_sc_strerror",
-    "polar_sc_abi_version",
+    "polar_sc_abi_version", "polar_sc_plan_compile", "polar_sc_plan_kernel_source",
 )
 
 _lib = None
@@ -100,6 +100,8 @@ def lib():
         "polar_sc_plan_get_stats": [p, p],
         "polar_sc_plan_get_schedule": [p, p, u32, ctypes.POINTER(u32)],
         "polar_sc_selftest_lanes": [p],
+        "polar_sc_plan_compile": [p],
+        "polar_sc_plan_kernel_source": [p, ctypes.c_char_p, sz, ctypes.POINTER(sz)],
         "polar_sc_strerror": [i32],
         "polar_sc_abi_version": [],
     }
@@ -226,6 +228,26 @@ class Decoder:
         _check("polar_sc_plan_get_schedule", lib().polar_sc_plan_get_schedule(self._plan, arr, n.value, ctypes.byref(n)))
         return [dict(op=OPS.get(o.code, o.code), level=o.level, n=o.n, pos=o.pos, upos=o.upos, fb=o.fb)
                 for o in arr]
+
+    def compile(self):
+        """Build the per-mask kernel now (host-only hipRTC); False if the plan uses the
+        schedule interpreter instead."""
+        rc = lib().polar_sc_plan_compile(self._plan)
+        if rc == -95:
+            return False
+        _check("polar_sc_plan_compile", rc)
+        return True
+
+    def kernel_source(self):
+        n = ctypes.c_size_t(0)
+        rc = lib().polar_sc_plan_kernel_source(self._plan, None, 0, ctypes.byref(n))
+        if rc == -95:
+            return None
+        _check("polar_sc_plan_kernel_source", rc)
+        buf = ctypes.create_string_buffer(n.value + 1)
+        _check("polar_sc_plan_kernel_source",
+               lib().polar_sc_plan_kernel_source(self._plan, buf, n.value + 1, ctypes.byref(n)))
+        return buf.value.decode()
 
     def prepare(self, max_batch):
         _check("polar_sc_plan_prepare", lib().polar_sc_plan_prepare(self._plan, int(max_batch)))

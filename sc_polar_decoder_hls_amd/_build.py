@@ -9,8 +9,11 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "lib", "libpolar_sc.so")
-SOURCES = [os.path.join(PKG, "csrc", "polar_sc_kernels.hip"), os.path.join(PKG, "csrc", "polar_sc_host.cpp")]
-HEADERS = [os.path.join(ROOT, "include", "polar_sc.h")]
+SOURCES = [os.path.join(PKG, "csrc", "polar_sc_kernels.hip"), os.path.join(PKG, "csrc", "polar_sc_host.cpp"),
+           os.path.join(PKG, "csrc", "polar_sc_jit.cpp")]
+DEVICE_H = os.path.join(PKG, "csrc", "polar_sc_device.h")
+HEADERS = [os.path.join(ROOT, "include", "polar_sc.h"), DEVICE_H, os.path.join(PKG, "csrc", "polar_sc_plan.hpp")]
+GEN_DIR = os.path.join(PKG, "build")
 ARCH = os.environ.get("POLAR_SC_ARCH", "gfx950")
 
 
@@ -33,9 +36,16 @@ def build(force=False, verbose=False):
     if not force and not needs_build():
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    os.makedirs(GEN_DIR, exist_ok=True)
+    # embed the device header for hipRTC (per-mask kernels are compiled at plan time)
+    with open(DEVICE_H) as f:
+        dev_src = f.read()
+    assert ")POLARSRC\"" not in dev_src
+    with open(os.path.join(GEN_DIR, "polar_sc_device_src.inc"), "w") as f:
+        f.write("static const char kPolarDeviceSrc[] = R\"POLARSRC(" + dev_src + ")POLARSRC\";\n")
     tmp = LIB + ".tmp.%d" % os.getpid()
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-I" + os.path.join(ROOT, "include")] + SOURCES + ["-o", tmp]
+           "-I" + os.path.join(ROOT, "include"), "-I" + GEN_DIR] + SOURCES + ["-o", tmp, "-lhiprtc"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

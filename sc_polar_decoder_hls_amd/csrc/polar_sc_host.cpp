@@ -6,17 +6,13 @@
 // frozen-bit table (my_module.h:61-166 classifies 16-bit groups, then every transition is
 // a function of those classes). This file "compiles" that walk once per table into a flat
 // op list (polar_sc_op); the GPU kernel interprets the list with wave-uniform control.
-#include "../../include/polar_sc.h"
-
-#include <hip/hip_runtime.h>
+#include "polar_sc_plan.hpp"
 
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
-#include <map>
-#include <mutex>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -26,6 +22,8 @@ extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out
                                       int waves_per_block, int wave_dwords, void *stream);
 extern "C" int polar_sc_launch_selftest(uint32_t *out_dev);
 
+using polar_host::DevState;
+
 namespace {
 
 // node codes of shared/src/library.h:34-40
@@ -34,28 +32,7 @@ constexpr uint32_t NODE_R0 = 0x00, NODE_R1 = 0x0F, NODE_REP = 0x02, NODE_SPC = 0
 // largest per-wave LDS footprint kept on chip; above it stages go to HBM scratch
 constexpr uint32_t LDS_WAVE_LIMIT = 80u * 1024u;
 
-struct DevState {
-    void *ops = nullptr;
-    uint32_t *scratch = nullptr;
-    size_t scratch_bytes = 0;
-};
-
 }  // namespace
-
-struct polar_sc_plan {
-    uint32_t N = 0, G = 0, K = 0;
-    polar_sc_config cfg{};
-    std::vector<uint8_t> mask;       // N, 1 = information
-    std::vector<uint16_t> fb;        // G, Bit_Frozen (bit k = mask[16g+k])
-    std::vector<uint8_t> type;       // G, Node_Type
-    std::vector<polar_sc_op> ops;
-    polar_sc_plan_stats stats{};
-    int gmem = 0;
-    int wave_dwords = 0;             // per-wave storage, dwords (stage slots + bit dwords) * 64
-    int waves_per_block = 1;
-    mutable std::mutex mu;
-    mutable std::map<int, DevState> dev;
-};
 
 namespace {
 
@@ -161,6 +138,12 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
     if (hipGetDevice(&dev) != hipSuccess) return -EIO;
     std::lock_guard<std::mutex> lk(p->mu);
     DevState &st = p->dev[dev];
+    if (p->jit) {
+        int rc = polar_host::jit_load(*p, st);
+        if (rc) return rc;
+        *out = &st;
+        return 0;
+    }
     if (!st.ops) {
         size_t bytes = p->ops.size() * sizeof(polar_sc_op);
         if (hipMalloc(&st.ops, bytes) != hipSuccess) return -ENOMEM;
@@ -176,7 +159,7 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
                 st.scratch = nullptr;
                 st.scratch_bytes = 0;
             }
-            if (hipMalloc((void **)&st.scratch, need) != hipSuccess) return -ENOMEM;
+            if (hipMalloc(&st.scratch, need) != hipSuccess) return -ENOMEM;
             st.scratch_bytes = need;
         }
     }
@@ -193,7 +176,8 @@ int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size
     DevState *st = nullptr;
     int rc = ensure_device(p, batch, &st);
     if (rc) return rc;
-    rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, st->scratch, (int)p->N, (long)batch,
+    if (p->jit) return polar_host::jit_launch(*p, *st, llr, out, (long)batch, out_stride, stream);
+    rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, (uint32_t *)st->scratch, (int)p->N, (long)batch,
                                 out_stride, p->waves_per_block, p->wave_dwords, stream);
     return rc ? -EIO : 0;
 }
@@ -298,7 +282,11 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     const uint64_t wave_bytes = (uint64_t)p->wave_dwords * 4u;
     p->gmem = wave_bytes > LDS_WAVE_LIMIT ? 1 : 0;
     p->waves_per_block = 1;
-    s.storage = (uint32_t)p->gmem;
+    while ((1u << p->lg) < p->G) p->lg++;
+    // per-mask register kernel for N <= 1024 unless POLAR_SC_JIT=0 (schedule interpreter)
+    const char *jit_env = std::getenv("POLAR_SC_JIT");
+    p->jit = (polar_host::jit_supported(N) && !(jit_env && jit_env[0] == '0')) ? 1 : 0;
+    s.storage = p->jit ? 2u : (uint32_t)p->gmem;
     s.lds_bytes_per_wave = p->gmem ? 0u : (uint32_t)wave_bytes;
     s.scratch_bytes_per_wave = p->gmem ? wave_bytes : 0u;
     *out = p;
@@ -313,6 +301,7 @@ int polar_sc_plan_destroy(polar_sc_plan *p)
     for (auto &kv : p->dev) {
         if (have_dev) (void)hipSetDevice(kv.first);
         if (kv.second.ops) (void)hipFree(kv.second.ops);
+        if (kv.second.module) (void)hipModuleUnload(kv.second.module);
         if (kv.second.scratch) (void)hipFree(kv.second.scratch);
     }
     if (have_dev && !p->dev.empty()) (void)hipSetDevice(cur);
@@ -452,6 +441,28 @@ int polar_sc_plan_get_schedule(const polar_sc_plan *p, polar_sc_op *ops, uint32_
     if (ops) {
         uint32_t n = cap < *count ? cap : *count;
         std::memcpy(ops, p->ops.data(), n * sizeof(polar_sc_op));
+    }
+    return 0;
+}
+
+int polar_sc_plan_compile(const polar_sc_plan *p)
+{
+    if (!p) return -EINVAL;
+    if (!p->jit) return -ENOTSUP;
+    std::lock_guard<std::mutex> lk(p->mu);
+    return polar_host::jit_compile(*p);
+}
+
+int polar_sc_plan_kernel_source(const polar_sc_plan *p, char *buf, size_t cap, size_t *len)
+{
+    if (!p || !len) return -EINVAL;
+    if (!p->jit) return -ENOTSUP;
+    const std::string src = polar_host::jit_source(*p);
+    *len = src.size();
+    if (buf && cap) {
+        size_t n = cap - 1 < src.size() ? cap - 1 : src.size();
+        std::memcpy(buf, src.data(), n);
+        buf[n] = 0;
     }
     return 0;
 }

@@ -21,13 +21,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "polar_sc_device.h"
+
 namespace polar {
-
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-typedef short i16x2 __attribute__((ext_vector_type(2)));
-
-constexpr uint32_t SGN = 0x80008000u;   // sign flags of both halves
-constexpr uint32_t MAG = 0x7FFF7FFFu;   // magnitudes of both halves
 
 enum : int {
     OP_F = 1, OP_G = 2, OP_FLEAF = 3, OP_GLEAF = 4, OP_REP = 5, OP_R1 = 6, OP_SPC = 7,
@@ -39,179 +35,6 @@ struct Op {            // == polar_sc_op (include/polar_sc.h)
     uint32_t fb;
     int32_t r0, r1;
 };
-
-// ---------------------------------------------------------------------------------------
-// packed 16-bit helpers
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t U(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ u16x2 V(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
-__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) { return U(__builtin_elementwise_min(V(a), V(b))); }
-__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return U(V(a) + V(b)); }
-__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) { return U(V(a) - V(b)); }
-__device__ __forceinline__ uint32_t pk_sra15(uint32_t a)
-{
-    i16x2 x = __builtin_bit_cast(i16x2, a);
-    x = x >> (short)15;
-    return __builtin_bit_cast(uint32_t, x);
-}
-__device__ __forceinline__ uint32_t pk_abs_i16(uint32_t a)
-{
-    i16x2 x = __builtin_bit_cast(i16x2, a);
-    i16x2 y = -x;
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
-}
-// bitwise select: m ? a : b
-__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
-
-// F_function_SM (shared/src/functions.h:124-145): sign xor, magnitude min, no saturation.
-__device__ __forceinline__ uint32_t F_sm(uint32_t a, uint32_t b)
-{
-    return pk_min(a & MAG, b & MAG) | ((a ^ b) & SGN);
-}
-
-// qfull_add_sub_sm (shared/src/scalar.h:196-225) on SM16, followed by an optional clamp:
-//   a' = a with sign ^ u; same signs -> |a|+|b|, else ||a|-|b||;
-//   sign = |a| < |b| ? sign(b) : sign(a')      (ties -> sign(a'), may produce -0)
-// SAT = 15 : G_function_SM, VECTOR_SAT_SM<P,Q-1> clamp (functions.h:186-194, scalar.h:94-99)
-// SAT = 511: qfull_adder_sat_sm<11> of the REP accumulator (scalar.h:164-194)
-// SAT = 0  : G_extended_SM / qfull_adder_sm (exact; leaves and the REP pair tree)
-// u holds sign-flip flags at bit positions 15/31 only.
-template <int SAT>
-__device__ __forceinline__ uint32_t G_sm(uint32_t a, uint32_t b, uint32_t u)
-{
-    uint32_t a2 = a ^ u;
-    uint32_t ma = a & MAG, mb = b & MAG;
-    uint32_t d = pk_sub(ma, mb);              // bit 15 set iff |a| < |b|
-    uint32_t sum = pk_add(ma, mb);
-    uint32_t dif = pk_abs_i16(d);
-    uint32_t dm = pk_sra15(a2 ^ b);           // 0xFFFF where signs differ
-    uint32_t m = bsel(dm, dif, sum);
-    if constexpr (SAT != 0) m = pk_min(m, (uint32_t)SAT * 0x00010001u);
-    uint32_t s = bsel(d, b, a2) & SGN;        // only bits 15/31 of the selector matter
-    return s | m;
-}
-
-// ---------------------------------------------------------------------------------------
-// cross-lane exchange inside a 16-lane DPP row: value of lane (l ^ H)
-// ---------------------------------------------------------------------------------------
-template <int H>
-__device__ __forceinline__ uint32_t xorlane(uint32_t v)
-{
-    if constexpr (H == 1) {
-        return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    } else if constexpr (H == 2) {
-        return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    } else if constexpr (H == 4) {
-        uint32_t t = __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);  // row_half_mirror: l^7
-        return __builtin_amdgcn_mov_dpp(t, 0x1B, 0xF, 0xF, false);        // quad_perm [3,2,1,0]: ^3
-    } else {
-        static_assert(H == 8, "row partner distance");
-        return __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
-    }
-}
-
-// per-lane constants: all-ones where the lane is the lower ("a") member of its pair at
-// distance H
-struct Lanes {
-    uint32_t a1, a2, a4, a8;   // lane masks
-    uint32_t pl;               // PAR lane 0..15
-    uint32_t br;               // bitrev4(pl)
-    template <int H> __device__ __forceinline__ uint32_t amask() const
-    {
-        if constexpr (H == 1) return a1;
-        else if constexpr (H == 2) return a2;
-        else if constexpr (H == 4) return a4;
-        else return a8;
-    }
-};
-
-// ---------------------------------------------------------------------------------------
-// Leaf: Spec_PolarDec_16 -> Spec_P16_ext<6> (functions.h:521-546, 413-492, 366-384):
-// exact SC over the 16 LLRs of one word, F (min) + G_extended (exact, width grows).
-// Executed by all 16 lanes of each row (4 rows x 2 halves = 8 frames at once).
-// Returns x (the 16 encoded bits) as sign-position flags per lane.
-// Blocks whose frozen pattern is all-frozen return 0; all-information blocks return the
-// hard decisions of their LLRs, which is what the recursion computes for them
-// (induction on G with u = x_a: sign(a') = sign(b)).
-// ---------------------------------------------------------------------------------------
-template <int B, int W>
-__device__ __forceinline__ uint32_t leaf_rec(uint32_t L, uint32_t fb, uint32_t fbm, const Lanes &ln)
-{
-    constexpr uint32_t bm = ((1u << W) - 1u) << B;
-    const uint32_t sub = fb & bm;
-    if (sub == 0u) return 0u;
-    if (sub == bm) return L & SGN;
-    if constexpr (W == 2) {
-        // Spec_P2 (functions.h:366-384): lane B = a, lane B+1 = b
-        uint32_t P = xorlane<1>(L);
-        uint32_t u0 = (L ^ P) & fbm;                   // F_simplified & fb[B]   (valid on a)
-        uint32_t u0p = xorlane<1>(u0);
-        uint32_t d = pk_sub(P & MAG, L & MAG);         // |a| < |b|              (on b)
-        uint32_t u1 = bsel(d, L, P ^ u0p) & fbm;       // G_simplified & fb[B+1] (valid on b)
-        uint32_t u1p = xorlane<1>(u1);
-        return bsel(ln.a1, u0 ^ u1p, u1);
-    } else {
-        constexpr int H = W / 2;
-        uint32_t P = xorlane<H>(L);
-        uint32_t La = F_sm(L, P);                             // valid on a-lanes
-        uint32_t xa = leaf_rec<B, H>(La, fb, fbm, ln);
-        uint32_t Lb = G_sm<0>(P, L, xorlane<H>(xa));          // valid on b-lanes
-        uint32_t xb = leaf_rec<B + H, H>(Lb, fb, fbm, ln);
-        return bsel(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
-    }
-}
-
-__device__ __forceinline__ uint32_t leaf16(uint32_t L, uint32_t fb, const Lanes &ln)
-{
-    uint32_t fbm = ((fb >> ln.pl) & 1u) ? SGN : 0u;
-    return leaf_rec<0, 16>(L, fb, fbm, ln);
-}
-
-// ---------------------------------------------------------------------------------------
-// Row reductions
-// ---------------------------------------------------------------------------------------
-// ADD_TREE_16_SM (functions.h:3036-3083): pair (j, j+8), then (j, j+4) ... with the lower
-// lane as operand a. Butterfly form: both partners compute combine(lower, upper), so every
-// lane ends with the row total (same pairing and operand order as the reference tree).
-__device__ __forceinline__ uint32_t row_add_tree(uint32_t v, const Lanes &ln)
-{
-    uint32_t p;
-    p = xorlane<8>(v); v = G_sm<0>(bsel(ln.a8, v, p), bsel(ln.a8, p, v), 0u);
-    p = xorlane<4>(v); v = G_sm<0>(bsel(ln.a4, v, p), bsel(ln.a4, p, v), 0u);
-    p = xorlane<2>(v); v = G_sm<0>(bsel(ln.a2, v, p), bsel(ln.a2, p, v), 0u);
-    p = xorlane<1>(v); v = G_sm<0>(bsel(ln.a1, v, p), bsel(ln.a1, p, v), 0u);
-    return v;
-}
-
-__device__ __forceinline__ uint32_t row_min_u32(uint32_t v)
-{
-    v = min(v, xorlane<8>(v));
-    v = min(v, xorlane<4>(v));
-    v = min(v, xorlane<2>(v));
-    v = min(v, xorlane<1>(v));
-    return v;
-}
-
-__device__ __forceinline__ uint32_t row_xor(uint32_t v)
-{
-    v ^= xorlane<8>(v);
-    v ^= xorlane<4>(v);
-    v ^= xorlane<2>(v);
-    v ^= xorlane<1>(v);
-    return v;
-}
-
-// ---------------------------------------------------------------------------------------
-// Channel LLR -> SM16: wrapper_in + Adapt_format/qconv_format (wrapper_in.h:34,
-// library.h:18-28, scalar.h:229-239). The LLR is the low 6 bits (sc_bigint<6>); -32 -> +0.
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t conv_half(int c)
-{
-    int t = (int)((uint32_t)c << 26) >> 26;      // sign-extend 6 bits
-    uint32_t m = (uint32_t)(t < 0 ? -t : t) & 31u;
-    uint32_t s = (t < 0 && m != 0u) ? 0x8000u : 0u;
-    return m | s;
-}
 
 // ---------------------------------------------------------------------------------------
 // Per-wave storage: LDS (small N) or HBM scratch (large N). `base` already includes the
@@ -427,17 +250,6 @@ __device__ __forceinline__ void op_h(const Ctx &c, int pos, int n)
     }
 }
 
-// 16x16 bit transpose inside a row on both 16-bit halves: lane l bit j <- lane j bit l.
-__device__ __forceinline__ uint32_t row_transpose16(uint32_t v, const Lanes &ln)
-{
-    uint32_t p;
-    p = xorlane<8>(v); v = bsel(ln.a8, (v & 0x00FF00FFu) | ((p & 0x00FF00FFu) << 8), ((p >> 8) & 0x00FF00FFu) | (v & 0xFF00FF00u));
-    p = xorlane<4>(v); v = bsel(ln.a4, (v & 0x0F0F0F0Fu) | ((p & 0x0F0F0F0Fu) << 4), ((p >> 4) & 0x0F0F0F0Fu) | (v & 0xF0F0F0F0u));
-    p = xorlane<2>(v); v = bsel(ln.a2, (v & 0x33333333u) | ((p & 0x33333333u) << 2), ((p >> 2) & 0x33333333u) | (v & 0xCCCCCCCCu));
-    p = xorlane<1>(v); v = bsel(ln.a1, (v & 0x55555555u) | ((p & 0x55555555u) << 1), ((p >> 1) & 0x55555555u) | (v & 0xAAAAAAAAu));
-    return v;
-}
-
 // ---------------------------------------------------------------------------------------
 // The decode kernel: one wave = 8 frames; `ops` is the compiled schedule.
 //   llr:  [batch][N] int8;   out: [batch][out_stride] uint16 (bit_mem_1 words, END order)
@@ -469,12 +281,7 @@ __global__ void __launch_bounds__(256) polar_sc_decode_kernel(
     const long f_hi_c = f_hi < batch ? f_hi : (long)batch - 1;
     c.llr_lo = llr + (size_t)f_lo_c * (size_t)N + pl;
     c.llr_hi = llr + (size_t)f_hi_c * (size_t)N + pl;
-    c.ln.pl = (uint32_t)pl;
-    c.ln.br = (uint32_t)(((pl & 1) << 3) | ((pl & 2) << 1) | ((pl & 4) >> 1) | ((pl & 8) >> 3));
-    c.ln.a1 = (pl & 1) ? 0u : 0xFFFFFFFFu;
-    c.ln.a2 = (pl & 2) ? 0u : 0xFFFFFFFFu;
-    c.ln.a4 = (pl & 4) ? 0u : 0xFFFFFFFFu;
-    c.ln.a8 = (pl & 8) ? 0u : 0xFFFFFFFFu;
+    c.ln.init((uint32_t)pl);
 
     if (wave * 8 >= batch) return;   // whole wave idle (uniform)
 

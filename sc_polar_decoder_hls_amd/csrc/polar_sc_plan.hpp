@@ -1,0 +1,57 @@
+// polar_sc_plan.hpp -- private definition of polar_sc_plan (include/polar_sc.h), shared by
+// the host plan/schedule code (polar_sc_host.cpp) and the per-mask kernel generator
+// (polar_sc_jit.cpp).
+#pragma once
+
+#include "../../include/polar_sc.h"
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace polar_host {
+
+struct DevState {
+    void *ops = nullptr;          // schedule (interpreter kernels)
+    void *scratch = nullptr;      // HBM stage scratch (interpreter, large N)
+    size_t scratch_bytes = 0;
+    hipModule_t module = nullptr; // per-mask kernel
+    hipFunction_t fn = nullptr;
+};
+
+enum JitMode { JIT_OFF = 0, JIT_AUTO = 1 };
+
+}  // namespace polar_host
+
+struct polar_sc_plan {
+    uint32_t N = 0, G = 0, K = 0;
+    int lg = 0;                      // log2(N/16)
+    polar_sc_config cfg{};
+    std::vector<uint8_t> mask;       // N, 1 = information
+    std::vector<uint16_t> fb;        // G, Bit_Frozen (bit k = mask[16g+k])
+    std::vector<uint8_t> type;       // G, Node_Type
+    std::vector<polar_sc_op> ops;
+    polar_sc_plan_stats stats{};
+    int gmem = 0;
+    int wave_dwords = 0;             // interpreter: per-wave storage, dwords
+    int waves_per_block = 1;
+    int jit = 0;                     // 1: decode with the per-mask kernel
+    mutable std::mutex mu;
+    mutable std::map<int, polar_host::DevState> dev;
+    mutable std::vector<char> jit_code;   // compiled code object (lazily built)
+    mutable std::string jit_log;
+};
+
+namespace polar_host {
+// per-mask kernel: generate source, compile with hipRTC for gfx950 (host only), load it on
+// the current device, launch it
+std::string jit_source(const polar_sc_plan &p);
+int jit_compile(const polar_sc_plan &p);                 // fills p.jit_code (idempotent)
+int jit_load(const polar_sc_plan &p, DevState &st);      // module + function on this device
+int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out,
+               long batch, int out_stride, void *stream);
+bool jit_supported(uint32_t N);
+}  // namespace polar_host

@@ -1,5 +1,7 @@
 """GPU parity: the HIP decoder (through the C ABI) must be bit-exact with the CPU oracle
 (literal restatement of my_module::do_action) on the same LLR frames."""
+import os
+
 import numpy as np
 import pytest
 
@@ -8,8 +10,22 @@ import util
 pytestmark = pytest.mark.gpu
 
 
-def _decode(pkg, torch, mask, llr):
-    dec = pkg.Decoder(mask)
+def make_decoder(pkg, mask, jit=True):
+    """jit=True: default plan (per-mask register kernel for N <= 1024); False: schedule
+    interpreter (POLAR_SC_JIT=0 at plan creation)."""
+    old = os.environ.get("POLAR_SC_JIT")
+    os.environ["POLAR_SC_JIT"] = "1" if jit else "0"
+    try:
+        return pkg.Decoder(mask)
+    finally:
+        if old is None:
+            del os.environ["POLAR_SC_JIT"]
+        else:
+            os.environ["POLAR_SC_JIT"] = old
+
+
+def _decode(pkg, torch, mask, llr, jit=True):
+    dec = make_decoder(pkg, mask, jit)
     out = dec.decode(torch.from_numpy(np.ascontiguousarray(llr)).cuda())
     torch.cuda.synchronize()
     return pkg.unpack_bits(out.cpu().numpy(), mask.size)
@@ -31,15 +47,17 @@ def test_dpp_row_exchange(pkg, cuda):
                                   "frozen_n_1024_k_512", "frozen_n_1024_k_768", "FB_N2048_K1024",
                                   "frozen_n_2048_k_1024", "frozen_n_4096_k_2048"])
 @pytest.mark.parametrize("ebn0", [0.0, 2.5])
-def test_parity_awgn(pkg, cuda, oracle_mod, name, ebn0):
+@pytest.mark.parametrize("jit", [True, False], ids=["maskkernel", "interp"])
+def test_parity_awgn(pkg, cuda, oracle_mod, name, ebn0, jit):
     mask = util.mask(name)
     batch = 67 if mask.size <= 1024 else 19
     llr, _ = util.synth_frames(mask, batch, ebn0_db=ebn0, seed=1234 + int(ebn0 * 10))
-    _assert_same(_decode(pkg, cuda, mask, llr), oracle_mod.decode_fsm(mask, llr), name)
+    _assert_same(_decode(pkg, cuda, mask, llr, jit), oracle_mod.decode_fsm(mask, llr), name)
 
 
 @pytest.mark.parametrize("kind", ["uniform6", "int8_wrap", "zero", "sat", "minus32", "tiny"])
-def test_parity_llr_edge_cases(pkg, cuda, oracle_mod, kind):
+@pytest.mark.parametrize("jit", [True, False], ids=["maskkernel", "interp"])
+def test_parity_llr_edge_cases(pkg, cuda, oracle_mod, kind, jit):
     mask = util.mask("FB_N1024_K512")
     rng = np.random.default_rng(99)
     shape = (40, mask.size)
@@ -51,7 +69,7 @@ def test_parity_llr_edge_cases(pkg, cuda, oracle_mod, kind):
         "minus32": lambda: rng.choice([-32, -1, 0, 1], shape),
         "tiny": lambda: rng.integers(-1, 2, shape),
     }[kind]().astype(np.int8)
-    _assert_same(_decode(pkg, cuda, mask, llr), oracle_mod.decode_fsm(mask, llr), kind)
+    _assert_same(_decode(pkg, cuda, mask, llr, jit), oracle_mod.decode_fsm(mask, llr), kind)
 
 
 @pytest.mark.parametrize("batch", [1, 3, 8, 9, 15, 16, 33])
@@ -77,7 +95,7 @@ def test_parity_random_masks(pkg, cuda, oracle_mod):
             mask = np.full(N, trial & 1)
         mask = mask.astype(np.uint8)
         llr = rng.integers(-32, 32, size=(13, N)).astype(np.int8)
-        _assert_same(_decode(pkg, cuda, mask, llr), oracle_mod.decode_fsm(mask, llr),
+        _assert_same(_decode(pkg, cuda, mask, llr, jit=(trial % 2 == 0)), oracle_mod.decode_fsm(mask, llr),
                      "random mask trial %d N=%d" % (trial, N))
 
 
@@ -95,6 +113,7 @@ def test_u16_and_host_entry_points(pkg, cuda, oracle_mod):
     llr, _ = util.synth_frames(mask, 21, ebn0_db=1.5, seed=5)
     ref = oracle_mod.decode_fsm(mask, llr)
     dec = pkg.Decoder(mask)
+    assert dec.stats["storage"] == 2
     w16 = dec.decode_u16(cuda.from_numpy(llr).cuda())
     cuda.cuda.synchronize()
     bits16 = np.unpackbits(w16.cpu().numpy().view(np.uint8), axis=1, bitorder="little")
@@ -103,11 +122,12 @@ def test_u16_and_host_entry_points(pkg, cuda, oracle_mod):
     _assert_same(pkg.unpack_bits(host, mask.size), ref, "decode_host")
 
 
-def test_n32_output_padding(pkg, cuda, oracle_mod):
+@pytest.mark.parametrize("jit", [True, False], ids=["maskkernel", "interp"])
+def test_n32_output_padding(pkg, cuda, oracle_mod, jit):
     rng = np.random.default_rng(32)
     mask = rng.integers(0, 2, 32).astype(np.uint8)
     llr = rng.integers(-31, 32, size=(11, 32)).astype(np.int8)
-    dec = pkg.Decoder(mask)
+    dec = make_decoder(pkg, mask, jit)
     out = dec.decode(cuda.from_numpy(llr).cuda())
     cuda.cuda.synchronize()
     words = out.cpu().numpy().view(np.uint64)
@@ -147,8 +167,22 @@ def test_full_size_c2_noiseless_roundtrip(pkg, cuda):
     u = rng.integers(0, 2, size=(B, mask.size), dtype=np.uint8) & mask[None, :]
     x = util.encode_np(u)
     llr = np.where(x == 1, -31, 31).astype(np.int8)
-    got = _decode(pkg, cuda, mask, llr)
-    assert (got == x).all()
+    for jit in (True, False):
+        got = _decode(pkg, cuda, mask, llr, jit)
+        assert (got == x).all()
     dec = pkg.Decoder(mask)
     info = dec.codeword_to_info(pkg.pack_bits(got[:64]))
     np.testing.assert_array_equal(info, u[:64][:, mask.astype(bool)])
+
+
+def test_mask_kernel_equals_interpreter_full_c2(pkg, cuda):
+    """The two kernel families agree bit-for-bit on a full C2 batch of AWGN frames."""
+    import bench
+    mask = util.mask("FB_N1024_K512")
+    llr, _ = bench.gen_frames_torch(cuda, mask, 65536, 2.0, 99, cuda.device("cuda"))
+    outs = []
+    for jit in (True, False):
+        dec = make_decoder(pkg, mask, jit)
+        outs.append(dec.decode(llr).cpu().numpy())
+    cuda.cuda.synchronize()
+    assert (outs[0] == outs[1]).all()
