@@ -40,6 +40,14 @@ __device__ __forceinline__ u32 pk_abs_i16(u32 a)
 }
 // bitwise select: m ? a : b
 __device__ __forceinline__ u32 bsel(u32 m, u32 a, u32 b) { return (a & m) | (b & ~m); }
+// the same with the mask hidden from the optimiser: a mask known to be 0 / 0xFFFF per half
+// is otherwise rewritten into v_cmp + v_cndmask per half + v_perm (8 instructions for 1)
+__device__ __forceinline__ u32 opaque(u32 m)
+{
+    asm("" : "+v"(m));
+    return m;
+}
+__device__ __forceinline__ u32 bselo(u32 m, u32 a, u32 b) { return bsel(opaque(m), a, b); }
 
 // F_function_SM (shared/src/functions.h:124-145): sign xor, magnitude min, no saturation.
 __device__ __forceinline__ u32 F_sm(u32 a, u32 b)
@@ -57,16 +65,13 @@ __device__ __forceinline__ u32 F_sm(u32 a, u32 b)
 template <int SAT>
 __device__ __forceinline__ u32 G_sm(u32 a, u32 b, u32 u)
 {
-    u32 a2 = a ^ u;
-    u32 ma = a & MAG, mb = b & MAG;
-    u32 d = pk_sub(ma, mb);                   // bit 15 set iff |a| < |b|
-    u32 sum = pk_add(ma, mb);
-    u32 dif = pk_abs_i16(d);
-    u32 dm = pk_sra(a2 ^ b, 15);              // 0xFFFF where signs differ
-    u32 m = bsel(dm, dif, sum);
+    const u32 ma = a & MAG, mb = b & MAG;
+    const u32 d = pk_sub(ma, mb);             // bit 15 set iff |a| < |b|
+    const u32 x = a ^ u ^ b;                  // bit 15 set iff sign(a') != sign(b)
+    u32 m = bsel(pk_sra(x, 15), pk_abs_i16(d), pk_add(ma, mb));
     if constexpr (SAT != 0) m = pk_min(m, (u32)SAT * 0x00010001u);
-    u32 s = bsel(d, b, a2) & SGN;             // only bits 15/31 of the selector matter
-    return s | m;
+    // |a| < |b| -> sign(b); otherwise sign(a') = sign(b) ^ x
+    return ((b ^ (x & ~d)) & SGN) | m;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -76,15 +81,15 @@ template <int H>
 __device__ __forceinline__ u32 xorlane(u32 v)
 {
     if constexpr (H == 1) {
-        return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+        return __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
     } else if constexpr (H == 2) {
-        return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+        return __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
     } else if constexpr (H == 4) {
-        u32 t = __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);  // row_half_mirror: l^7
-        return __builtin_amdgcn_mov_dpp(t, 0x1B, 0xF, 0xF, false);   // quad_perm [3,2,1,0]: ^3
+        u32 t = __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, true);  // row_half_mirror: l^7
+        return __builtin_amdgcn_update_dpp(0u, t, 0x1B, 0xF, 0xF, true);   // quad_perm [3,2,1,0]: ^3
     } else {
         static_assert(H == 8, "row partner distance");
-        return __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
+        return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, true);  // row_ror:8
     }
 }
 
@@ -245,15 +250,135 @@ __device__ __forceinline__ u32 conv_half(int c)
     return m | s;
 }
 
-// raw = b_lo | b_hi << 16 (two int8 LLRs) -> SM16 pair
+// two channel bytes into the halves of one register (d16 / d16_hi loads)
+__device__ __forceinline__ u32 ld_pair(const unsigned char *lo, const unsigned char *hi)
+{
+    u16x2 v;
+    v.x = *lo;
+    v.y = *hi;
+    return U(v);
+}
+
+// raw = b_lo | b_hi << 16 (two int8 LLRs, any bits above bit 5 ignored) -> SM16 pair.
+// With t = raw & 63: |LLR| = min(t, 64 - t) & 31 (t = 32, i.e. -32, -> 0) and the sign is
+// set iff t >= 33 (t + 0x7FDF reaches bit 15).
 __device__ __forceinline__ u32 conv_pair(u32 raw)
 {
-    u32 t = pk_sra(pk_shl(raw, 10), 10);                     // sign-extend 6 bits per half
-    u32 m = pk_abs_i16(t) & 0x001F001Fu;                     // |t|, -32 -> 0
-    // sign iff t in [-31, -1]  <=>  x = t+31 in [0, 30]  <=>  x >= 0 && x - 31 < 0
-    u32 x = pk_add(t, 0x001F001Fu);
-    u32 w = pk_sub(x, 0x001F001Fu);
-    return m | ((~x & w) & SGN);
+    u32 t = raw & 0x003F003Fu;
+    u32 m = pk_min(t, pk_sub(0x00400040u, t)) & 0x001F001Fu;
+    return m | (pk_add(t, 0x7FDF7FDFu) & SGN);
+}
+
+// Channel byte -> SM8 (bit 7 sign, bits 0..4 magnitude): the per-mask kernels keep a
+// 256-entry copy of this map in LDS and convert a word with two lookups + 2 VALU.
+__device__ __forceinline__ u32 sm8_of_byte(u32 b)
+{
+    const u32 t = b & 63u;
+    const u32 m = (t < 64u - t ? t : 64u - t) & 31u;
+    return (t >= 33u ? 0x80u : 0u) | m;
+}
+// two SM8 bytes (low byte of lo, low byte of hi) -> SM16 pair: duplicate each byte into both
+// bytes of its half, keep bit 15 and bits 0..4
+__device__ __forceinline__ u32 sm8_pair(u32 lo, u32 hi)
+{
+    return __builtin_amdgcn_perm(hi, lo, 0x04040000u) & 0x801F801Fu;
+}
+
+// ---------------------------------------------------------------------------------------
+// Sign-only G: the hard decision of G_sm (R1 nodes need nothing else; the magnitude and its
+// saturation never change the sign). u as for G_sm.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ u32 G_sign(u32 a, u32 b, u32 u)
+{
+    u32 d = pk_sub(a & MAG, b & MAG);
+    return bsel(d, b, a ^ u) & SGN;
+}
+
+// ---------------------------------------------------------------------------------------
+// Leaf in split form (per-mask kernels): M = magnitudes (u16 pair), S = sign masks (0xFFFF
+// in a negative half). Same recursion and results as leaf_ct, fewer instructions:
+//   F : M = min(M, M'), S = S ^ S'
+//   G : x = S_F ^ U (signs of a' and b differ; S_F = S ^ S' is the F sign, U the partner's
+//       partial sums as masks), |a| < |b| from M' - M, magnitude = x ? |M' - M| : M' + M,
+//       sign = S ^ (x & ~lt)   (same signs -> sign(b); differ -> lt ? sign(b) : sign(a'))
+// Returns x as 16-bit masks (0xFFFF = bit 1).
+// ---------------------------------------------------------------------------------------
+template <u32 FB, int B, int W>
+__device__ __forceinline__ u32 leaf_ms(u32 M, u32 S, const Lanes &ln)
+{
+    constexpr u32 bm = ((1u << W) - 1u) << B;
+    constexpr u32 sub = FB & bm;
+    if constexpr (sub == 0u) {
+        return 0u;
+    } else if constexpr (sub == bm) {
+        return S;
+    } else if constexpr (W == 2) {
+        if constexpr ((sub >> B) == 1u) {
+            return (S ^ xorlane<1>(S)) & ln.a1;                 // (1, 0): x = [sa ^ sb, 0]
+        } else {
+            const u32 PM = xorlane<1>(M), PS = xorlane<1>(S);    // (0, 1): x = [u1, u1]
+            const u32 lt = pk_sra(pk_sub(PM, M), 15);
+            const u32 u1 = bselo(lt, S, PS);                     // valid on the b lane
+            return bselo(ln.a1, xorlane<1>(u1), u1);
+        }
+    } else {
+        constexpr int H = W / 2;
+        const u32 PM = xorlane<H>(M), PS = xorlane<H>(S);
+        const u32 SF = S ^ PS;
+        const u32 xa = leaf_ms<FB, B, H>(pk_min(M, PM), SF, ln);
+        const u32 x = opaque(SF ^ xorlane<H>(xa));
+        const u32 d = pk_sub(PM, M);
+        const u32 lt = opaque(pk_sra(d, 15));
+        const u32 Mb = bsel(x, pk_sub(d ^ lt, lt), pk_add(PM, M));
+        const u32 xb = leaf_ms<FB, B + H, H>(Mb, S ^ (x & ~lt), ln);
+        return bselo(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// REP nodes (Spec_REP, functions.h:3086-3107) -- value path. The reference decision is the
+// sign of acc = sat511(... sat511(T_1 + sat511(T_0 + 0)) ...) where T_w is the exact
+// pair-tree sum of word w. Every step is an exact sum or a clamp, so the two's-complement
+// chain below carries the same value; only a zero total needs the SM sign-of-zero rule,
+// which the caller resolves with the exact SM path (rep_exact_*).
+// ---------------------------------------------------------------------------------------
+// F(a, b) of two SM16 pairs as value + 512 per half (no carries between the halves: the
+// 16-word row sum stays within 0..16383)
+__device__ __forceinline__ u32 F_biased(u32 a, u32 b)
+{
+    const u32 m = pk_min(a & MAG, b & MAG);
+    const u32 s = pk_sra(a ^ b, 15);
+    return pk_add(pk_sub(m ^ s, s), 0x02000200u);
+}
+// SM16 pair -> value + 512 per half
+__device__ __forceinline__ u32 sm_biased(u32 x)
+{
+    const u32 s = pk_sra(x, 15);
+    return pk_add(pk_sub((x & MAG) ^ s, s), 0x02000200u);
+}
+// row total in every lane (rotation butterfly; 32-bit adds take the DPP operand directly)
+__device__ __forceinline__ u32 row_sum_biased(u32 v)
+{
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, true);   // row_ror:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x124, 0xF, 0xF, true);   // row_ror:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x122, 0xF, 0xF, true);   // row_ror:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x121, 0xF, 0xF, true);   // row_ror:1
+    return v;
+}
+// acc = clamp(acc + T, -511, 511) with T = row total - 16 * 512 (two's complement halves)
+__device__ __forceinline__ u32 rep_acc(u32 acc, u32 total_biased)
+{
+    u32 t = pk_sub(pk_add(acc, total_biased), 0x20002000u);
+    i16x2 v = __builtin_bit_cast(i16x2, t);
+    v = __builtin_elementwise_min(v, (i16x2){511, 511});
+    v = __builtin_elementwise_max(v, (i16x2){-511, -511});
+    return __builtin_bit_cast(u32, v);
+}
+// true if some frame of the wave ended with a zero accumulator
+__device__ __forceinline__ bool rep_any_zero(u32 acc)
+{
+    const bool z = ((acc & 0xFFFFu) == 0u) || ((acc >> 16) == 0u);
+    return __builtin_amdgcn_ballot_w64(z) != 0ull;
 }
 
 }  // namespace polar

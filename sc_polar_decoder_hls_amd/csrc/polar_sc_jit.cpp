@@ -42,19 +42,33 @@ struct Gen {
         else s << "b" << sd << "[" << i << "]";
         return s.str();
     }
-    // 16 partial-sum words starting at q: low frame bits 0..15, high frame bits 16..31
+    // Partial sums: u32 bw[max(1, G / 16)], dword j = groups 16 j .. 16 j + 15, low frame in
+    // bits 0..15 and high frame in bits 16..31 (the layout every consumer wants, so H ops
+    // are one or two instructions and the G ops take their u flags without repacking).
+    // 16 partial-sum words starting at q (only the low n bits of each half are used)
     static std::string get16(int q)
     {
         std::ostringstream s;
-        s << "(((u32)(bl >> " << q << ") & 0xFFFFu) | ((u32)(bh >> " << q << ") << 16))";
+        if (q % 16 == 0) s << "bw[" << q / 16 << "]";
+        else s << "(bw[" << q / 16 << "] >> " << q % 16 << ")";
         return s.str();
     }
+    static std::string hexmask(int pos, int n)   // bits [pos % 16, +n) of both halves
+    {
+        std::ostringstream s;
+        const unsigned m = ((1u << n) - 1u) << (pos % 16);
+        s << "0x" << std::hex << (m | (m << 16)) << std::dec << "u";
+        return s.str();
+    }
+    // write n <= 16 partial-sum words at pos from acc (low frame bits 0..n-1, high 16..)
     void put(int pos, int n, const std::string &acc)
     {
-        unsigned long long m = ((n >= 64) ? ~0ull : ((1ull << n) - 1ull)) << pos;
-        o << "    { const u32 a_ = " << acc << "; const u64 m_ = 0x" << std::hex << m << std::dec
-          << "ull; bl = (bl & ~m_) | (((u64)(a_ & 0xFFFFu) << " << pos << ") & m_); bh = (bh & ~m_) | (((u64)(a_ >> 16) << "
-          << pos << ") & m_); }\n";
+        if (n >= 16) {
+            o << "    bw[" << pos / 16 << "] = " << acc << ";\n";
+        } else {
+            o << "    bw[" << pos / 16 << "] = bsel(" << hexmask(pos, n) << ", (" << acc << ") << " << pos % 16 << ", bw["
+              << pos / 16 << "]);\n";
+        }
     }
     // G-type ops: loop over n words with partial sums from upos (or zero)
     void ucache(int upos, int i)
@@ -67,8 +81,18 @@ struct Gen {
     static std::string uflag(int i)
     {
         std::ostringstream s;
-        s << "((c_ << " << (15 - (i & 15)) << ") & SGN)";
+        s << "(c_ << " << (15 - (i & 15)) << ")";   // G_sm / G_sign read only bits 15 and 31 of u
         return s.str();
+    }
+
+    // After an F-type op (F, FLEAF, REP) the parent words stay live until the matching G.
+    // An empty asm that redefines them in place (no instruction) stops the optimiser from
+    // carrying the F op's intermediates (x & MAG, a ^ b) over to the G op, which would
+    // triple the registers held across the whole left subtree.
+    void clobber_parent(int sd, int n)
+    {
+        if (sd == LG) return;   // root: channel words are re-read from LDS
+        for (int i = 0; i < 2 * n; i++) o << "  asm volatile(\"\" : \"+v\"(b" << sd << "[" << i << "]));\n";
     }
 
     // scheduling fence: keeps the straight-line code from hoisting every load of a long
@@ -90,6 +114,7 @@ struct Gen {
                 o << "  b" << cd << "[" << i << "] = F_sm(" << S(sd, i) << ", " << S(sd, n + i) << ");\n";
                 chunk_fence(i, n);
             }
+            clobber_parent(sd, n);
             break;
         case POLAR_OP_G:
             o << "  { // G level " << op.level << " n " << n << " upos " << op.upos << "\n    u32 c_;\n";
@@ -106,26 +131,35 @@ struct Gen {
             o << "  { // " << (op.code == POLAR_OP_FLEAF ? "F" : "G") << "+leaf pos " << op.pos << " fb 0x" << std::hex
               << op.fb << std::dec << "\n";
             if (op.code == POLAR_OP_FLEAF) {
-                o << "    const u32 L_ = F_sm(" << S(sd, 0) << ", " << S(sd, 1) << ");\n";
+                o << "    const u32 a_ = " << S(sd, 0) << ", b_ = " << S(sd, 1) << ";\n"
+                  << "    const u32 M_ = pk_min(a_ & MAG, b_ & MAG), S_ = pk_sra(a_ ^ b_, 15);\n";
             } else {
                 o << "    u32 c_; ";
                 ucache(op.upos, 0);
-                o << "    const u32 L_ = G_sm<15>(" << S(sd, 0) << ", " << S(sd, 1) << ", " << uflag(0) << ");\n";
+                o << "    const u32 L_ = G_sm<15>(" << S(sd, 0) << ", " << S(sd, 1) << ", " << uflag(0) << ");\n"
+                  << "    const u32 M_ = L_ & MAG, S_ = pk_sra(L_, 15);\n";
             }
-            o << "    const u32 x_ = leaf_ct<0x" << std::hex << op.fb << std::dec << "u, 0, 16>(L_, ln);\n";
-            put(op.pos, 1, "((x_ >> 15) & 1u) | ((x_ >> 15) & 0x10000u)");
+            o << "    const u32 x_ = leaf_ms<0x" << std::hex << op.fb << std::dec << "u, 0, 16>(M_, S_, ln);\n";
+            put(op.pos, 1, "x_ & 0x00010001u");
             o << "  }\n";
+            if (op.code == POLAR_OP_FLEAF) clobber_parent(sd, 1);
             break;
         }
         case POLAR_OP_REP:
-            o << "  { // REP n " << n << " pos " << op.pos << "\n    u32 acc_ = 0u;\n";
+            // value chain in two's complement; the exact SM chain only when a total is 0
+            o << "  { // REP n " << n << " pos " << op.pos << "\n    u32 acc_ = 0u, full_;\n";
             for (int i = 0; i < n; i++) {
-                o << "    acc_ = G_sm<511>(row_add_tree(F_sm(" << S(sd, i) << ", " << S(sd, n + i) << "), ln), acc_, 0u);\n";
+                o << "    acc_ = rep_acc(acc_, row_sum_biased(F_biased(" << S(sd, i) << ", " << S(sd, n + i) << ")));\n";
                 chunk_fence(i, n);
             }
-            o << "    const u32 full_ = ((acc_ & 0x8000u) ? 0x0000FFFFu : 0u) | ((acc_ & 0x80000000u) ? 0xFFFF0000u : 0u);\n";
+            o << "    if (rep_any_zero(acc_)) {\n      acc_ = 0u;\n";
+            for (int i = 0; i < n; i++)
+                o << "      acc_ = G_sm<511>(row_add_tree(F_sm(" << S(sd, i) << ", " << S(sd, n + i) << "), ln), acc_, 0u);\n";
+            // two's complement or SM16: the hard decision is bit 15 / 31 either way
+            o << "    }\n    full_ = pk_sra(acc_, 15);\n";
             for (int j = 0; j < n; j += 16) put(op.pos + j, n < 16 ? n : 16, "full_");
             o << "  }\n";
+            clobber_parent(sd, n);
             break;
         case POLAR_OP_R1:
         case POLAR_OP_SPC: {
@@ -134,8 +168,9 @@ struct Gen {
               << "\n    u32 c_, acc_ = 0u, par_ = 0u, klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu;\n";
             for (int i = 0; i < n; i++) {
                 ucache(op.upos, i);
-                o << "    { const u32 l_ = G_sm<15>(" << S(sd, i) << ", " << S(sd, n + i) << ", " << uflag(i)
-                  << "); const u32 h_ = l_ & SGN; acc_ |= h_ >> " << (15 - (i & 15)) << ";";
+                o << "    { const u32 " << (spc ? "l_ = G_sm<15>(" : "h_ = G_sign(") << S(sd, i) << ", " << S(sd, n + i)
+                  << ", " << uflag(i) << ");" << (spc ? " const u32 h_ = l_ & SGN;" : "") << " acc_ |= h_ >> "
+                  << (15 - (i & 15)) << ";";
                 if (spc)
                     o << " par_ ^= h_; klo_ = __builtin_elementwise_min(klo_, ((l_ & 0x1Fu) << 24) | " << (i << 4)
                       << "u); khi_ = __builtin_elementwise_min(khi_, (((l_ >> 16) & 0x1Fu) << 24) | " << (i << 4)
@@ -148,25 +183,41 @@ struct Gen {
                 }
             }
             if (spc) {
+                // flip the partial sum at the least reliable position when the parity is odd
                 o << "    par_ = row_xor(par_);\n"
                      "    klo_ = row_min_u32(klo_ | ln.br); khi_ = row_min_u32(khi_ | ln.br);\n"
-                     "    if ((par_ & 0x8000u) && (klo_ & 15u) == ln.br) bl ^= 1ull << ("
-                  << op.pos << " + ((klo_ >> 4) & 0xFFFFFu));\n"
-                     "    if ((par_ & 0x80000000u) && (khi_ & 15u) == ln.br) bh ^= 1ull << ("
-                  << op.pos << " + ((khi_ >> 4) & 0xFFFFFu));\n";
+                     "    const u32 ilo_ = (klo_ >> 4) & 0xFFFFFu, ihi_ = (khi_ >> 4) & 0xFFFFFu;\n"
+                     "    const bool flo_ = (par_ & 0x8000u) && (klo_ & 15u) == ln.br;\n"
+                     "    const bool fhi_ = (par_ & 0x80000000u) && (khi_ & 15u) == ln.br;\n";
+                if (n <= 16) {
+                    o << "    bw[" << op.pos / 16 << "] ^= (flo_ ? 1u << (" << op.pos % 16 << " + ilo_) : 0u) | (fhi_ ? 0x10000u << ("
+                      << op.pos % 16 << " + ihi_) : 0u);\n";
+                } else {
+                    for (int k = 0; k < n / 16; k++)
+                        o << "    bw[" << op.pos / 16 + k << "] ^= (flo_ && (ilo_ >> 4) == " << k
+                          << "u ? 1u << (ilo_ & 15u) : 0u) | (fhi_ && (ihi_ >> 4) == " << k
+                          << "u ? 0x10000u << (ihi_ & 15u) : 0u);\n";
+                }
             }
             o << "  }\n";
             break;
         }
         case POLAR_OP_H:
         case POLAR_OP_H0: {
-            unsigned long long m = ((n >= 64) ? ~0ull : ((1ull << n) - 1ull)) << op.pos;
-            o << "  { const u64 m_ = 0x" << std::hex << m << std::dec << "ull; // " << (op.code == POLAR_OP_H ? "H" : "H0")
-              << " pos " << op.pos << " n " << n << "\n";
-            if (op.code == POLAR_OP_H)
-                o << "    bl ^= (bl >> " << n << ") & m_; bh ^= (bh >> " << n << ") & m_; }\n";
-            else
-                o << "    bl = (bl & ~m_) | ((bl >> " << n << ") & m_); bh = (bh & ~m_) | ((bh >> " << n << ") & m_); }\n";
+            const bool h = op.code == POLAR_OP_H;
+            o << "  { // " << (h ? "H" : "H0") << " pos " << op.pos << " n " << n << "\n";
+            if (n >= 16) {
+                for (int k = 0; k < n / 16; k++)
+                    o << "    bw[" << op.pos / 16 + k << "] " << (h ? "^=" : "=") << " bw[" << (op.pos + n) / 16 + k << "];\n";
+            } else {
+                const int j = op.pos / 16;
+                if (h)
+                    o << "    bw[" << j << "] ^= (bw[" << j << "] >> " << n << ") & " << hexmask(op.pos, n) << ";\n";
+                else
+                    o << "    bw[" << j << "] = bsel(" << hexmask(op.pos, n) << ", bw[" << j << "] >> " << n << ", bw[" << j
+                      << "]);\n";
+            }
+            o << "  }\n";
             break;
         }
         default:
@@ -177,19 +228,44 @@ struct Gen {
     std::string run()
     {
         const int N = (int)p.N, G = (int)p.G;
+        // Channel staging: each wave copies its 8 frames (8 x N bytes, contiguous rows of the
+        // [batch][N] input) into LDS with 16-byte loads, then reads the bytes of its lane
+        // (position 16 w + pl of frames row / row + 4) from there, once for the root F and
+        // once for the root G. Frame stride N + 16 bytes keeps the four rows of a read in
+        // different banks.
+        const int FS = N + 16, chunks = N / 2;   // 16-byte chunks per wave
         o << "#include \"polar_sc_device.h\"\nusing namespace polar;\n"
-          << "#define CH(w) conv_pair((u32)chl[16 * (w)] | ((u32)chh[16 * (w)] << 16))\n"
+          << "#define CH(w) sm8_pair(tab_[chl[16 * (w)]], tab_[chh[16 * (w)]])\n"
           << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
-          << "  const int lane = threadIdx.x & 63, row = lane >> 4, pl = lane & 15;\n"
-          << "  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);\n"
+          << "  __shared__ uint4 stage_[4 * 8 * " << FS / 16 << "];\n"
+          << "  __shared__ unsigned char tab_[256];   // channel byte -> SM8\n"
+          << "  tab_[threadIdx.x] = (unsigned char)sm8_of_byte(threadIdx.x);\n"
+          << "  __syncthreads();\n"
+          << "  const int lane = threadIdx.x & 63, row = lane >> 4, pl = lane & 15, wib = threadIdx.x >> 6;\n"
+          << "  const long wave = (long)blockIdx.x * 4 + wib;\n"
           << "  if (wave * 8 >= batch) return;\n"
           << "  const long f_lo = wave * 8 + row, f_hi = wave * 8 + 4 + row;\n"
-          << "  const long fl = f_lo < batch ? f_lo : (long)batch - 1, fh = f_hi < batch ? f_hi : (long)batch - 1;\n"
-          << "  const unsigned char *__restrict__ chl = llr + fl * " << N << " + pl;\n"
-          << "  const unsigned char *__restrict__ chh = llr + fh * " << N << " + pl;\n"
+          << "  unsigned char *st_ = (unsigned char *)stage_ + wib * " << 8 * FS << ";\n"
+          << "  if ((((unsigned long)llr) & 15u) == 0u) {\n"
+          << "    for (int q = lane; q < " << chunks << "; q += 64) {\n"
+          << "      const int f = q / " << N / 16 << ", off = (q % " << N / 16 << ") * 16;\n"
+          << "      const long fr = wave * 8 + f < batch ? wave * 8 + f : (long)batch - 1;\n"
+          << "      *(uint4 *)(st_ + f * " << FS << " + off) = *(const uint4 *)(llr + fr * " << N << " + off);\n"
+          << "    }\n"
+          << "  } else {   // input not 16-byte aligned: byte copy\n"
+          << "    for (int q = lane; q < " << 8 * N << "; q += 64) {\n"
+          << "      const int f = q / " << N << ", off = q % " << N << ";\n"
+          << "      const long fr = wave * 8 + f < batch ? wave * 8 + f : (long)batch - 1;\n"
+          << "      st_[f * " << FS << " + off] = llr[fr * " << N << " + off];\n"
+          << "    }\n"
+          << "  }\n"
+          << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
+          << "  __builtin_amdgcn_wave_barrier();\n"
+          << "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n"
+          << "  const unsigned char *chl = st_ + row * " << FS << " + pl, *chh = st_ + (row + 4) * " << FS << " + pl;\n"
           << "  Lanes ln; ln.init((u32)pl);\n"
-          << "  u64 bl = 0, bh = 0;\n";
+          << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
         for (int d = 1; d < LG; d++) o << "  u32 b" << d << "[" << (1 << d) << "];\n";
         for (const polar_sc_op &op : p.ops) {
             if (op.code == POLAR_OP_END) break;

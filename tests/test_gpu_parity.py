@@ -186,3 +186,17 @@ def test_mask_kernel_equals_interpreter_full_c2(pkg, cuda):
         outs.append(dec.decode(llr).cpu().numpy())
     cuda.cuda.synchronize()
     assert (outs[0] == outs[1]).all()
+
+
+@pytest.mark.parametrize("name", ["FB_N1024_K512", "FB_N128_K64"])
+def test_misaligned_input_pointer(pkg, cuda, oracle_mod, name):
+    """LLR rows handed over at an odd device address (the mask kernel's byte-copy staging)."""
+    mask = util.mask(name)
+    llr, _ = util.synth_frames(mask, 19, ebn0_db=1.0, seed=4)
+    flat = cuda.zeros(llr.size + 16, dtype=cuda.int8, device="cuda")
+    view = flat[3:3 + llr.size].view(llr.shape)
+    view.copy_(cuda.from_numpy(llr))
+    assert view.data_ptr() % 16 == 3
+    dec = make_decoder(pkg, mask, True)
+    got = pkg.unpack_bits(dec.decode(view).cpu().numpy(), mask.size)
+    _assert_same(got, oracle_mod.decode_fsm(mask, llr), "misaligned " + name)
