@@ -28,6 +28,11 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# PMC summary (tools/profile_gpu.sh + tools/pmc_summary.py) of the current C2 kernel: the
+# HBM bytes it reports (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
+# roofline.traffic when the benchmarked configuration is the profiled one.
+TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r01_v4_pmc.json")
+TRAFFIC_PROFILE_CONFIG = ("FB_N1024_K512", 65536)
 
 CONFIGS = {
     # name: (mask fixture, per-GPU frames at N=1 semantics, description)
@@ -104,6 +109,7 @@ def main():
 
     import torch
     import sc_polar_decoder_hls_amd as pkg
+    from sc_polar_decoder_hls_amd import sharding
     import util
 
     rank = int(os.environ.get("RANK", "0"))
@@ -122,16 +128,17 @@ def main():
     name, per_gpu, desc = CONFIGS[args.config]
     mask = util.mask(name)
     N, K = mask.size, int(mask.sum())
+    strong = per_gpu is None     # c4 / c5: a fixed total batch sharded over the ranks
     if args.config == "c4":
-        per_gpu = (1 << 20) // world
+        per_gpu = sharding.shard_bounds(1 << 20, world, rank)[1]
     elif args.config == "c5":
-        per_gpu = max(1, 512 // world)
+        per_gpu = sharding.shard_bounds(512, world, rank)[1]
     if args.batch:
         per_gpu = args.batch
 
     dec = pkg.Decoder(mask)
     dec.prepare(per_gpu)
-    llr, x = gen_frames_torch(torch, mask, per_gpu, args.ebn0, 0xF0 + 7919 * rank, dev)
+    llr, x = gen_frames_torch(torch, mask, per_gpu, args.ebn0, sharding.frame_seed(0xF0, rank), dev)
     out = torch.empty((per_gpu, dec.words), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
@@ -164,12 +171,15 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = sharding.max_over_ranks([elapsed, kern_ms], dist, dev)
+    if dist is not None:   # frames decoded by all ranks (shards may differ by a few frames)
+        cnt = torch.tensor([per_gpu], dtype=torch.float64, device=dev)
+        dist.all_reduce(cnt)
+        frames_all = int(cnt.item())
+    else:
+        frames_all = per_gpu
 
-    total_frames = per_gpu * world * args.steps
+    total_frames = frames_all * args.steps
     fps = total_frames / elapsed
     value = fps * K
 
@@ -180,6 +190,13 @@ def main():
     if rank == 0:
         bytes_per_launch = 1.125 * N * per_gpu
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = None, None
+        if (name, per_gpu) == TRAFFIC_PROFILE_CONFIG and os.path.exists(TRAFFIC_PROFILE):
+            with open(TRAFFIC_PROFILE) as f:
+                prof = json.load(f)
+            if "hbm_read_bytes_corrected" in prof and "hbm_write_bytes" in prof:
+                traffic = prof["hbm_read_bytes_corrected"] + prof["hbm_write_bytes"]
+                traffic_src = os.path.relpath(TRAFFIC_PROFILE, ROOT)
         res = {
             "metric": "decoded info bits/sec + frames/sec, N=1024 K=512 batch, 1/2/4/8 MI355X",
             "value": value,
@@ -190,14 +207,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "int16 sign-magnitude (6-bit LLRs, u8 in / bit-packed out)",
             "data": "synthetic AWGN frames generated on-device (BPSK, Eb/N0=%.1f dB, 4x quantizer, +-31)" % args.ebn0,
             "config": {"workload": desc, "N": N, "K": K, "frames_per_gpu": per_gpu,
                        "mask": name, "parallelism": "frames sharded, dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                         "traffic_source": traffic_src,
                          "kernel": KERNEL_NAMES[dec.stats["storage"]], "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "frame_error_rate": fer,

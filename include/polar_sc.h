@@ -56,8 +56,10 @@ typedef struct polar_sc_config {
 } polar_sc_config;
 
 /* Immutable decode plan: N, config, frozen mask, compiled decode schedule and its device
- * copy. Safe to share read-only between threads; decode calls on different streams may
- * overlap (each call owns its scratch, see polar_sc_decode). */
+ * copy. Safe to share between threads. Decode calls on different streams may overlap for
+ * plans whose stats.storage is 0 or 2 (state in LDS / registers); a storage == 1 plan
+ * (large N, stage LLRs in an HBM scratch owned by the plan) must be used by one stream at a
+ * time on a device -- create one plan per stream to overlap those. */
 typedef struct polar_sc_plan polar_sc_plan;
 
 /* One step of the compiled, data-independent decode schedule (introspection only; the

@@ -14,6 +14,8 @@ SOURCES = [os.path.join(PKG, "csrc", "polar_sc_kernels.hip"), os.path.join(PKG, 
 DEVICE_H = os.path.join(PKG, "csrc", "polar_sc_device.h")
 HEADERS = [os.path.join(ROOT, "include", "polar_sc.h"), DEVICE_H, os.path.join(PKG, "csrc", "polar_sc_plan.hpp")]
 GEN_DIR = os.path.join(PKG, "build")
+CLI_SRC = os.path.join(ROOT, "examples", "polar_decode_cli.c")
+CLI = os.path.join(PKG, "lib", "polar_decode_cli")
 ARCH = os.environ.get("POLAR_SC_ARCH", "gfx950")
 
 
@@ -29,6 +31,18 @@ def needs_build():
         return True
     t = os.path.getmtime(LIB)
     return any(os.path.getmtime(s) > t for s in SOURCES + HEADERS)
+
+
+def build_cli(verbose=False):
+    """Plain-C example caller (examples/polar_decode_cli.c) linked against the library."""
+    if os.path.exists(CLI) and os.path.getmtime(CLI) > max(os.path.getmtime(CLI_SRC), os.path.getmtime(LIB)):
+        return CLI
+    cmd = ["gcc", "-O2", "-Wall", "-I" + os.path.join(ROOT, "include"), CLI_SRC, "-o", CLI,
+           "-L" + os.path.dirname(LIB), "-lpolar_sc", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return CLI
 
 
 def build(force=False, verbose=False):

@@ -1,0 +1,62 @@
+"""Multi-GPU layout of the decode: frames are independent, so a batch is split into
+contiguous per-rank shards (one process per GPU) and every rank decodes its shard with no
+data-path collective. Collectives appear only around the data path: a barrier + max-over-
+ranks for timing, and an optional all-gather of the decoded words for verification.
+
+The reference decodes one frame per top-level call (src/testbench/main.cpp:98-155 loops
+frames through wrapper_in -> my_module -> wrapper_out); a batch of frames is the unit that
+shards here.
+"""
+
+WAVE_FRAMES = 8   # frames per wave64 in the decode kernels; shard starts stay aligned to it
+
+
+def shard_bounds(total, world, rank, align=WAVE_FRAMES):
+    """Contiguous shard [start, start + count) of `total` frames for `rank` of `world`.
+
+    Shards cover 0..total exactly once, differ in size by less than 2 `align` frames (one
+    alignment unit plus the ragged tail), and start
+    on multiples of `align` (so no wave straddles two ranks' halves of a batch)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank %r / world %r" % (rank, world))
+    if total < 0:
+        raise ValueError("negative frame count")
+    units = (total + align - 1) // align
+    base, extra = divmod(units, world)
+    u0 = rank * base + min(rank, extra)
+    u1 = u0 + base + (1 if rank < extra else 0)
+    start = min(total, u0 * align)
+    end = min(total, u1 * align)
+    return start, end - start
+
+
+def frame_seed(base, rank):
+    """Per-rank generator seed for synthetic frames (distinct streams per rank)."""
+    return int(base) + 7919 * int(rank)
+
+
+def max_over_ranks(values, dist=None, device=None):
+    """Element-wise max of a list of floats over all ranks (timing aggregation)."""
+    vals = [float(v) for v in values]
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return vals
+    import torch
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
+
+
+def gather_shards(local, total, dist=None, device=None):
+    """All-gather the per-rank decoded words [count, words] (int64 tensors) into the full
+    [total, words] batch on every rank (verification only; not part of the timed path)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return local
+    import torch
+    world = dist.get_world_size()
+    counts = [shard_bounds(total, world, r)[1] for r in range(world)]
+    cap = max(counts)
+    pad = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device if device is None else device)
+    pad[: local.shape[0]] = local.to(pad.device)
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)

@@ -124,3 +124,24 @@ def test_pack_unpack_bits(pkg):
     for N in (32, 64, 1024, 100):
         b = rng.integers(0, 2, size=(3, N)).astype(np.uint8)
         np.testing.assert_array_equal(pkg.unpack_bits(pkg.pack_bits(b), N), b)
+
+
+def _cli(pkg):
+    from sc_polar_decoder_hls_amd import _build
+    pkg.build()
+    return _build.build_cli()
+
+
+def test_c_cli_stats_generated_mask_format(pkg, tmp_path):
+    """examples/polar_decode_cli.c: plain C through include/polar_sc.h, Generated_Frozen_Bit
+    format (space-separated 0/1 tokens), plan census matches the Python binding."""
+    import subprocess
+    import util
+    mask = util.mask("frozen_n_1024_k_512")
+    p = tmp_path / "frozen_n_1024_k_512.txt"
+    p.write_text(" ".join(str(int(b)) for b in mask))
+    r = subprocess.run([_cli(pkg), str(p), "0", "--stats"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    st = pkg.Decoder(mask).stats
+    assert ("N=1024 K=512 groups=64 R0=%d R1=%d REP=%d SPC=%d RN=%d" %
+            (st["n_r0"], st["n_r1"], st["n_rep"], st["n_spc"], st["n_rn"])) in r.stdout

@@ -1,0 +1,94 @@
+"""Multi-rank decode layout (sc_polar_decoder_hls_amd.sharding) on CPU with gloo, world 2:
+frames shard across ranks with no data-path collective; the gathered result equals a
+single-process decode of the whole batch; timing aggregates as max over ranks."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from sc_polar_decoder_hls_amd import sharding  # noqa: E402
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("total", [0, 1, 7, 8, 9, 64, 1000, 65536, (1 << 20) + 5])
+def test_shard_bounds_cover_disjoint_balanced(world, total):
+    spans = [sharding.shard_bounds(total, world, r) for r in range(world)]
+    pos = 0
+    for start, count in spans:
+        assert start == pos and count >= 0
+        assert start % sharding.WAVE_FRAMES == 0 or count == 0
+        pos += count
+    assert pos == total
+    counts = [c for _, c in spans]
+    assert max(counts) - min(counts) < 2 * sharding.WAVE_FRAMES
+
+
+def test_shard_bounds_rejects_bad_rank():
+    with pytest.raises(ValueError):
+        sharding.shard_bounds(10, 2, 2)
+    with pytest.raises(ValueError):
+        sharding.shard_bounds(-1, 2, 0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, total, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import util
+        from oracle import oracle
+        mask = util.mask("FB_N128_K64")
+        # every rank builds the same global batch (same seed) and decodes only its shard
+        llr, _ = util.synth_frames(mask, total, ebn0_db=1.0, seed=2024)
+        start, count = sharding.shard_bounds(total, world, rank)
+        bits = oracle.decode_fsm(mask, llr[start:start + count]) if count else np.zeros((0, mask.size), np.uint8)
+        words = torch.from_numpy(np.packbits(bits.astype(np.uint8), axis=1, bitorder="little").copy()
+                                 .view(np.int64) if count else np.zeros((0, mask.size // 64), np.int64))
+        full = sharding.gather_shards(words, total, dist)
+        t = sharding.max_over_ranks([0.5 + rank, 3.0 - rank], dist)
+        if rank == 0:
+            ref = oracle.decode_fsm(mask, llr)
+            ref_words = np.packbits(ref.astype(np.uint8), axis=1, bitorder="little").view(np.int64)
+            q.put(("ok", bool(np.array_equal(full.numpy(), ref_words)), t, [sharding.shard_bounds(total, world, r)
+                                                                           for r in range(world)]))
+    except Exception as e:   # surface worker failures to the test
+        q.put(("err", repr(e), None, None))
+        raise
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total", [37, 64])
+def test_two_rank_gloo_shard_decode_gather(oracle_mod, total):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        status, same, t, spans = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert status == "ok", same
+    assert same, "gathered shard decode differs from the single-process decode"
+    assert t == [1.5, 3.0]
+    assert sum(c for _, c in spans) == total
+    assert all(p.exitcode == 0 for p in procs)

@@ -200,3 +200,19 @@ def test_misaligned_input_pointer(pkg, cuda, oracle_mod, name):
     dec = make_decoder(pkg, mask, True)
     got = pkg.unpack_bits(dec.decode(view).cpu().numpy(), mask.size)
     _assert_same(got, oracle_mod.decode_fsm(mask, llr), "misaligned " + name)
+
+
+def test_c_cli_decode_file(pkg, cuda, oracle_mod, tmp_path):
+    """The plain-C example caller decodes an LLR file through polar_sc_decode_host."""
+    import subprocess
+    from sc_polar_decoder_hls_amd import _build
+    mask = util.mask("frozen_n_1024_k_768")
+    tab = tmp_path / "mask.txt"
+    tab.write_text(" ".join(str(int(b)) for b in mask))
+    llr, _ = util.synth_frames(mask, 29, ebn0_db=2.0, seed=29)
+    (tmp_path / "llr.bin").write_bytes(llr.tobytes())
+    r = subprocess.run([_build.build_cli(), str(tab), "0", str(tmp_path / "llr.bin"), str(tmp_path / "x.bin")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    words = np.frombuffer((tmp_path / "x.bin").read_bytes(), dtype=np.uint64).reshape(29, -1)
+    _assert_same(pkg.unpack_bits(words, mask.size), oracle_mod.decode_fsm(mask, llr), "C CLI")

@@ -157,3 +157,41 @@ def test_group_classification(oracle_mod):
     assert L.orc_classify_group(0xFFFE) == 0x04
     for fb in (0x0001, 0x7FFF, 0xC000, 0xFFFC, 0x1234):
         assert L.orc_classify_group(fb) == 0x08
+
+
+def _sm8_of_byte(b):
+    """Mirror of polar::sm8_of_byte (csrc/polar_sc_device.h): the per-mask kernels' LDS table."""
+    t = b & 63
+    m = min(t, 64 - t) & 31
+    return (0x80 if t >= 33 else 0) | m
+
+
+def _sm8_pair(lo, hi):
+    """Mirror of polar::sm8_pair: v_perm duplicates each byte into its half, then & 0x801F801F."""
+    x = (lo & 0xFF) | ((lo & 0xFF) << 8) | ((hi & 0xFF) << 16) | ((hi & 0xFF) << 24)
+    return x & 0x801F801F
+
+
+def _conv_pair(raw):
+    """Mirror of polar::conv_pair (interpreter kernels)."""
+    out = 0
+    for h in (0, 16):
+        t = (raw >> h) & 0x3F
+        m = min(t, (0x40 - t) & 0xFFFF) & 0x1F
+        s = (t + 0x7FDF) & 0x8000
+        out |= (m | s) << h
+    return out
+
+
+def test_device_channel_conversions_match_qconv_all_bytes(oracle_mod):
+    """Every int8 channel byte (the reference keeps the low 6 bits, sc_bigint<6>) converts to
+    the SM value of qconv_format (scalar.h:229-239) under both device formulas."""
+    L = oracle_mod.lib()
+    for b in range(256):
+        q = L.orc_qconv_format(6, b & 63)          # 6-bit SM: bit 5 sign, bits 0..4 magnitude
+        exp16 = ((q >> 5) << 15) | (q & 31)
+        got = _sm8_pair(_sm8_of_byte(b), _sm8_of_byte(255 - b))
+        assert got & 0xFFFF == exp16, b
+        q2 = L.orc_qconv_format(6, (255 - b) & 63)
+        assert got >> 16 == ((q2 >> 5) << 15) | (q2 & 31), b
+        assert _conv_pair(b | ((255 - b) << 16)) == got, b
