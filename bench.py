@@ -118,12 +118,21 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             sys.exit("--gpus %d needs torchrun with %d processes" % (args.gpus, args.gpus))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; local ranks beyond the visible devices wrap (rehearsals on a
+    # 1-GPU box: POLAR_BENCH_BACKEND=gloo torchrun --nproc-per-node 2 bench.py --gpus 2)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     dist = None
+    coll_dev = dev
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("POLAR_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+            coll_dev = torch.device("cpu")
 
     name, per_gpu, desc = CONFIGS[args.config]
     mask = util.mask(name)
@@ -171,9 +180,9 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    elapsed, kern_ms = sharding.max_over_ranks([elapsed, kern_ms], dist, dev)
+    elapsed, kern_ms = sharding.max_over_ranks([elapsed, kern_ms], dist, coll_dev)
     if dist is not None:   # frames decoded by all ranks (shards may differ by a few frames)
-        cnt = torch.tensor([per_gpu], dtype=torch.float64, device=dev)
+        cnt = torch.tensor([per_gpu], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(cnt)
         frames_all = int(cnt.item())
     else:
