@@ -336,6 +336,65 @@ __device__ __forceinline__ u32 leaf_ms(u32 M, u32 S, const Lanes &ln)
 }
 
 // ---------------------------------------------------------------------------------------
+// Split stage words (per-mask kernels): magnitudes as u16 pairs (M) and the signs of 16
+// words packed in one "plane" dword (bit i = low frame of word i, bit 16 + i = high frame),
+// the same layout as the partial sums. F is then one v_pk_min per word plus one XOR per
+// 16 words; G needs the sign plane only as a mask per word (2 ops) and emits the
+// |a| < |b| flags back into a plane.
+// ---------------------------------------------------------------------------------------
+// bit I of each half of plane p -> 0xFFFF / 0 per half
+template <int I>
+__device__ __forceinline__ u32 plane_mask(u32 p)
+{
+    return pk_sra(pk_shl(p, (unsigned short)(15 - I)), 15);
+}
+// bits 15 / 31 of v -> bits I / 16 + I of the plane
+template <int I>
+__device__ __forceinline__ u32 plane_put(u32 acc, u32 v)
+{
+    return ((v >> (15 - I)) & (0x00010001u << I)) | acc;
+}
+// F on the channel (SM16 in, split out)
+template <int I>
+__device__ __forceinline__ u32 F_root(u32 a, u32 b, u32 &S)
+{
+    S = plane_put<I>(S, a ^ b);
+    return pk_min(a & MAG, b & MAG);
+}
+// G on the channel (SM16 in, split out): G_sm<15> with the sign emitted into a plane
+template <int I>
+__device__ __forceinline__ u32 G_root(u32 a, u32 b, u32 u, u32 &S)
+{
+    const u32 ma = a & MAG, mb = b & MAG;
+    const u32 d = pk_sub(ma, mb);
+    const u32 x = a ^ u ^ b;
+    S = plane_put<I>(S, b ^ (x & ~d));
+    return pk_min(bsel(opaque(pk_sra(x, 15)), pk_abs_i16(d), pk_add(ma, mb)), 0x000F000Fu);
+}
+// G on split words: X = plane of sign(a') ^ sign(b); returns the clamped magnitude and puts
+// |a| < |b| into LT. The output sign plane is then sign(b) ^ (X & ~LT) per 16 words.
+template <int I>
+__device__ __forceinline__ u32 G_split(u32 ma, u32 mb, u32 X, u32 &LT)
+{
+    const u32 xm = opaque(plane_mask<I>(X));
+    const u32 d = pk_sub(ma, mb);
+    LT = plane_put<I>(LT, d);
+    return pk_min(bsel(xm, pk_abs_i16(d), pk_add(ma, mb)), 0x000F000Fu);
+}
+// REP word from split parent words: F value + 512 per half, and its SM16 form
+template <int I>
+__device__ __forceinline__ u32 F_split_biased(u32 ma, u32 mb, u32 FS)
+{
+    const u32 m = pk_min(ma, mb), s = plane_mask<I>(FS);
+    return pk_add(pk_sub(m ^ s, s), 0x02000200u);
+}
+template <int I>
+__device__ __forceinline__ u32 F_split_sm(u32 ma, u32 mb, u32 FS)
+{
+    return pk_min(ma, mb) | (plane_mask<I>(FS) & SGN);
+}
+
+// ---------------------------------------------------------------------------------------
 // REP nodes (Spec_REP, functions.h:3086-3107) -- value path. The reference decision is the
 // sign of acc = sat511(... sat511(T_1 + sat511(T_0 + 0)) ...) where T_w is the exact
 // pair-tree sum of word w. Every step is an exact sum or a clamp, so the two's-complement

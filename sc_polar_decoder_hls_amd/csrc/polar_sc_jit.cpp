@@ -34,14 +34,6 @@ struct Gen {
     int LG;
     explicit Gen(const polar_sc_plan &pp) : p(pp), LG(pp.lg) {}
 
-    // word i of the node of depth sd (2^sd words)
-    std::string S(int sd, int i) const
-    {
-        std::ostringstream s;
-        if (sd == LG) s << "CH(" << i << ")";
-        else s << "b" << sd << "[" << i << "]";
-        return s.str();
-    }
     // Partial sums: u32 bw[max(1, G / 16)], dword j = groups 16 j .. 16 j + 15, low frame in
     // bits 0..15 and high frame in bits 16..31 (the layout every consumer wants, so H ops
     // are one or two instructions and the G ops take their u flags without repacking).
@@ -85,14 +77,38 @@ struct Gen {
         return s.str();
     }
 
+    // Stage words below the root are split (polar_sc_device.h): m<d>[i] magnitudes and
+    // s<d>[k] sign planes of words 16k..16k+15. The root reads SM16 channel words CH(i).
+    static int planes(int words) { return words >= 16 ? words / 16 : 1; }
+    static std::string M(int sd, int i)
+    {
+        std::ostringstream s;
+        s << "m" << sd << "[" << i << "]";
+        return s.str();
+    }
+    // sign plane of depth sd shifted so that word i is at bit 0 (bits past the op's words are
+    // don't-care: every consumer reads only the bits of its own words)
+    std::string P(int sd, int i) const
+    {
+        std::ostringstream s;
+        if (i % 16 == 0) s << "s" << sd << "[" << i / 16 << "]";
+        else s << "(s" << sd << "[" << i / 16 << "] >> " << i % 16 << ")";
+        return s.str();
+    }
+    static std::string U(int upos, int k)
+    {
+        return upos >= 0 ? get16(upos + 16 * k) : std::string("0u");
+    }
+
     // After an F-type op (F, FLEAF, REP) the parent words stay live until the matching G.
     // An empty asm that redefines them in place (no instruction) stops the optimiser from
-    // carrying the F op's intermediates (x & MAG, a ^ b) over to the G op, which would
-    // triple the registers held across the whole left subtree.
+    // carrying the F op's intermediates over to the G op, which would multiply the
+    // registers held across the whole left subtree.
     void clobber_parent(int sd, int n)
     {
         if (sd == LG) return;   // root: channel words are re-read from LDS
-        for (int i = 0; i < 2 * n; i++) o << "  asm volatile(\"\" : \"+v\"(b" << sd << "[" << i << "]));\n";
+        for (int i = 0; i < 2 * n; i++) o << "  asm volatile(\"\" : \"+v\"(" << M(sd, i) << "));\n";
+        for (int k = 0; k < planes(2 * n); k++) o << "  asm volatile(\"\" : \"+v\"(s" << sd << "[" << k << "]));\n";
     }
 
     // scheduling fence: keeps the straight-line code from hoisting every load of a long
@@ -102,89 +118,151 @@ struct Gen {
     {
         if ((i & 7) == 7 && i + 1 < n) fence();
     }
+    // X_[k] = sign(a') ^ sign(b) planes of a G-type op on split words
+    void xplanes(int sd, int n, int upos)
+    {
+        const int np = planes(n);
+        o << "    u32 X_[" << np << "], LT_[" << np << "] = {};\n";
+        for (int k = 0; k < np; k++)
+            o << "    X_[" << k << "] = " << P(sd, 16 * k) << " ^ " << P(sd, n + 16 * k) << " ^ " << U(upos, k) << ";\n";
+    }
 
     void op(const polar_sc_op &op)
     {
-        const int sd = LG - op.level, cd = sd - 1, n = op.n;
+        const int sd = LG - op.level, cd = sd - 1, n = op.n, np = planes(n);
+        const bool root = sd == LG;
         fence();
         switch (op.code) {
         case POLAR_OP_F:
-            o << "  // F level " << op.level << " n " << n << "\n";
-            for (int i = 0; i < n; i++) {
-                o << "  b" << cd << "[" << i << "] = F_sm(" << S(sd, i) << ", " << S(sd, n + i) << ");\n";
-                chunk_fence(i, n);
+            o << "  { // F level " << op.level << " n " << n << "\n";
+            if (root) {
+                o << "    u32 P_[" << np << "] = {};\n";
+                for (int i = 0; i < n; i++) {
+                    o << "    " << M(cd, i) << " = F_root<" << i % 16 << ">(CH(" << i << "), CH(" << n + i << "), P_["
+                      << i / 16 << "]);\n";
+                    chunk_fence(i, n);
+                }
+                for (int k = 0; k < np; k++) o << "    s" << cd << "[" << k << "] = P_[" << k << "];\n";
+            } else {
+                for (int i = 0; i < n; i++) {
+                    o << "    " << M(cd, i) << " = pk_min(" << M(sd, i) << ", " << M(sd, n + i) << ");\n";
+                    chunk_fence(i, n);
+                }
+                for (int k = 0; k < np; k++)
+                    o << "    s" << cd << "[" << k << "] = " << P(sd, 16 * k) << " ^ " << P(sd, n + 16 * k) << ";\n";
             }
+            o << "  }\n";
             clobber_parent(sd, n);
             break;
         case POLAR_OP_G:
-            o << "  { // G level " << op.level << " n " << n << " upos " << op.upos << "\n    u32 c_;\n";
-            for (int i = 0; i < n; i++) {
-                ucache(op.upos, i);
-                o << "    b" << cd << "[" << i << "] = G_sm<15>(" << S(sd, i) << ", " << S(sd, n + i) << ", "
-                  << uflag(i) << ");\n";
-                chunk_fence(i, n);
+            o << "  { // G level " << op.level << " n " << n << " upos " << op.upos << "\n";
+            if (root) {
+                o << "    u32 c_, P_[" << np << "] = {};\n";
+                for (int i = 0; i < n; i++) {
+                    ucache(op.upos, i);
+                    o << "    " << M(cd, i) << " = G_root<" << i % 16 << ">(CH(" << i << "), CH(" << n + i << "), "
+                      << uflag(i) << ", P_[" << i / 16 << "]);\n";
+                    chunk_fence(i, n);
+                }
+                for (int k = 0; k < np; k++) o << "    s" << cd << "[" << k << "] = P_[" << k << "];\n";
+            } else {
+                xplanes(sd, n, op.upos);
+                for (int i = 0; i < n; i++) {
+                    o << "    " << M(cd, i) << " = G_split<" << i % 16 << ">(" << M(sd, i) << ", " << M(sd, n + i) << ", X_["
+                      << i / 16 << "], LT_[" << i / 16 << "]);\n";
+                    chunk_fence(i, n);
+                }
+                for (int k = 0; k < np; k++)
+                    o << "    s" << cd << "[" << k << "] = " << P(sd, n + 16 * k) << " ^ (X_[" << k << "] & ~LT_[" << k
+                      << "]);\n";
             }
             o << "  }\n";
             break;
         case POLAR_OP_FLEAF:
         case POLAR_OP_GLEAF: {
-            o << "  { // " << (op.code == POLAR_OP_FLEAF ? "F" : "G") << "+leaf pos " << op.pos << " fb 0x" << std::hex
-              << op.fb << std::dec << "\n";
-            if (op.code == POLAR_OP_FLEAF) {
-                o << "    const u32 a_ = " << S(sd, 0) << ", b_ = " << S(sd, 1) << ";\n"
-                  << "    const u32 M_ = pk_min(a_ & MAG, b_ & MAG), S_ = pk_sra(a_ ^ b_, 15);\n";
+            const bool f = op.code == POLAR_OP_FLEAF;
+            o << "  { // " << (f ? "F" : "G") << "+leaf pos " << op.pos << " fb 0x" << std::hex << op.fb << std::dec << "\n";
+            if (root) {
+                if (f) {
+                    o << "    const u32 a_ = CH(0), b_ = CH(1);\n"
+                      << "    const u32 M_ = pk_min(a_ & MAG, b_ & MAG), S_ = pk_sra(a_ ^ b_, 15);\n";
+                } else {
+                    o << "    u32 c_; ";
+                    ucache(op.upos, 0);
+                    o << "    const u32 L_ = G_sm<15>(CH(0), CH(1), " << uflag(0) << ");\n"
+                      << "    const u32 M_ = L_ & MAG, S_ = pk_sra(L_, 15);\n";
+                }
+            } else if (f) {
+                o << "    const u32 M_ = pk_min(" << M(sd, 0) << ", " << M(sd, 1) << ");\n"
+                  << "    const u32 S_ = plane_mask<0>(" << P(sd, 0) << " ^ " << P(sd, 1) << ");\n";
             } else {
-                o << "    u32 c_; ";
-                ucache(op.upos, 0);
-                o << "    const u32 L_ = G_sm<15>(" << S(sd, 0) << ", " << S(sd, 1) << ", " << uflag(0) << ");\n"
-                  << "    const u32 M_ = L_ & MAG, S_ = pk_sra(L_, 15);\n";
+                o << "    const u32 xm_ = opaque(plane_mask<0>(" << P(sd, 0) << " ^ " << P(sd, 1) << " ^ " << U(op.upos, 0)
+                  << "));\n"
+                  << "    const u32 d_ = pk_sub(" << M(sd, 0) << ", " << M(sd, 1) << ");\n"
+                  << "    const u32 M_ = pk_min(bsel(xm_, pk_abs_i16(d_), pk_add(" << M(sd, 0) << ", " << M(sd, 1)
+                  << ")), 0x000F000Fu);\n"
+                  << "    const u32 S_ = plane_mask<0>(" << P(sd, 1) << ") ^ (xm_ & ~pk_sra(d_, 15));\n";
             }
             o << "    const u32 x_ = leaf_ms<0x" << std::hex << op.fb << std::dec << "u, 0, 16>(M_, S_, ln);\n";
             put(op.pos, 1, "x_ & 0x00010001u");
             o << "  }\n";
-            if (op.code == POLAR_OP_FLEAF) clobber_parent(sd, 1);
+            if (f) clobber_parent(sd, 1);
             break;
         }
-        case POLAR_OP_REP:
+        case POLAR_OP_REP: {
             // value chain in two's complement; the exact SM chain only when a total is 0
-            o << "  { // REP n " << n << " pos " << op.pos << "\n    u32 acc_ = 0u, full_;\n";
+            o << "  { // REP n " << n << " pos " << op.pos << "\n    u32 acc_ = 0u, full_, FS_[" << np << "];\n";
+            for (int k = 0; k < np; k++)
+                o << "    FS_[" << k << "] = " << P(sd, 16 * k) << " ^ " << P(sd, n + 16 * k) << ";\n";
             for (int i = 0; i < n; i++) {
-                o << "    acc_ = rep_acc(acc_, row_sum_biased(F_biased(" << S(sd, i) << ", " << S(sd, n + i) << ")));\n";
+                o << "    acc_ = rep_acc(acc_, row_sum_biased(F_split_biased<" << i % 16 << ">(" << M(sd, i) << ", "
+                  << M(sd, n + i) << ", FS_[" << i / 16 << "])));\n";
                 chunk_fence(i, n);
             }
             o << "    if (rep_any_zero(acc_)) {\n      acc_ = 0u;\n";
             for (int i = 0; i < n; i++)
-                o << "      acc_ = G_sm<511>(row_add_tree(F_sm(" << S(sd, i) << ", " << S(sd, n + i) << "), ln), acc_, 0u);\n";
+                o << "      acc_ = G_sm<511>(row_add_tree(F_split_sm<" << i % 16 << ">(" << M(sd, i) << ", " << M(sd, n + i)
+                  << ", FS_[" << i / 16 << "]), ln), acc_, 0u);\n";
             // two's complement or SM16: the hard decision is bit 15 / 31 either way
             o << "    }\n    full_ = pk_sra(acc_, 15);\n";
             for (int j = 0; j < n; j += 16) put(op.pos + j, n < 16 ? n : 16, "full_");
             o << "  }\n";
             clobber_parent(sd, n);
             break;
+        }
         case POLAR_OP_R1:
         case POLAR_OP_SPC: {
             const bool spc = op.code == POLAR_OP_SPC;
-            o << "  { // " << (spc ? "SPC" : "R1") << " n " << n << " pos " << op.pos << " upos " << op.upos
-              << "\n    u32 c_, acc_ = 0u, par_ = 0u, klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu;\n";
+            o << "  { // " << (spc ? "SPC" : "R1") << " n " << n << " pos " << op.pos << " upos " << op.upos << "\n";
+            xplanes(sd, n, op.upos);
+            if (spc) o << "    u32 klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu, par_ = 0u;\n";
             for (int i = 0; i < n; i++) {
-                ucache(op.upos, i);
-                o << "    { const u32 " << (spc ? "l_ = G_sm<15>(" : "h_ = G_sign(") << S(sd, i) << ", " << S(sd, n + i)
-                  << ", " << uflag(i) << ");" << (spc ? " const u32 h_ = l_ & SGN;" : "") << " acc_ |= h_ >> "
-                  << (15 - (i & 15)) << ";";
                 if (spc)
-                    o << " par_ ^= h_; klo_ = __builtin_elementwise_min(klo_, ((l_ & 0x1Fu) << 24) | " << (i << 4)
-                      << "u); khi_ = __builtin_elementwise_min(khi_, (((l_ >> 16) & 0x1Fu) << 24) | " << (i << 4)
-                      << "u);";
-                o << " }\n";
+                    o << "    { const u32 l_ = G_split<" << i % 16 << ">(" << M(sd, i) << ", " << M(sd, n + i) << ", X_["
+                      << i / 16 << "], LT_[" << i / 16 << "]);\n"
+                      << "      klo_ = __builtin_elementwise_min(klo_, (l_ << 24) | " << (i << 4) << "u);\n"
+                      << "      khi_ = __builtin_elementwise_min(khi_, ((l_ >> 16) << 24) | " << (i << 4) << "u); }\n";
+                else
+                    o << "    LT_[" << i / 16 << "] = plane_put<" << i % 16 << ">(LT_[" << i / 16 << "], pk_sub(" << M(sd, i)
+                      << ", " << M(sd, n + i) << "));\n";
                 chunk_fence(i, n);
-                if ((i & 15) == 15 || i == n - 1) {
-                    put(op.pos + (i & ~15), n < 16 ? n : 16, "acc_");
-                    o << "    acc_ = 0u;\n";
-                }
+            }
+            // hard decisions: sign(b) ^ (X & ~LT), already in partial-sum layout
+            for (int k = 0; k < np; k++) {
+                o << "    { const u32 h_ = " << P(sd, n + 16 * k) << " ^ (X_[" << k << "] & ~LT_[" << k << "]);\n";
+                put(op.pos + 16 * k, n < 16 ? n : 16, "h_");
+                if (spc) o << "      par_ ^= h_; }\n";
+                else o << "    }\n";
             }
             if (spc) {
-                // flip the partial sum at the least reliable position when the parity is odd
-                o << "    par_ = row_xor(par_);\n"
+                // parity of each frame's hard decisions; flip the partial sum at the least
+                // reliable position when it is odd
+                if (n < 16) {
+                    const unsigned m = (1u << n) - 1u;
+                    o << "    par_ &= 0x" << std::hex << (m | (m << 16)) << std::dec << "u;\n";
+                }
+                o << "    par_ = ((__builtin_popcount(par_ & 0xFFFFu) & 1u) << 15) | ((__builtin_popcount(par_ >> 16) & 1u) << 31);\n"
+                     "    par_ = row_xor(par_);\n"
                      "    klo_ = row_min_u32(klo_ | ln.br); khi_ = row_min_u32(khi_ | ln.br);\n"
                      "    const u32 ilo_ = (klo_ >> 4) & 0xFFFFFu, ihi_ = (khi_ >> 4) & 0xFFFFFu;\n"
                      "    const bool flo_ = (par_ & 0x8000u) && (klo_ & 15u) == ln.br;\n"
@@ -266,7 +344,8 @@ struct Gen {
           << "  const unsigned char *chl = st_ + row * " << FS << " + pl, *chh = st_ + (row + 4) * " << FS << " + pl;\n"
           << "  Lanes ln; ln.init((u32)pl);\n"
           << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
-        for (int d = 1; d < LG; d++) o << "  u32 b" << d << "[" << (1 << d) << "];\n";
+        for (int d = 1; d < LG; d++)
+            o << "  u32 m" << d << "[" << (1 << d) << "], s" << d << "[" << planes(1 << d) << "];\n";
         for (const polar_sc_op &op : p.ops) {
             if (op.code == POLAR_OP_END) break;
             this->op(op);
