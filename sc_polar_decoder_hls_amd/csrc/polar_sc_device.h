@@ -24,6 +24,9 @@ __device__ __forceinline__ u32 U(u16x2 v) { return __builtin_bit_cast(u32, v); }
 __device__ __forceinline__ u16x2 V(u32 v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ u32 pk_min(u32 a, u32 b) { return U(__builtin_elementwise_min(V(a), V(b))); }
 __device__ __forceinline__ u32 pk_add(u32 a, u32 b) { return U(V(a) + V(b)); }
+__device__ __forceinline__ u32 pk_max_u16(u32 a, u32 b) { return U(__builtin_elementwise_max(V(a), V(b))); }
+// a * b + c per 16-bit half, modulo 2^16 (v_pk_mad_u16)
+__device__ __forceinline__ u32 pk_mad_u16(u32 a, u32 b, u32 c) { return U(V(a) * V(b) + V(c)); }
 __device__ __forceinline__ u32 pk_sub(u32 a, u32 b) { return U(V(a) - V(b)); }
 __device__ __forceinline__ u32 pk_sra(u32 a, short s)
 {
@@ -75,10 +78,24 @@ __device__ __forceinline__ u32 G_sm(u32 a, u32 b, u32 u)
 }
 
 // ---------------------------------------------------------------------------------------
-// cross-lane exchange inside a 16-lane DPP row: value of lane (l ^ H)
+// cross-lane exchange inside a 16-lane DPP row
 // ---------------------------------------------------------------------------------------
+// Lane order. POLAR_LANE_REMAP = 0: lane l of a row holds word position l. With 1 (the
+// per-mask kernels), positions 4..7 and 12..15 sit mirrored in their quad
+// (lane = p ^ (p & 4 ? 3 : 0), an involution). Partners at position distance 8 / 4 / 2 / 1
+// are then lanes l^8 (row_ror:8), l^7 (row_half_mirror), l^2, l^1 (quad_perm): one DPP
+// each, where the identity order needs two for distance 4.
+#ifndef POLAR_LANE_REMAP
+#define POLAR_LANE_REMAP 0
+#endif
+__device__ __forceinline__ u32 lane_pos(u32 lane)
+{
+    return POLAR_LANE_REMAP ? (lane ^ ((lane & 4u) ? 3u : 0u)) : lane;
+}
+
+// value of physical lane (l ^ H)
 template <int H>
-__device__ __forceinline__ u32 xorlane(u32 v)
+__device__ __forceinline__ u32 xorlane_phys(u32 v)
 {
     if constexpr (H == 1) {
         return __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
@@ -92,13 +109,23 @@ __device__ __forceinline__ u32 xorlane(u32 v)
         return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, true);  // row_ror:8
     }
 }
+// value at word-position distance H (the partner of the leaf / pair-tree recursions)
+template <int H>
+__device__ __forceinline__ u32 xorlane(u32 v)
+{
+    if constexpr (POLAR_LANE_REMAP && H == 4)
+        return __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, true);   // row_half_mirror: l^7
+    else
+        return xorlane_phys<H>(v);
+}
 
 // per-lane constants: all-ones where the lane is the lower ("a") member of its pair at
-// distance H
+// word-position distance H
 struct Lanes {
     u32 a1, a2, a4, a8;   // lane masks
-    u32 pl;               // PAR lane 0..15
-    u32 br;               // bitrev4(pl)
+    u32 pl;               // physical lane in the row, 0..15
+    u32 pos;              // word position held by this lane (lane_pos(pl))
+    u32 br;               // bitrev4(pos)
     template <int H> __device__ __forceinline__ u32 amask() const
     {
         if constexpr (H == 1) return a1;
@@ -109,13 +136,23 @@ struct Lanes {
     __device__ __forceinline__ void init(u32 p)
     {
         pl = p;
-        br = ((p & 1u) << 3) | ((p & 2u) << 1) | ((p & 4u) >> 1) | ((p & 8u) >> 3);
-        a1 = (p & 1u) ? 0u : 0xFFFFFFFFu;
-        a2 = (p & 2u) ? 0u : 0xFFFFFFFFu;
-        a4 = (p & 4u) ? 0u : 0xFFFFFFFFu;
-        a8 = (p & 8u) ? 0u : 0xFFFFFFFFu;
+        pos = lane_pos(p);
+        br = ((pos & 1u) << 3) | ((pos & 2u) << 1) | ((pos & 4u) >> 1) | ((pos & 8u) >> 3);
+        a1 = (pos & 1u) ? 0u : 0xFFFFFFFFu;
+        a2 = (pos & 2u) ? 0u : 0xFFFFFFFFu;
+        a4 = (pos & 4u) ? 0u : 0xFFFFFFFFu;
+        a8 = (pos & 8u) ? 0u : 0xFFFFFFFFu;
     }
 };
+
+// per-lane data back to identity lane order (lane p receives position p's value)
+__device__ __forceinline__ u32 to_position_order(u32 v, const Lanes &ln)
+{
+    if constexpr (POLAR_LANE_REMAP)
+        return bselo(ln.a4, v, __builtin_amdgcn_update_dpp(0u, v, 0x1B, 0xF, 0xF, true));  // quad mirror
+    else
+        return v;
+}
 
 // ---------------------------------------------------------------------------------------
 // Leaf: Spec_PolarDec_16 -> Spec_P16_ext<6> (functions.h:521-546, 413-492, 366-384):
@@ -231,10 +268,10 @@ __device__ __forceinline__ u32 row_xor(u32 v)
 __device__ __forceinline__ u32 row_transpose16(u32 v, const Lanes &ln)
 {
     u32 p;
-    p = xorlane<8>(v); v = bsel(ln.a8, (v & 0x00FF00FFu) | ((p & 0x00FF00FFu) << 8), ((p >> 8) & 0x00FF00FFu) | (v & 0xFF00FF00u));
-    p = xorlane<4>(v); v = bsel(ln.a4, (v & 0x0F0F0F0Fu) | ((p & 0x0F0F0F0Fu) << 4), ((p >> 4) & 0x0F0F0F0Fu) | (v & 0xF0F0F0F0u));
-    p = xorlane<2>(v); v = bsel(ln.a2, (v & 0x33333333u) | ((p & 0x33333333u) << 2), ((p >> 2) & 0x33333333u) | (v & 0xCCCCCCCCu));
-    p = xorlane<1>(v); v = bsel(ln.a1, (v & 0x55555555u) | ((p & 0x55555555u) << 1), ((p >> 1) & 0x55555555u) | (v & 0xAAAAAAAAu));
+    p = xorlane_phys<8>(v); v = bsel((((ln.pl & 8u) != 0u) ? 0u : 0xFFFFFFFFu), (v & 0x00FF00FFu) | ((p & 0x00FF00FFu) << 8), ((p >> 8) & 0x00FF00FFu) | (v & 0xFF00FF00u));
+    p = xorlane_phys<4>(v); v = bsel((((ln.pl & 4u) != 0u) ? 0u : 0xFFFFFFFFu), (v & 0x0F0F0F0Fu) | ((p & 0x0F0F0F0Fu) << 4), ((p >> 4) & 0x0F0F0F0Fu) | (v & 0xF0F0F0F0u));
+    p = xorlane_phys<2>(v); v = bsel((((ln.pl & 2u) != 0u) ? 0u : 0xFFFFFFFFu), (v & 0x33333333u) | ((p & 0x33333333u) << 2), ((p >> 2) & 0x33333333u) | (v & 0xCCCCCCCCu));
+    p = xorlane_phys<1>(v); v = bsel((((ln.pl & 1u) != 0u) ? 0u : 0xFFFFFFFFu), (v & 0x55555555u) | ((p & 0x55555555u) << 1), ((p >> 1) & 0x55555555u) | (v & 0xAAAAAAAAu));
     return v;
 }
 
@@ -325,11 +362,12 @@ __device__ __forceinline__ u32 leaf_ms(u32 M, u32 S, const Lanes &ln)
         constexpr int H = W / 2;
         const u32 PM = xorlane<H>(M), PS = xorlane<H>(S);
         const u32 SF = S ^ PS;
-        const u32 xa = leaf_ms<FB, B, H>(pk_min(M, PM), SF, ln);
+        const u32 Mf = pk_min(M, PM);
+        const u32 xa = leaf_ms<FB, B, H>(Mf, SF, ln);
         const u32 x = opaque(SF ^ xorlane<H>(xa));
-        const u32 d = pk_sub(PM, M);
-        const u32 lt = opaque(pk_sra(d, 15));
-        const u32 Mb = bsel(x, pk_sub(d ^ lt, lt), pk_add(PM, M));
+        const u32 lt = opaque(pk_sra(pk_sub(PM, M), 15));
+        // magnitude: signs differ -> max - min, else max + min  (min = the F magnitude)
+        const u32 Mb = pk_mad_u16(Mf, x | 0x00010001u, pk_max_u16(M, PM));
         const u32 xb = leaf_ms<FB, B + H, H>(Mb, S ^ (x & ~lt), ln);
         return bselo(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
     }

@@ -312,7 +312,7 @@ struct Gen {
         // once for the root G. Frame stride N + 16 bytes keeps the four rows of a read in
         // different banks.
         const int FS = N + 16, chunks = N / 2;   // 16-byte chunks per wave
-        o << "#include \"polar_sc_device.h\"\nusing namespace polar;\n"
+        o << "#define POLAR_LANE_REMAP 1\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
           << "#define CH(w) sm8_pair(tab_[chl[16 * (w)]], tab_[chh[16 * (w)]])\n"
           << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
@@ -341,8 +341,9 @@ struct Gen {
           << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
           << "  __builtin_amdgcn_wave_barrier();\n"
           << "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n"
-          << "  const unsigned char *chl = st_ + row * " << FS << " + pl, *chh = st_ + (row + 4) * " << FS << " + pl;\n"
           << "  Lanes ln; ln.init((u32)pl);\n"
+          << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
+          << " + ln.pos;\n"
           << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
         for (int d = 1; d < LG; d++)
             o << "  u32 m" << d << "[" << (1 << d) << "], s" << d << "[" << planes(1 << d) << "];\n";
@@ -354,7 +355,7 @@ struct Gen {
         o << "  const bool st_lo = f_lo < batch, st_hi = f_hi < batch;\n"
           << "  unsigned short *o_lo = out + (size_t)f_lo * out_stride, *o_hi = out + (size_t)f_hi * out_stride;\n";
         for (int c = 0; c < (G + 15) / 16; c++) {
-            o << "  { const u32 t_ = row_transpose16(" << get16(16 * c) << ", ln); const int w_ = " << 16 * c << " + pl;\n"
+            o << "  { const u32 t_ = row_transpose16(to_position_order(" << get16(16 * c) << ", ln), ln); const int w_ = " << 16 * c << " + pl;\n"
               << "    if (w_ < " << G << ") { if (st_lo) o_lo[w_] = (unsigned short)(t_ & 0xFFFFu); "
               << "if (st_hi) o_hi[w_] = (unsigned short)(t_ >> 16); } }\n";
         }
