@@ -31,7 +31,12 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # PMC summary (tools/profile_gpu.sh + tools/pmc_summary.py) of the current C2 kernel: the
 # HBM bytes it reports (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
 # roofline.traffic when the benchmarked configuration is the profiled one.
-TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r01_v4_pmc.json")
+TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r01_v6_pmc.json")
+# VALU issue cost on gfx950 measured by tools/valu_microbench.hip (profiles/
+# r01_valu_microbench.log): 4.2-4.7 cycles per wave64 instruction for the packed-16 / logic /
+# DPP classes the decoder issues (8 waves per SIMD, independent chains)
+VALU_CYCLES_PER_INST = 4.4
+NOMINAL_CLOCK_GHZ = 2.4
 TRAFFIC_PROFILE_CONFIG = ("FB_N1024_K512", 65536)
 
 CONFIGS = {
@@ -217,13 +222,25 @@ def main():
     if rank == 0:
         bytes_per_launch = 1.125 * N * per_gpu
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = None, None
+        traffic, traffic_src, valu = None, None, None
         if (name, per_gpu) == TRAFFIC_PROFILE_CONFIG and os.path.exists(TRAFFIC_PROFILE):
             with open(TRAFFIC_PROFILE) as f:
                 prof = json.load(f)
             if "hbm_read_bytes_corrected" in prof and "hbm_write_bytes" in prof:
                 traffic = prof["hbm_read_bytes_corrected"] + prof["hbm_write_bytes"]
                 traffic_src = os.path.relpath(TRAFFIC_PROFILE, ROOT)
+            if "valu_insts_per_wave" in prof:
+                # supplementary: the bound that actually limits this kernel
+                simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+                waves = (per_gpu + 7) // 8
+                rate = waves * prof["valu_insts_per_wave"] / (kern_ms * 1e-3)
+                peak = simds * NOMINAL_CLOCK_GHZ * 1e9 / VALU_CYCLES_PER_INST
+                valu = {"insts_per_wave": prof["valu_insts_per_wave"], "waves_per_launch": waves,
+                        "achieved": rate, "peak": peak, "unit": "wave-instructions/s", "frac": rate / peak,
+                        "peak_basis": "%d SIMDs x %.1f GHz / %.1f cycles per wave64 VALU instruction "
+                                      "(profiles/r01_valu_microbench.log)" % (simds, NOMINAL_CLOCK_GHZ,
+                                                                             VALU_CYCLES_PER_INST),
+                        "source": os.path.relpath(TRAFFIC_PROFILE, ROOT)}
         res = {
             "metric": "decoded info bits/sec + frames/sec, N=1024 K=512 batch, 1/2/4/8 MI355X",
             "value": value,
@@ -245,6 +262,7 @@ def main():
                          "traffic_source": traffic_src,
                          "kernel": KERNEL_NAMES[dec.stats["storage"]], "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": bytes_per_launch},
+            "valu_roofline": valu,
             "frame_error_rate": fer,
             "parity_check": check,
         }
