@@ -19,7 +19,8 @@
 
 extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out, const void *ops,
                                       uint32_t *scratch, int N, long batch, int out_stride,
-                                      int waves_per_block, int wave_dwords, void *stream);
+                                      int waves_per_group, int groups_per_block, int group_dwords,
+                                      void *stream);
 extern "C" int polar_sc_launch_selftest(uint32_t *out_dev);
 
 using polar_host::DevState;
@@ -138,6 +139,11 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
     if (hipGetDevice(&dev) != hipSuccess) return -EIO;
     std::lock_guard<std::mutex> lk(p->mu);
     DevState &st = p->dev[dev];
+    if (st.simds == 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        st.simds = 4 * cus;
+    }
     if (p->jit) {
         int rc = polar_host::jit_load(*p, st);
         if (rc) return rc;
@@ -167,6 +173,24 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
     return 0;
 }
 
+// Interpreter launches: waves per 8-frame group. Large batches keep one wave per group;
+// when the groups cannot fill the GPU (about 2 waves per SIMD), a group gets up to 16 waves
+// that split its wide ops (polar_sc_kernels.hip). POLAR_SC_WAVES_PER_GROUP overrides.
+int waves_per_group(const polar_sc_plan *p, size_t batch, int simds)
+{
+    const char *env = std::getenv("POLAR_SC_WAVES_PER_GROUP");
+    if (env && *env) {
+        int w = std::atoi(env);
+        if (w >= 1 && w <= 16 && (w & (w - 1)) == 0) return w;
+    }
+    const size_t groups = (batch + 7) / 8;
+    const size_t target = 2u * (size_t)(simds > 0 ? simds : 1024);
+    int w = 1;
+    while (w < 16 && groups * (size_t)w < target) w *= 2;
+    (void)p;
+    return w;
+}
+
 int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size_t batch,
                   int out_stride, void *stream)
 {
@@ -177,8 +201,9 @@ int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size
     int rc = ensure_device(p, batch, &st);
     if (rc) return rc;
     if (p->jit) return polar_host::jit_launch(*p, *st, llr, out, (long)batch, out_stride, stream);
+    const int wpg = waves_per_group(p, batch, st->simds);
     rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, (uint32_t *)st->scratch, (int)p->N, (long)batch,
-                                out_stride, p->waves_per_block, p->wave_dwords, stream);
+                                out_stride, wpg, 1, p->wave_dwords, stream);
     return rc ? -EIO : 0;
 }
 
@@ -281,7 +306,6 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     p->wave_dwords = (int)((nslot + nbd) * 64u);
     const uint64_t wave_bytes = (uint64_t)p->wave_dwords * 4u;
     p->gmem = wave_bytes > LDS_WAVE_LIMIT ? 1 : 0;
-    p->waves_per_block = 1;
     while ((1u << p->lg) < p->G) p->lg++;
     // per-mask register kernel for N <= 1024 unless POLAR_SC_JIT=0 (schedule interpreter)
     const char *jit_env = std::getenv("POLAR_SC_JIT");

@@ -79,66 +79,65 @@ __device__ __forceinline__ void bits_put_small(const Ctx &c, int pos, int n, uin
 // ---------------------------------------------------------------------------------------
 // Ops
 // ---------------------------------------------------------------------------------------
-// F_STATE / G_STATE word loops (my_module.h:373-445, 704-781) for n >= 2 output words:
-// dst[i] = F(src[i], src[n+i]) or G(src[i], src[n+i], bit_mem[upos+i]).
-template <bool ISG>
-__device__ __forceinline__ void op_fg(const Ctx &c, int k, int n, int upos)
+template <bool ISG, bool ROOT>
+__device__ __forceinline__ void fg_words(const Ctx &c, int k, int n, int upos, int i0, int i1)
 {
     const int dst = c.lvl_off(k + 1);
-    uint32_t ud = 0;
-    if (k == 0) {
-        for (int i = 0; i < n; i++) {
-            uint32_t a = c.chan(i), b = c.chan(n + i);
-            uint32_t r;
-            if constexpr (ISG) {
-                uint32_t u = 0;
-                if (upos >= 0) {
-                    if (((upos + i) & 15) == 0 || i == 0) ud = c.bld((upos + i) >> 4);
-                    u = ubit(ud, upos + i);
-                }
-                r = G_sm<15>(a, b, u);
-            } else {
-                r = F_sm(a, b);
-            }
-            c.st(dst + i, r);
+    const int s0 = ROOT ? 0 : c.lvl_off(k);
+    auto src = [&](int w) -> uint32_t {
+        if constexpr (ROOT) return c.chan(w);
+        else return c.ld(s0 + w);
+    };
+    int i = i0;
+    // 8 words per iteration: 16 independent source loads in flight (HBM latency)
+    for (; i + 8 <= i1; i += 8) {
+        uint32_t a[8], b[8], r[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a[j] = src(i + j);
+            b[j] = src(n + i + j);
         }
-        return;
-    }
-    const int s0 = c.lvl_off(k);
-    int i = 0;
-    for (; i + 4 <= n; i += 4) {
-        uint32_t a0 = c.ld(s0 + i), a1 = c.ld(s0 + i + 1), a2 = c.ld(s0 + i + 2), a3 = c.ld(s0 + i + 3);
-        uint32_t b0 = c.ld(s0 + n + i), b1 = c.ld(s0 + n + i + 1), b2 = c.ld(s0 + n + i + 2), b3 = c.ld(s0 + n + i + 3);
-        uint32_t r0, r1, r2, r3;
         if constexpr (ISG) {
-            uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
+            // partial sums of words upos+i .. upos+i+7 (at most two bit dwords)
+            uint32_t u0 = 0, u1 = 0;
             if (upos >= 0) {
-                if (((upos + i) & 15) == 0 || i == 0) ud = c.bld((upos + i) >> 4);
-                u0 = ubit(ud, upos + i); u1 = ubit(ud, upos + i + 1);
-                u2 = ubit(ud, upos + i + 2); u3 = ubit(ud, upos + i + 3);
+                u0 = c.bld((upos + i) >> 4);
+                u1 = c.bld((upos + i + 7) >> 4);
             }
-            r0 = G_sm<15>(a0, b0, u0); r1 = G_sm<15>(a1, b1, u1);
-            r2 = G_sm<15>(a2, b2, u2); r3 = G_sm<15>(a3, b3, u3);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int q = upos + i + j;
+                const uint32_t u = (upos >= 0) ? ubit(((q >> 4) == ((upos + i) >> 4)) ? u0 : u1, q) : 0u;
+                r[j] = G_sm<15>(a[j], b[j], u);
+            }
         } else {
-            r0 = F_sm(a0, b0); r1 = F_sm(a1, b1); r2 = F_sm(a2, b2); r3 = F_sm(a3, b3);
+#pragma unroll
+            for (int j = 0; j < 8; j++) r[j] = F_sm(a[j], b[j]);
         }
-        c.st(dst + i, r0); c.st(dst + i + 1, r1); c.st(dst + i + 2, r2); c.st(dst + i + 3, r3);
+#pragma unroll
+        for (int j = 0; j < 8; j++) c.st(dst + i + j, r[j]);
     }
-    for (; i < n; i++) {
-        uint32_t a = c.ld(s0 + i), b = c.ld(s0 + n + i);
+    for (; i < i1; i++) {
+        const uint32_t a = src(i), b = src(n + i);
         uint32_t r;
         if constexpr (ISG) {
-            uint32_t u = 0;
-            if (upos >= 0) {
-                if (((upos + i) & 15) == 0 || i == 0) ud = c.bld((upos + i) >> 4);
-                u = ubit(ud, upos + i);
-            }
+            const uint32_t u = (upos >= 0) ? ubit(c.bld((upos + i) >> 4), upos + i) : 0u;
             r = G_sm<15>(a, b, u);
         } else {
             r = F_sm(a, b);
         }
         c.st(dst + i, r);
     }
+}
+
+// F_STATE / G_STATE word loops (my_module.h:373-445, 704-781) for n >= 2 output words:
+// dst[i] = F(src[i], src[n+i]) or G(src[i], src[n+i], bit_mem[upos+i]), i in [i0, i1)
+// (the words of this wave when the op is split across the waves of a group).
+template <bool ISG>
+__device__ __forceinline__ void op_fg(const Ctx &c, int k, int n, int upos, int i0, int i1)
+{
+    if (k == 0) fg_words<ISG, true>(c, k, n, upos, i0, i1);
+    else fg_words<ISG, false>(c, k, n, upos, i0, i1);
 }
 
 // F/G with NB_ITER = 1 followed by R_STATE: Spec_Polar_Decoder on reg_result
@@ -186,16 +185,17 @@ __device__ __forceinline__ void op_rep(const Ctx &c, int k, int n, int pos)
 // lambda = G(parent, bits[upos..]); x = sign(lambda); SPC additionally flips the first
 // minimum-|lambda| position (lexicographic (|l|, word, bitrev4(lane)) == Min_Mask_16_SM
 // tournament + strict '<' across words) when the parity of x is odd.
+// [i0, i1): the words of this wave (R1 split in whole 16-word chunks; SPC is never split).
 template <bool SPC>
-__device__ __forceinline__ void op_r1spc(const Ctx &c, int k, int n, int upos, int pos)
+__device__ __forceinline__ void op_r1spc(const Ctx &c, int k, int n, int upos, int pos, int i0, int i1)
 {
     const int s0 = c.lvl_off(k);
     uint32_t ud = 0, acc = 0, par = 0;
     uint32_t key_lo = 0xFFFFFFFFu, key_hi = 0xFFFFFFFFu;
-    for (int i = 0; i < n; i++) {
+    for (int i = i0; i < i1; i++) {
         uint32_t u = 0;
         if (upos >= 0) {
-            if (((upos + i) & 15) == 0 || i == 0) ud = c.bld((upos + i) >> 4);
+            if (((upos + i) & 15) == 0 || i == i0) ud = c.bld((upos + i) >> 4);
             u = ubit(ud, upos + i);
         }
         uint32_t lam = G_sm<15>(c.ld(s0 + i), c.ld(s0 + n + i), u);
@@ -232,12 +232,13 @@ __device__ __forceinline__ void op_r1spc(const Ctx &c, int k, int n, int upos, i
 // H_STATE / H0_STATE (my_module.h:903-932, 1020-1042):
 // bits[pos..pos+n) = bits[pos..pos+n) ^ bits[pos+n..pos+2n)   (H)
 //                  = bits[pos+n..pos+2n)                      (H0)
+// [j0, j1): the bit dwords of this wave when n >= 16 (split across the waves of a group)
 template <bool H0>
-__device__ __forceinline__ void op_h(const Ctx &c, int pos, int n)
+__device__ __forceinline__ void op_h(const Ctx &c, int pos, int n, int j0, int j1)
 {
     if (n >= 16) {
         const int da = pos >> 4, db = (pos + n) >> 4;
-        for (int j = 0; j < n / 16; j++) {
+        for (int j = j0; j < j1; j++) {
             uint32_t b = c.bld(db + j);
             c.bst(da + j, H0 ? b : (c.bld(da + j) ^ b));
         }
@@ -251,19 +252,40 @@ __device__ __forceinline__ void op_h(const Ctx &c, int pos, int n)
 }
 
 // ---------------------------------------------------------------------------------------
-// The decode kernel: one wave = 8 frames; `ops` is the compiled schedule.
+// The decode kernel. A "group" of `wpg` waves decodes 8 frames together; a block holds
+// `gpb` groups (gpb > 1 only when wpg == 1). With wpg > 1 the waves share the group's stage
+// storage and split every op that is wide enough (F/G: n >= wpg words; H/H0/R1: n >= 16 wpg
+// words, in whole bit dwords); leaves, REP and SPC run on wave 0. A block barrier precedes
+// an op whenever it or the op before it was split, so every read sees the writes of the
+// waves that produced it. The schedule is data independent, so all groups of a block pass
+// the same barriers.
 //   llr:  [batch][N] int8;   out: [batch][out_stride] uint16 (bit_mem_1 words, END order)
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool op_split(int code, int n, int wpg)
+{
+    if (wpg <= 1) return false;
+    switch (code) {
+    case OP_F:
+    case OP_G: return n >= wpg;
+    case OP_H:
+    case OP_H0:
+    case OP_R1: return n >= 16 * wpg;
+    default: return false;
+    }
+}
+
 template <bool GMEM>
-__global__ void __launch_bounds__(256) polar_sc_decode_kernel(
+__global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
     const int8_t *__restrict__ llr, uint16_t *__restrict__ out, const Op *__restrict__ ops,
-    uint32_t *__restrict__ scratch, int N, int batch, int out_stride, int waves_per_block,
-    int wave_dwords)
+    uint32_t *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb,
+    int group_dwords)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
-    const long wave = (long)blockIdx.x * waves_per_block + wib;
+    const int wi = wib % wpg;                       // wave index in its group
+    const int gib = wib / wpg;                      // group index in the block
+    const long group = (long)blockIdx.x * gpb + gib;
     const int G = N >> 4;
     const int row = lane >> 4;
     const int pl = lane & 15;
@@ -272,23 +294,26 @@ __global__ void __launch_bounds__(256) polar_sc_decode_kernel(
     c.G = G;
     c.nslot = (uint32_t)(G - 1);
     if constexpr (GMEM) {
-        c.base = scratch + (size_t)wave * (size_t)wave_dwords + lane;
+        c.base = scratch + (size_t)group * (size_t)group_dwords + lane;
     } else {
-        c.base = smem + (size_t)wib * (size_t)wave_dwords + lane;
+        c.base = smem + (size_t)gib * (size_t)group_dwords + lane;
     }
-    long f_lo = wave * 8 + row, f_hi = wave * 8 + 4 + row;
+    long f_lo = group * 8 + row, f_hi = group * 8 + 4 + row;
     const long f_lo_c = f_lo < batch ? f_lo : (long)batch - 1;
     const long f_hi_c = f_hi < batch ? f_hi : (long)batch - 1;
     c.llr_lo = llr + (size_t)f_lo_c * (size_t)N + pl;
     c.llr_hi = llr + (size_t)f_hi_c * (size_t)N + pl;
     c.ln.init((uint32_t)pl);
 
-    if (wave * 8 >= batch) return;   // whole wave idle (uniform)
+    // an idle group is a whole block when wpg > 1 (gpb == 1), so no barrier is stranded
+    if (group * 8 >= batch) return;
 
     // clear partial-sum memory (H0 may read words the H0 route never wrote)
     const int nbd = (G + 15) >> 4;
-    for (int d = 0; d < nbd; d++) c.bst(d, 0u);
+    if (wi == 0)
+        for (int d = 0; d < nbd; d++) c.bst(d, 0u);
 
+    bool prev_split = true;
     for (int oi = 0;; oi++) {
         const int code = __builtin_amdgcn_readfirstlane(ops[oi].code);
         if (code == OP_END) break;
@@ -297,19 +322,28 @@ __global__ void __launch_bounds__(256) polar_sc_decode_kernel(
         const int pos = __builtin_amdgcn_readfirstlane(ops[oi].pos);
         const int upos = __builtin_amdgcn_readfirstlane(ops[oi].upos);
         const uint32_t fb = (uint32_t)__builtin_amdgcn_readfirstlane((int)ops[oi].fb);
+        const bool split = op_split(code, n, wpg);
+        if (wpg > 1 && (split || prev_split)) __syncthreads();
+        prev_split = split;
+        if (!split && wi != 0) continue;
+        // this wave's share of a split op (whole op otherwise)
+        const int i0 = split ? (int)(((long)n * wi) / wpg) : 0;
+        const int i1 = split ? (int)(((long)n * (wi + 1)) / wpg) : n;
         switch (code) {
-        case OP_F: op_fg<false>(c, k, n, -1); break;
-        case OP_G: op_fg<true>(c, k, n, upos); break;
+        case OP_F: op_fg<false>(c, k, n, -1, i0, i1); break;
+        case OP_G: op_fg<true>(c, k, n, upos, i0, i1); break;
         case OP_FLEAF: op_leaf<false>(c, k, pos, -1, fb); break;
         case OP_GLEAF: op_leaf<true>(c, k, pos, upos, fb); break;
         case OP_REP: op_rep(c, k, n, pos); break;
-        case OP_R1: op_r1spc<false>(c, k, n, upos, pos); break;
-        case OP_SPC: op_r1spc<true>(c, k, n, upos, pos); break;
-        case OP_H: op_h<false>(c, pos, n); break;
-        case OP_H0: op_h<true>(c, pos, n); break;
+        case OP_R1: op_r1spc<false>(c, k, n, upos, pos, i0, i1); break;
+        case OP_SPC: op_r1spc<true>(c, k, n, upos, pos, 0, n); break;
+        case OP_H: op_h<false>(c, pos, n, i0 >> 4, i1 >> 4); break;
+        case OP_H0: op_h<true>(c, pos, n, i0 >> 4, i1 >> 4); break;
         default: break;
         }
     }
+    if (wpg > 1) __syncthreads();
+    if (wi != 0) return;
 
     // END (my_module.h:1848-1869) + wrapper_out: emit bit_mem words in natural order.
     const bool st_lo = f_lo < batch, st_hi = f_hi < batch;
@@ -346,25 +380,26 @@ __global__ void polar_sc_lane_selftest_kernel(uint32_t *out)
 // ---------------------------------------------------------------------------------------
 extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out, const void *ops,
                                       uint32_t *scratch, int N, long batch, int out_stride,
-                                      int waves_per_block, int wave_dwords, void *stream)
+                                      int waves_per_group, int groups_per_block, int group_dwords,
+                                      void *stream)
 {
-    const long waves = (batch + 7) / 8;
-    const long blocks = (waves + waves_per_block - 1) / waves_per_block;
-    dim3 grid((unsigned)blocks), block((unsigned)(64 * waves_per_block));
+    const long groups = (batch + 7) / 8;
+    const long blocks = (groups + groups_per_block - 1) / groups_per_block;
+    dim3 grid((unsigned)blocks), block((unsigned)(64 * waves_per_group * groups_per_block));
     hipStream_t s = (hipStream_t)stream;
     const polar::Op *o = (const polar::Op *)ops;
     if (gmem) {
-        hipLaunchKernelGGL(polar::polar_sc_decode_kernel<true>, grid, block, 0, s, llr, out, o,
-                           scratch, N, (int)batch, out_stride, waves_per_block, wave_dwords);
+        hipLaunchKernelGGL(polar::polar_sc_decode_kernel<true>, grid, block, 0, s, llr, out, o, scratch, N,
+                           (int)batch, out_stride, waves_per_group, groups_per_block, group_dwords);
     } else {
-        size_t lds = (size_t)waves_per_block * (size_t)wave_dwords * 4u;
+        size_t lds = (size_t)groups_per_block * (size_t)group_dwords * 4u;
         if (lds > 65536) {
             hipError_t ae = hipFuncSetAttribute((const void *)polar::polar_sc_decode_kernel<false>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (ae != hipSuccess) return -(int)ae - 1000;
         }
-        hipLaunchKernelGGL(polar::polar_sc_decode_kernel<false>, grid, block, lds, s, llr, out, o,
-                           scratch, N, (int)batch, out_stride, waves_per_block, wave_dwords);
+        hipLaunchKernelGGL(polar::polar_sc_decode_kernel<false>, grid, block, lds, s, llr, out, o, scratch, N,
+                           (int)batch, out_stride, waves_per_group, groups_per_block, group_dwords);
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -(int)e - 1000;

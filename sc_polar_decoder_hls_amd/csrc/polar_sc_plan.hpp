@@ -20,6 +20,7 @@ struct DevState {
     size_t scratch_bytes = 0;
     hipModule_t module = nullptr; // per-mask kernel
     hipFunction_t fn = nullptr;
+    int simds = 0;                // SIMDs of the device (4 per CU), for launch sizing
 };
 
 enum JitMode { JIT_OFF = 0, JIT_AUTO = 1 };
@@ -36,8 +37,7 @@ struct polar_sc_plan {
     std::vector<polar_sc_op> ops;
     polar_sc_plan_stats stats{};
     int gmem = 0;
-    int wave_dwords = 0;             // interpreter: per-wave storage, dwords
-    int waves_per_block = 1;
+    int wave_dwords = 0;             // interpreter: stage + bit storage of one 8-frame group, dwords
     int jit = 0;                     // 1: decode with the per-mask kernel
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;

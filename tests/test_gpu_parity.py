@@ -216,3 +216,23 @@ def test_c_cli_decode_file(pkg, cuda, oracle_mod, tmp_path):
     assert r.returncode == 0, r.stderr
     words = np.frombuffer((tmp_path / "x.bin").read_bytes(), dtype=np.uint64).reshape(29, -1)
     _assert_same(pkg.unpack_bits(words, mask.size), oracle_mod.decode_fsm(mask, llr), "C CLI")
+
+
+@pytest.mark.parametrize("wpg", [1, 2, 4, 16])
+@pytest.mark.parametrize("name,batch", [("frozen_n_2048_k_1024", 21), ("frozen_n_4096_k_2048", 13),
+                                        ("frozen_n_16384_k_8192", 9)])
+def test_interpreter_waves_per_group(pkg, cuda, oracle_mod, name, batch, wpg):
+    """Schedule interpreter with 1..16 cooperating waves per 8-frame group (split F/G/H/R1
+    ops, leaves/REP/SPC on wave 0, barriers between differently split ops)."""
+    mask = util.mask(name)
+    llr, _ = util.synth_frames(mask, batch, ebn0_db=1.5, seed=wpg)
+    old = os.environ.get("POLAR_SC_WAVES_PER_GROUP")
+    os.environ["POLAR_SC_WAVES_PER_GROUP"] = str(wpg)
+    try:
+        got = _decode(pkg, cuda, mask, llr, jit=False)
+    finally:
+        if old is None:
+            del os.environ["POLAR_SC_WAVES_PER_GROUP"]
+        else:
+            os.environ["POLAR_SC_WAVES_PER_GROUP"] = old
+    _assert_same(got, oracle_mod.decode_fsm(mask, llr), "%s wpg=%d" % (name, wpg))
