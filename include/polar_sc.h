@@ -97,8 +97,11 @@ typedef struct polar_sc_plan_stats {
                                          0 = LDS (schedule interpreter), 1 = HBM scratch
                                          (interpreter, large N), 2 = VGPRs (per-mask kernel,
                                          N <= 1024)                                      */
-    uint32_t lds_bytes_per_wave;      /* LDS footprint of one wave (8 frames)          */
-    uint64_t scratch_bytes_per_wave;  /* HBM scratch of one wave when storage == 1     */
+    uint32_t lds_bytes_per_wave;      /* LDS footprint of one 8-frame group: storage 2:
+                                         the staged channel frames; 0: all stage slots and
+                                         partial sums; 1: the lower tree levels          */
+    uint64_t scratch_bytes_per_wave;  /* HBM scratch of one 8-frame group (storage 1:
+                                         upper tree levels + partial sums), else 0       */
 } polar_sc_plan_stats;
 
 /* Fill *cfg with the reference configuration (config.h as shipped). */

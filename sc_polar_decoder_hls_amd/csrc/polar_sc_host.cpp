@@ -20,7 +20,7 @@
 extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out, const void *ops,
                                       uint32_t *scratch, int N, long batch, int out_stride,
                                       int waves_per_group, int groups_per_block, int group_dwords,
-                                      void *stream);
+                                      int lds_dwords, int lds0, void *stream);
 extern "C" int polar_sc_launch_selftest(uint32_t *out_dev);
 
 using polar_host::DevState;
@@ -31,7 +31,8 @@ namespace {
 constexpr uint32_t NODE_R0 = 0x00, NODE_R1 = 0x0F, NODE_REP = 0x02, NODE_SPC = 0x04, NODE_RN = 0x08;
 
 // largest per-wave LDS footprint kept on chip; above it stages go to HBM scratch
-constexpr uint32_t LDS_WAVE_LIMIT = 80u * 1024u;
+constexpr uint32_t LDS_WAVE_LIMIT = 80u * 1024u;   // all-LDS interpreter limit per 8-frame group
+constexpr int LDS_LOW_SLOTS = 128;                  // HBM mode: nodes <= 128 words keep their levels in LDS
 
 }  // namespace
 
@@ -78,6 +79,43 @@ void emit(polar_sc_plan &p, int code, int level, int n, int pos, int upos, uint3
     o.upos = upos;
     o.fb = fb;
     p.ops.push_back(o);
+}
+
+// HBM-scratch plans: the device copy of the schedule brackets every subtree of <= 128 words
+// (LDS_LOW_SLOTS) with POLAR_OP_WOPEN / POLAR_OP_WFLUSH and flags its ops (reserved[0] = 1):
+// their partial-sum dwords live in an LDS window (cleared on open, written to the HBM bits on
+// flush). The subtree's ops are contiguous in the schedule and touch only bits of their own
+// subtree; the ops of larger nodes run after the flush and use the HBM copy. The exported
+// schedule (polar_sc_plan_get_schedule) stays the plain one.
+void window_schedule(polar_sc_plan &p)
+{
+    const int W = LDS_LOW_SLOTS;
+    p.dev_ops.clear();
+    int cur = -1;
+    auto mark = [&](int code, int pos) {
+        polar_sc_op o{};
+        o.code = code;
+        o.pos = pos;
+        o.upos = -1;
+        p.dev_ops.push_back(o);
+    };
+    for (const polar_sc_op &op : p.ops) {
+        int win = -1;
+        if (op.code != POLAR_OP_END && 2 * op.n <= W) {
+            const bool right = op.code == POLAR_OP_G || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC ||
+                               op.code == POLAR_OP_GLEAF;
+            const int node = right ? op.pos - op.n : op.pos;
+            win = (node / W) * W;
+        }
+        if (win != cur) {
+            if (cur >= 0) mark(polar_host::POLAR_OP_WFLUSH, cur);
+            if (win >= 0) mark(polar_host::POLAR_OP_WOPEN, win);
+            cur = win;
+        }
+        polar_sc_op o = op;
+        o.reserved[0] = win >= 0 ? 1 : 0;
+        p.dev_ops.push_back(o);
+    }
 }
 
 // Decode the children of the node at `level` covering groups [g0, g0+cnt) (cnt >= 2) whose
@@ -151,13 +189,14 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
         return 0;
     }
     if (!st.ops) {
-        size_t bytes = p->ops.size() * sizeof(polar_sc_op);
+        const std::vector<polar_sc_op> &dops = p->dev_ops.empty() ? p->ops : p->dev_ops;
+        size_t bytes = dops.size() * sizeof(polar_sc_op);
         if (hipMalloc(&st.ops, bytes) != hipSuccess) return -ENOMEM;
-        if (hipMemcpy(st.ops, p->ops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+        if (hipMemcpy(st.ops, dops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
     }
     if (p->gmem) {
         size_t waves = (batch + 7) / 8;
-        size_t need = waves * (size_t)p->wave_dwords * 4u;
+        size_t need = waves * (size_t)p->hbm_group_dwords * 4u;
         if (need > st.scratch_bytes) {
             if (st.scratch) {
                 if (hipDeviceSynchronize() != hipSuccess) return -EIO;
@@ -203,7 +242,7 @@ int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size
     if (p->jit) return polar_host::jit_launch(*p, *st, llr, out, (long)batch, out_stride, stream);
     const int wpg = waves_per_group(p, batch, st->simds);
     rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, (uint32_t *)st->scratch, (int)p->N, (long)batch,
-                                out_stride, wpg, 1, p->wave_dwords, stream);
+                                out_stride, wpg, 1, p->hbm_group_dwords, p->lds_group_dwords, p->lds0, stream);
     return rc ? -EIO : 0;
 }
 
@@ -303,16 +342,27 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         if (o.code <= POLAR_OP_SPC) s.word_ops += (uint64_t)o.n;
     }
     const uint32_t nslot = p->G - 1, nbd = (p->G + 15) / 16;
-    p->wave_dwords = (int)((nslot + nbd) * 64u);
-    const uint64_t wave_bytes = (uint64_t)p->wave_dwords * 4u;
-    p->gmem = wave_bytes > LDS_WAVE_LIMIT ? 1 : 0;
+    const uint64_t all_bytes = (uint64_t)(nslot + nbd) * 256u;   // one 8-frame group, all in LDS
+    p->gmem = all_bytes > LDS_WAVE_LIMIT ? 1 : 0;
+    if (p->gmem) {
+        // upper levels + bit dwords in HBM scratch; the levels of nodes <= 128 words in LDS,
+        // plus an LDS window for the partial sums of the current 128-word subtree
+        p->lds0 = (int)p->G - LDS_LOW_SLOTS;
+        p->hbm_group_dwords = (p->lds0 + (int)nbd) * 64;
+        p->lds_group_dwords = ((int)nslot - p->lds0 + LDS_LOW_SLOTS / 16) * 64;
+        window_schedule(*p);
+    } else {
+        p->lds0 = 0;
+        p->hbm_group_dwords = 0;
+        p->lds_group_dwords = (int)(nslot + nbd) * 64;
+    }
     while ((1u << p->lg) < p->G) p->lg++;
     // per-mask register kernel for N <= 1024 unless POLAR_SC_JIT=0 (schedule interpreter)
     const char *jit_env = std::getenv("POLAR_SC_JIT");
     p->jit = (polar_host::jit_supported(N) && !(jit_env && jit_env[0] == '0')) ? 1 : 0;
     s.storage = p->jit ? 2u : (uint32_t)p->gmem;
-    s.lds_bytes_per_wave = p->gmem ? 0u : (uint32_t)wave_bytes;
-    s.scratch_bytes_per_wave = p->gmem ? wave_bytes : 0u;
+    s.lds_bytes_per_wave = p->jit ? 8u * (N + 16u) : (uint32_t)p->lds_group_dwords * 4u;
+    s.scratch_bytes_per_wave = p->jit ? 0u : (uint64_t)p->hbm_group_dwords * 4u;
     *out = p;
     return 0;
 }

@@ -27,8 +27,10 @@ namespace polar {
 
 enum : int {
     OP_F = 1, OP_G = 2, OP_FLEAF = 3, OP_GLEAF = 4, OP_REP = 5, OP_R1 = 6, OP_SPC = 7,
-    OP_H = 8, OP_H0 = 9, OP_END = 10
+    OP_H = 8, OP_H0 = 9, OP_END = 10,
+    OP_WOPEN = 11, OP_WFLUSH = 12   // HBM-scratch plans: partial-sum window of a 128-word subtree
 };
+constexpr int WIN_DWORDS = 8;       // 128 words of partial sums
 
 struct Op {            // == polar_sc_op (include/polar_sc.h)
     int32_t code, level, n, pos, upos;
@@ -37,19 +39,50 @@ struct Op {            // == polar_sc_op (include/polar_sc.h)
 };
 
 // ---------------------------------------------------------------------------------------
-// Per-wave storage: LDS (small N) or HBM scratch (large N). `base` already includes the
-// lane offset; slot / bit-dword indices are wave-uniform.
+// Per-group storage. GMEM = false (small N): every stage slot and the bit dwords in LDS.
+// GMEM = true (large N): the slots of the upper tree levels [0, lds0) and the bit dwords in
+// HBM scratch, the slots of the lower levels [lds0, nslot) in LDS -- every level moves the
+// same volume per frame, and the lower levels run the narrow, latency-bound ops. Slot s,
+// lane L lives at dword s*64+L of its space (one 256-byte row per wave access). Base
+// pointers include the lane offset; slot / bit-dword indices are wave-uniform.
 // ---------------------------------------------------------------------------------------
+template <bool GMEM>
 struct Ctx {
-    uint32_t *base;        // stage slots [0, nslot), then bits dwords
+    uint32_t *hb;          // HBM scratch (GMEM): slots [0, lds0), then bit dwords
+    uint32_t *lb;          // LDS: slots [lds0, nslot) (GMEM) / slots + bit dwords (!GMEM)
+    int lds0;              // first slot held in LDS (0 when !GMEM)
+    int wd0;               // GMEM: first bit dword of the open partial-sum window, -1 = none
     uint32_t nslot;        // G - 1
     int G;
     const int8_t *llr_lo, *llr_hi;   // frame rows (lane offset included)
     Lanes ln;
-    __device__ __forceinline__ uint32_t ld(int slot) const { return base[slot * 64]; }
-    __device__ __forceinline__ void st(int slot, uint32_t v) const { base[slot * 64] = v; }
-    __device__ __forceinline__ uint32_t bld(int d) const { return base[(nslot + d) * 64]; }
-    __device__ __forceinline__ void bst(int d, uint32_t v) const { base[(nslot + d) * 64] = v; }
+    __device__ __forceinline__ bool in_lds(int slot) const { return !GMEM || slot >= lds0; }
+    __device__ __forceinline__ uint32_t ldl(int slot) const { return lb[(slot - lds0) * 64]; }
+    __device__ __forceinline__ uint32_t ldh(int slot) const { return hb[slot * 64]; }
+    __device__ __forceinline__ void stl(int slot, uint32_t v) const { lb[(slot - lds0) * 64] = v; }
+    __device__ __forceinline__ void sth(int slot, uint32_t v) const { hb[slot * 64] = v; }
+    __device__ __forceinline__ uint32_t ld(int slot) const { return in_lds(slot) ? ldl(slot) : ldh(slot); }
+    __device__ __forceinline__ void st(int slot, uint32_t v) const
+    {
+        if (in_lds(slot)) stl(slot, v);
+        else sth(slot, v);
+    }
+    // bit dword d: LDS window (ops inside a windowed subtree), HBM bits, or LDS (!GMEM)
+    __device__ __forceinline__ uint32_t *wl(int d) const { return lb + ((int)nslot - lds0 + d - wd0) * 64; }
+    __device__ __forceinline__ uint32_t bld(int d) const
+    {
+        if constexpr (GMEM) return wd0 >= 0 ? *wl(d) : hb[(lds0 + d) * 64];
+        else return lb[(nslot + d) * 64];
+    }
+    __device__ __forceinline__ void bst(int d, uint32_t v) const
+    {
+        if constexpr (GMEM) {
+            if (wd0 >= 0) *wl(d) = v;
+            else hb[(lds0 + d) * 64] = v;
+        } else {
+            lb[(nslot + d) * 64] = v;
+        }
+    }
     __device__ __forceinline__ int lvl_off(int k) const { return G - (G >> (k - 1)); }  // k >= 1
     __device__ __forceinline__ uint32_t chan(int w) const
     {
@@ -68,7 +101,8 @@ struct Ctx {
 __device__ __forceinline__ uint32_t ubit(uint32_t dword, int q) { return (dword << (15 - (q & 15))) & SGN; }
 
 // write n (< 16, aligned) words of hard-decision flags packed in `acc` (bit j = word pos+j)
-__device__ __forceinline__ void bits_put_small(const Ctx &c, int pos, int n, uint32_t acc)
+template <class C>
+__device__ __forceinline__ void bits_put_small(const C &c, int pos, int n, uint32_t acc)
 {
     uint32_t mlo = ((1u << n) - 1u) << (pos & 15);
     uint32_t m = mlo | (mlo << 16);
@@ -79,14 +113,20 @@ __device__ __forceinline__ void bits_put_small(const Ctx &c, int pos, int n, uin
 // ---------------------------------------------------------------------------------------
 // Ops
 // ---------------------------------------------------------------------------------------
-template <bool ISG, bool ROOT>
-__device__ __forceinline__ void fg_words(const Ctx &c, int k, int n, int upos, int i0, int i1)
+// SL / DL: source / destination slots in LDS (else HBM scratch)
+template <bool ISG, bool ROOT, bool SL, bool DL, class C>
+__device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int i0, int i1)
 {
     const int dst = c.lvl_off(k + 1);
     const int s0 = ROOT ? 0 : c.lvl_off(k);
     auto src = [&](int w) -> uint32_t {
         if constexpr (ROOT) return c.chan(w);
-        else return c.ld(s0 + w);
+        else if constexpr (SL) return c.ldl(s0 + w);
+        else return c.ldh(s0 + w);
+    };
+    auto put = [&](int w, uint32_t v) {
+        if constexpr (DL) c.stl(dst + w, v);
+        else c.sth(dst + w, v);
     };
     int i = i0;
     // 8 words per iteration: 16 independent source loads in flight (HBM latency)
@@ -115,7 +155,7 @@ __device__ __forceinline__ void fg_words(const Ctx &c, int k, int n, int upos, i
             for (int j = 0; j < 8; j++) r[j] = F_sm(a[j], b[j]);
         }
 #pragma unroll
-        for (int j = 0; j < 8; j++) c.st(dst + i + j, r[j]);
+        for (int j = 0; j < 8; j++) put(i + j, r[j]);
     }
     for (; i < i1; i++) {
         const uint32_t a = src(i), b = src(n + i);
@@ -126,24 +166,33 @@ __device__ __forceinline__ void fg_words(const Ctx &c, int k, int n, int upos, i
         } else {
             r = F_sm(a, b);
         }
-        c.st(dst + i, r);
+        put(i, r);
     }
 }
 
 // F_STATE / G_STATE word loops (my_module.h:373-445, 704-781) for n >= 2 output words:
 // dst[i] = F(src[i], src[n+i]) or G(src[i], src[n+i], bit_mem[upos+i]), i in [i0, i1)
 // (the words of this wave when the op is split across the waves of a group).
-template <bool ISG>
-__device__ __forceinline__ void op_fg(const Ctx &c, int k, int n, int upos, int i0, int i1)
+template <bool ISG, class C>
+__device__ __forceinline__ void op_fg(const C &c, int k, int n, int upos, int i0, int i1)
 {
-    if (k == 0) fg_words<ISG, true>(c, k, n, upos, i0, i1);
-    else fg_words<ISG, false>(c, k, n, upos, i0, i1);
+    const bool dl = c.in_lds(c.lvl_off(k + 1));
+    if (k == 0) {
+        if (dl) fg_words<ISG, true, false, true>(c, k, n, upos, i0, i1);
+        else fg_words<ISG, true, false, false>(c, k, n, upos, i0, i1);
+    } else if (c.in_lds(c.lvl_off(k))) {
+        fg_words<ISG, false, true, true>(c, k, n, upos, i0, i1);
+    } else if (dl) {
+        fg_words<ISG, false, false, true>(c, k, n, upos, i0, i1);
+    } else {
+        fg_words<ISG, false, false, false>(c, k, n, upos, i0, i1);
+    }
 }
 
 // F/G with NB_ITER = 1 followed by R_STATE: Spec_Polar_Decoder on reg_result
 // (my_module.h:544-612)
-template <bool ISG>
-__device__ __forceinline__ void op_leaf(const Ctx &c, int k, int pos, int upos, uint32_t fb)
+template <bool ISG, class C>
+__device__ __forceinline__ void op_leaf(const C &c, int k, int pos, int upos, uint32_t fb)
 {
     uint32_t a = c.src(k, 0), b = c.src(k, 1);
     uint32_t L;
@@ -163,7 +212,8 @@ __device__ __forceinline__ void op_leaf(const Ctx &c, int k, int pos, int upos, 
 // F_REP_STATE (my_module.h:1292-1390): lambda = F(parent); per word the 16-lane exact SM
 // adder tree, accumulated over words in order by the 11-bit saturating SM adder
 // (ADDER_TREE_16, functions.h:3190-3205); x = all sign(acc).
-__device__ __forceinline__ void op_rep(const Ctx &c, int k, int n, int pos)
+template <class C>
+__device__ __forceinline__ void op_rep(const C &c, int k, int n, int pos)
 {
     const int s0 = c.lvl_off(k);
     uint32_t acc = 0;
@@ -186,8 +236,8 @@ __device__ __forceinline__ void op_rep(const Ctx &c, int k, int n, int pos)
 // minimum-|lambda| position (lexicographic (|l|, word, bitrev4(lane)) == Min_Mask_16_SM
 // tournament + strict '<' across words) when the parity of x is odd.
 // [i0, i1): the words of this wave (R1 split in whole 16-word chunks; SPC is never split).
-template <bool SPC>
-__device__ __forceinline__ void op_r1spc(const Ctx &c, int k, int n, int upos, int pos, int i0, int i1)
+template <bool SPC, class C>
+__device__ __forceinline__ void op_r1spc(const C &c, int k, int n, int upos, int pos, int i0, int i1)
 {
     const int s0 = c.lvl_off(k);
     uint32_t ud = 0, acc = 0, par = 0;
@@ -233,8 +283,8 @@ __device__ __forceinline__ void op_r1spc(const Ctx &c, int k, int n, int upos, i
 // bits[pos..pos+n) = bits[pos..pos+n) ^ bits[pos+n..pos+2n)   (H)
 //                  = bits[pos+n..pos+2n)                      (H0)
 // [j0, j1): the bit dwords of this wave when n >= 16 (split across the waves of a group)
-template <bool H0>
-__device__ __forceinline__ void op_h(const Ctx &c, int pos, int n, int j0, int j1)
+template <bool H0, class C>
+__device__ __forceinline__ void op_h(const C &c, int pos, int n, int j0, int j1)
 {
     if (n >= 16) {
         const int da = pos >> 4, db = (pos + n) >> 4;
@@ -278,7 +328,7 @@ template <bool GMEM>
 __global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
     const int8_t *__restrict__ llr, uint16_t *__restrict__ out, const Op *__restrict__ ops,
     uint32_t *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb,
-    int group_dwords)
+    int group_dwords, int lds_dwords, int lds0)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int lane = threadIdx.x & 63;
@@ -290,14 +340,13 @@ __global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
     const int row = lane >> 4;
     const int pl = lane & 15;
 
-    Ctx c;
+    Ctx<GMEM> c;
     c.G = G;
     c.nslot = (uint32_t)(G - 1);
-    if constexpr (GMEM) {
-        c.base = scratch + (size_t)group * (size_t)group_dwords + lane;
-    } else {
-        c.base = smem + (size_t)gib * (size_t)group_dwords + lane;
-    }
+    c.lds0 = GMEM ? lds0 : 0;
+    c.wd0 = -1;
+    c.lb = smem + (size_t)gib * (size_t)lds_dwords + lane;
+    c.hb = GMEM ? scratch + (size_t)group * (size_t)group_dwords + lane : nullptr;
     long f_lo = group * 8 + row, f_hi = group * 8 + 4 + row;
     const long f_lo_c = f_lo < batch ? f_lo : (long)batch - 1;
     const long f_hi_c = f_hi < batch ? f_hi : (long)batch - 1;
@@ -314,6 +363,7 @@ __global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
         for (int d = 0; d < nbd; d++) c.bst(d, 0u);
 
     bool prev_split = true;
+    int win_d0 = -1;   // GMEM: first bit dword of the open partial-sum window
     for (int oi = 0;; oi++) {
         const int code = __builtin_amdgcn_readfirstlane(ops[oi].code);
         if (code == OP_END) break;
@@ -325,6 +375,21 @@ __global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
         const bool split = op_split(code, n, wpg);
         if (wpg > 1 && (split || prev_split)) __syncthreads();
         prev_split = split;
+        if constexpr (GMEM) {
+            if (code == OP_WOPEN || code == OP_WFLUSH) {
+                // open: clear the window (bits start at 0); flush: copy it to the HBM bits
+                if (wi == 0) {
+                    c.wd0 = pos >> 4;
+                    for (int j = 0; j < WIN_DWORDS; j++) {
+                        if (code == OP_WOPEN) *c.wl(c.wd0 + j) = 0u;
+                        else c.hb[(c.lds0 + c.wd0 + j) * 64] = *c.wl(c.wd0 + j);
+                    }
+                }
+                win_d0 = code == OP_WOPEN ? (pos >> 4) : -1;
+                continue;
+            }
+            c.wd0 = __builtin_amdgcn_readfirstlane(ops[oi].r0) ? win_d0 : -1;
+        }
         if (!split && wi != 0) continue;
         // this wave's share of a split op (whole op otherwise)
         const int i0 = split ? (int)(((long)n * wi) / wpg) : 0;
@@ -342,6 +407,7 @@ __global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
         default: break;
         }
     }
+    if constexpr (GMEM) c.wd0 = -1;
     if (wpg > 1) __syncthreads();
     if (wi != 0) return;
 
@@ -381,25 +447,28 @@ __global__ void polar_sc_lane_selftest_kernel(uint32_t *out)
 extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out, const void *ops,
                                       uint32_t *scratch, int N, long batch, int out_stride,
                                       int waves_per_group, int groups_per_block, int group_dwords,
-                                      void *stream)
+                                      int lds_dwords, int lds0, void *stream)
 {
     const long groups = (batch + 7) / 8;
     const long blocks = (groups + groups_per_block - 1) / groups_per_block;
     dim3 grid((unsigned)blocks), block((unsigned)(64 * waves_per_group * groups_per_block));
     hipStream_t s = (hipStream_t)stream;
     const polar::Op *o = (const polar::Op *)ops;
+    const size_t lds = (size_t)groups_per_block * (size_t)lds_dwords * 4u;
+    const void *fn = gmem ? (const void *)polar::polar_sc_decode_kernel<true>
+                          : (const void *)polar::polar_sc_decode_kernel<false>;
+    if (lds > 65536) {
+        hipError_t ae = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (ae != hipSuccess) return -(int)ae - 1000;
+    }
     if (gmem) {
-        hipLaunchKernelGGL(polar::polar_sc_decode_kernel<true>, grid, block, 0, s, llr, out, o, scratch, N,
-                           (int)batch, out_stride, waves_per_group, groups_per_block, group_dwords);
+        hipLaunchKernelGGL(polar::polar_sc_decode_kernel<true>, grid, block, lds, s, llr, out, o, scratch, N,
+                           (int)batch, out_stride, waves_per_group, groups_per_block, group_dwords, lds_dwords,
+                           lds0);
     } else {
-        size_t lds = (size_t)groups_per_block * (size_t)group_dwords * 4u;
-        if (lds > 65536) {
-            hipError_t ae = hipFuncSetAttribute((const void *)polar::polar_sc_decode_kernel<false>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (ae != hipSuccess) return -(int)ae - 1000;
-        }
         hipLaunchKernelGGL(polar::polar_sc_decode_kernel<false>, grid, block, lds, s, llr, out, o, scratch, N,
-                           (int)batch, out_stride, waves_per_group, groups_per_block, group_dwords);
+                           (int)batch, out_stride, waves_per_group, groups_per_block, group_dwords, lds_dwords,
+                           lds0);
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -(int)e - 1000;

@@ -25,6 +25,9 @@ struct DevState {
 
 enum JitMode { JIT_OFF = 0, JIT_AUTO = 1 };
 
+// device-internal schedule records of HBM-scratch plans (never exported)
+enum { POLAR_OP_WOPEN = 11, POLAR_OP_WFLUSH = 12 };
+
 }  // namespace polar_host
 
 struct polar_sc_plan {
@@ -35,9 +38,12 @@ struct polar_sc_plan {
     std::vector<uint16_t> fb;        // G, Bit_Frozen (bit k = mask[16g+k])
     std::vector<uint8_t> type;       // G, Node_Type
     std::vector<polar_sc_op> ops;
+    std::vector<polar_sc_op> dev_ops;   // device copy when it differs (HBM-scratch plans)
     polar_sc_plan_stats stats{};
     int gmem = 0;
-    int wave_dwords = 0;             // interpreter: stage + bit storage of one 8-frame group, dwords
+    // interpreter storage of one 8-frame group (dwords): HBM scratch part, LDS part, and the
+    // first stage slot held in LDS (polar_sc_kernels.hip, Ctx)
+    int hbm_group_dwords = 0, lds_group_dwords = 0, lds0 = 0;
     int jit = 0;                     // 1: decode with the per-mask kernel
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;
