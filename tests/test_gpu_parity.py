@@ -236,3 +236,11 @@ def test_interpreter_waves_per_group(pkg, cuda, oracle_mod, name, batch, wpg):
         else:
             os.environ["POLAR_SC_WAVES_PER_GROUP"] = old
     _assert_same(got, oracle_mod.decode_fsm(mask, llr), "%s wpg=%d" % (name, wpg))
+
+
+@pytest.mark.parametrize("case", ["c1", "c2_snr", "c2_edge", "c3"])
+@pytest.mark.parametrize("jit", [True, False], ids=["maskkernel", "interp"])
+def test_gpu_matches_committed_vectors(pkg, cuda, case, jit):
+    """GPU decode of the committed regression vectors (tests/golden/decode_vectors.npz)."""
+    name, llr, x = util.decode_vectors()[case]
+    _assert_same(_decode(pkg, cuda, util.mask(name), llr, jit), x, case)

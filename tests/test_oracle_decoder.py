@@ -92,3 +92,10 @@ def test_stale_node_stack_is_harmless(oracle_mod):
     batch = oracle_mod.decode_fsm(mask, llr)
     single = np.concatenate([oracle_mod.decode_fsm(mask, llr[i:i + 1]) for i in range(5)])
     np.testing.assert_array_equal(batch, single)
+
+
+@pytest.mark.parametrize("case", ["c1", "c2_snr", "c2_edge", "c3"])
+def test_restatement_reproduces_committed_vectors(oracle_mod, case):
+    """The oracle still decodes the committed regression vectors to the committed x^."""
+    name, llr, x = util.decode_vectors()[case]
+    np.testing.assert_array_equal(oracle_mod.decode_fsm(util.mask(name), llr), x, err_msg=case)

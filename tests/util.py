@@ -167,3 +167,16 @@ def run_schedule(ops, N, llr):
         else:
             raise ValueError(code)
     return bits.reshape(B, N).astype(np.uint8)
+
+
+def decode_vectors():
+    """tests/golden/decode_vectors.npz (tools/make_decode_vectors.py): {case: (mask name,
+    llr [B, N] int8, x^ [B, N] uint8)}."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "decode_vectors.npz")
+    z = np.load(path, allow_pickle=False)
+    out = {}
+    for key in sorted({k.split("__")[0] for k in z.files}):
+        llr = z[key + "__llr"]
+        x = np.unpackbits(z[key + "__xhat"], axis=1, bitorder="little")[:, : llr.shape[1]]
+        out[key] = (str(z[key + "__mask"]), llr, x)
+    return out
