@@ -197,39 +197,6 @@ __device__ __forceinline__ u32 leaf16(u32 L, u32 fb, const Lanes &ln)
     return leaf_rec<0, 16>(L, fb, fbm, ln);
 }
 
-// (b) frozen pattern FB known at compile time (per-mask kernels): the same recursion with
-// every frozen-pattern decision resolved statically. Mixed 2-blocks are (1,0) -> x=[u0,0]
-// and (0,1) -> x=[u1,u1] (F_simplified / G_simplified with the frozen lane's bit = 0).
-template <u32 FB, int B, int W>
-__device__ __forceinline__ u32 leaf_ct(u32 L, const Lanes &ln)
-{
-    constexpr u32 bm = ((1u << W) - 1u) << B;
-    constexpr u32 sub = FB & bm;
-    if constexpr (sub == 0u) {
-        return 0u;
-    } else if constexpr (sub == bm) {
-        return L & SGN;
-    } else if constexpr (W == 2) {
-        u32 P = xorlane<1>(L);
-        if constexpr ((sub >> B) == 1u) {
-            // fb = (1, 0): u0 = sign(a) ^ sign(b), u1 = 0 -> x = [u0, 0]
-            return ((L ^ P) & SGN) & ln.a1;
-        } else {
-            // fb = (0, 1): u0 = 0, u1 = |a| < |b| ? sign(b) : sign(a) -> x = [u1, u1]
-            u32 d = pk_sub(P & MAG, L & MAG);
-            u32 u1 = bsel(d, L, P) & SGN;        // valid on the b lane
-            return bsel(ln.a1, xorlane<1>(u1), u1);
-        }
-    } else {
-        constexpr int H = W / 2;
-        u32 P = xorlane<H>(L);
-        u32 xa = leaf_ct<FB, B, H>(F_sm(L, P), ln);
-        u32 Lb = G_sm<0>(P, L, xorlane<H>(xa));
-        u32 xb = leaf_ct<FB, B + H, H>(Lb, ln);
-        return bsel(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
-    }
-}
-
 // ---------------------------------------------------------------------------------------
 // Row reductions
 // ---------------------------------------------------------------------------------------
@@ -279,23 +246,6 @@ __device__ __forceinline__ u32 row_transpose16(u32 v, const Lanes &ln)
 // Channel LLR -> SM16: wrapper_in + Adapt_format/qconv_format (wrapper_in.h:34,
 // library.h:18-28, scalar.h:229-239). The LLR is the low 6 bits (sc_bigint<6>); -32 -> +0.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ u32 conv_half(int c)
-{
-    int t = (int)((u32)c << 26) >> 26;      // sign-extend 6 bits
-    u32 m = (u32)(t < 0 ? -t : t) & 31u;
-    u32 s = (t < 0 && m != 0u) ? 0x8000u : 0u;
-    return m | s;
-}
-
-// two channel bytes into the halves of one register (d16 / d16_hi loads)
-__device__ __forceinline__ u32 ld_pair(const unsigned char *lo, const unsigned char *hi)
-{
-    u16x2 v;
-    v.x = *lo;
-    v.y = *hi;
-    return U(v);
-}
-
 // raw = b_lo | b_hi << 16 (two int8 LLRs, any bits above bit 5 ignored) -> SM16 pair.
 // With t = raw & 63: |LLR| = min(t, 64 - t) & 31 (t = 32, i.e. -32, -> 0) and the sign is
 // set iff t >= 33 (t + 0x7FDF reaches bit 15).
@@ -322,18 +272,9 @@ __device__ __forceinline__ u32 sm8_pair(u32 lo, u32 hi)
 }
 
 // ---------------------------------------------------------------------------------------
-// Sign-only G: the hard decision of G_sm (R1 nodes need nothing else; the magnitude and its
-// saturation never change the sign). u as for G_sm.
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ u32 G_sign(u32 a, u32 b, u32 u)
-{
-    u32 d = pk_sub(a & MAG, b & MAG);
-    return bsel(d, b, a ^ u) & SGN;
-}
-
-// ---------------------------------------------------------------------------------------
 // Leaf in split form (per-mask kernels): M = magnitudes (u16 pair), S = sign masks (0xFFFF
-// in a negative half). Same recursion and results as leaf_ct, fewer instructions:
+// in a negative half), frozen pattern FB known at compile time. Same recursion and results
+// as leaf_rec with every frozen-pattern decision resolved statically:
 //   F : M = min(M, M'), S = S ^ S'
 //   G : x = S_F ^ U (signs of a' and b differ; S_F = S ^ S' is the F sign, U the partner's
 //       partial sums as masks), |a| < |b| from M' - M, magnitude = x ? |M' - M| : M' + M,
@@ -439,20 +380,6 @@ __device__ __forceinline__ u32 F_split_sm(u32 ma, u32 mb, u32 FS)
 // chain below carries the same value; only a zero total needs the SM sign-of-zero rule,
 // which the caller resolves with the exact SM path (rep_exact_*).
 // ---------------------------------------------------------------------------------------
-// F(a, b) of two SM16 pairs as value + 512 per half (no carries between the halves: the
-// 16-word row sum stays within 0..16383)
-__device__ __forceinline__ u32 F_biased(u32 a, u32 b)
-{
-    const u32 m = pk_min(a & MAG, b & MAG);
-    const u32 s = pk_sra(a ^ b, 15);
-    return pk_add(pk_sub(m ^ s, s), 0x02000200u);
-}
-// SM16 pair -> value + 512 per half
-__device__ __forceinline__ u32 sm_biased(u32 x)
-{
-    const u32 s = pk_sra(x, 15);
-    return pk_add(pk_sub((x & MAG) ^ s, s), 0x02000200u);
-}
 // row total in every lane (rotation butterfly; 32-bit adds take the DPP operand directly)
 __device__ __forceinline__ u32 row_sum_biased(u32 v)
 {

@@ -73,7 +73,7 @@ struct Gen {
     static std::string uflag(int i)
     {
         std::ostringstream s;
-        s << "(c_ << " << (15 - (i & 15)) << ")";   // G_sm / G_sign read only bits 15 and 31 of u
+        s << "(c_ << " << (15 - (i & 15)) << ")";   // G_sm / G_root read only bits 15 and 31 of u
         return s.str();
     }
 

@@ -86,9 +86,7 @@ struct Ctx {
     __device__ __forceinline__ int lvl_off(int k) const { return G - (G >> (k - 1)); }  // k >= 1
     __device__ __forceinline__ uint32_t chan(int w) const
     {
-        int lo = llr_lo[16 * w];
-        int hi = llr_hi[16 * w];
-        return conv_half(lo) | (conv_half(hi) << 16);
+        return conv_pair((uint32_t)(uint8_t)llr_lo[16 * w] | ((uint32_t)(uint8_t)llr_hi[16 * w] << 16));
     }
     // source word i of a level-k node (k = 0: channel)
     __device__ __forceinline__ uint32_t src(int k, int i) const

@@ -46,9 +46,34 @@ def max_over_ranks(values, dist=None, device=None):
     return [float(v) for v in t.tolist()]
 
 
+def scatter_shards(full, total, frame_shape, dtype, dist=None, device=None):
+    """Scatter a [total, *frame_shape] batch held by rank 0 into the per-rank shards of
+    shard_bounds (RCCL over xGMI with the nccl backend). `full` is ignored on the other ranks
+    (pass None); every rank knows the frame shape from its plan. Returns this rank's
+    [count, *frame_shape] shard on `device`."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return full
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    spans = [shard_bounds(total, world, r) for r in range(world)]
+    cap = max(c for _, c in spans)
+    shape = (cap,) + tuple(frame_shape)
+    out = torch.empty(shape, dtype=dtype, device=device)
+    parts = None
+    if rank == 0:
+        parts = []
+        for start, count in spans:   # equal-size (padded) chunks, as scatter requires
+            buf = torch.zeros(shape, dtype=dtype, device=device)
+            buf[:count] = full[start:start + count]
+            parts.append(buf)
+    dist.scatter(out, parts, src=0)
+    return out[: spans[rank][1]]
+
+
 def gather_shards(local, total, dist=None, device=None):
     """All-gather the per-rank decoded words [count, words] (int64 tensors) into the full
-    [total, words] batch on every rank (verification only; not part of the timed path)."""
+    [total, words] batch on every rank (verification, and the gather half of the C4
+    scatter/gather mode of bench.py)."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return local
     import torch
@@ -59,4 +84,22 @@ def gather_shards(local, total, dist=None, device=None):
     pad[: local.shape[0]] = local.to(pad.device)
     parts = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(parts, pad)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)
+
+
+def gather_to_root(local, total, dist=None, device=None):
+    """Gather the per-rank [count, ...] results into [total, ...] on rank 0 (None elsewhere)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return local
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    counts = [shard_bounds(total, world, r)[1] for r in range(world)]
+    cap = max(counts)
+    dev = local.device if device is None else device
+    pad = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+    pad[: local.shape[0]] = local.to(dev)
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+    dist.gather(pad, parts, dst=0)
+    if rank != 0:
+        return None
     return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)

@@ -60,12 +60,18 @@ def _worker(rank, world, port, total, q):
         words = torch.from_numpy(np.packbits(bits.astype(np.uint8), axis=1, bitorder="little").copy()
                                  .view(np.int64) if count else np.zeros((0, mask.size // 64), np.int64))
         full = sharding.gather_shards(words, total, dist)
+        # scatter from rank 0 (the C4 scatter/gather mode): each rank must receive its span
+        whole = torch.from_numpy(llr) if rank == 0 else None
+        mine = sharding.scatter_shards(whole, total, (mask.size,), torch.int8, dist)
+        scattered_ok = bool(np.array_equal(mine.numpy(), llr[start:start + count]))
+        ok_all = torch.tensor([1 if scattered_ok else 0])
+        dist.all_reduce(ok_all)
         t = sharding.max_over_ranks([0.5 + rank, 3.0 - rank], dist)
         if rank == 0:
             ref = oracle.decode_fsm(mask, llr)
             ref_words = np.packbits(ref.astype(np.uint8), axis=1, bitorder="little").view(np.int64)
-            q.put(("ok", bool(np.array_equal(full.numpy(), ref_words)), t, [sharding.shard_bounds(total, world, r)
-                                                                           for r in range(world)]))
+            q.put(("ok", bool(np.array_equal(full.numpy(), ref_words)) and int(ok_all) == world, t,
+                   [sharding.shard_bounds(total, world, r) for r in range(world)]))
     except Exception as e:   # surface worker failures to the test
         q.put(("err", repr(e), None, None))
         raise

@@ -173,7 +173,7 @@ def _sm8_pair(lo, hi):
 
 
 def _conv_pair(raw):
-    """Mirror of polar::conv_pair (interpreter kernels)."""
+    """Mirror of polar::conv_pair (schedule interpreter, Ctx::chan)."""
     out = 0
     for h in (0, 16):
         t = (raw >> h) & 0x3F
