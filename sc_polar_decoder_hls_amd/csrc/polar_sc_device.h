@@ -314,6 +314,14 @@ __device__ __forceinline__ u32 leaf_ms(u32 M, u32 S, const Lanes &ln)
     }
 }
 
+// SM16 pair with magnitudes <= 31 -> two SM8 bytes (low frame in bits 0..7, high frame in
+// bits 8..15); inverse of sm8_pair
+__device__ __forceinline__ u32 sm16_to_sm8x2(u32 v)
+{
+    const u32 t = (v & 0x001F001Fu) | ((v >> 8) & 0x00800080u);   // SM8 in bytes 0 and 2
+    return __builtin_amdgcn_perm(t, t, 0x0C0C0200u);              // bytes [0, 2] -> [0, 1]
+}
+
 // ---------------------------------------------------------------------------------------
 // Split stage words (per-mask kernels): magnitudes as u16 pairs (M) and the signs of 16
 // words packed in one "plane" dword (bit i = low frame of word i, bit 16 + i = high frame),

@@ -189,7 +189,9 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
         return 0;
     }
     if (!st.ops) {
-        const std::vector<polar_sc_op> &dops = p->dev_ops.empty() ? p->ops : p->dev_ops;
+        // device copy (+ a spare END: the interpreter loads record i+1 while running i)
+        std::vector<polar_sc_op> dops = p->dev_ops.empty() ? p->ops : p->dev_ops;
+        dops.push_back(dops.back());
         size_t bytes = dops.size() * sizeof(polar_sc_op);
         if (hipMalloc(&st.ops, bytes) != hipSuccess) return -ENOMEM;
         if (hipMemcpy(st.ops, dops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
@@ -348,7 +350,7 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         // upper levels + bit dwords in HBM scratch; the levels of nodes <= 128 words in LDS,
         // plus an LDS window for the partial sums of the current 128-word subtree
         p->lds0 = (int)p->G - LDS_LOW_SLOTS;
-        p->hbm_group_dwords = (p->lds0 + (int)nbd) * 64;
+        p->hbm_group_dwords = p->lds0 * 32 + (int)nbd * 64;   // SM8-pair slots + bit dwords
         p->lds_group_dwords = ((int)nslot - p->lds0 + LDS_LOW_SLOTS / 16) * 64;
         window_schedule(*p);
     } else {

@@ -42,13 +42,15 @@ struct Op {            // == polar_sc_op (include/polar_sc.h)
 // Per-group storage. GMEM = false (small N): every stage slot and the bit dwords in LDS.
 // GMEM = true (large N): the slots of the upper tree levels [0, lds0) and the bit dwords in
 // HBM scratch, the slots of the lower levels [lds0, nslot) in LDS -- every level moves the
-// same volume per frame, and the lower levels run the narrow, latency-bound ops. Slot s,
+// same volume per frame, and the lower levels run the narrow, latency-bound ops. HBM slots
+// hold SM8 pairs (stage values above the leaves never exceed magnitude 31), half the bytes. Slot s,
 // lane L lives at dword s*64+L of its space (one 256-byte row per wave access). Base
 // pointers include the lane offset; slot / bit-dword indices are wave-uniform.
 // ---------------------------------------------------------------------------------------
 template <bool GMEM>
 struct Ctx {
-    uint32_t *hb;          // HBM scratch (GMEM): slots [0, lds0), then bit dwords
+    uint16_t *hs;          // HBM scratch (GMEM): slots [0, lds0) as SM8 pairs (128 B rows)
+    uint32_t *hbit;        // HBM scratch (GMEM): bit dwords (256 B rows)
     uint32_t *lb;          // LDS: slots [lds0, nslot) (GMEM) / slots + bit dwords (!GMEM)
     int lds0;              // first slot held in LDS (0 when !GMEM)
     int wd0;               // GMEM: first bit dword of the open partial-sum window, -1 = none
@@ -58,9 +60,13 @@ struct Ctx {
     Lanes ln;
     __device__ __forceinline__ bool in_lds(int slot) const { return !GMEM || slot >= lds0; }
     __device__ __forceinline__ uint32_t ldl(int slot) const { return lb[(slot - lds0) * 64]; }
-    __device__ __forceinline__ uint32_t ldh(int slot) const { return hb[slot * 64]; }
+    __device__ __forceinline__ uint32_t ldh(int slot) const
+    {
+        const uint32_t h = hs[slot * 64];
+        return sm8_pair(h, h >> 8);
+    }
     __device__ __forceinline__ void stl(int slot, uint32_t v) const { lb[(slot - lds0) * 64] = v; }
-    __device__ __forceinline__ void sth(int slot, uint32_t v) const { hb[slot * 64] = v; }
+    __device__ __forceinline__ void sth(int slot, uint32_t v) const { hs[slot * 64] = (uint16_t)sm16_to_sm8x2(v); }
     __device__ __forceinline__ uint32_t ld(int slot) const { return in_lds(slot) ? ldl(slot) : ldh(slot); }
     __device__ __forceinline__ void st(int slot, uint32_t v) const
     {
@@ -71,14 +77,14 @@ struct Ctx {
     __device__ __forceinline__ uint32_t *wl(int d) const { return lb + ((int)nslot - lds0 + d - wd0) * 64; }
     __device__ __forceinline__ uint32_t bld(int d) const
     {
-        if constexpr (GMEM) return wd0 >= 0 ? *wl(d) : hb[(lds0 + d) * 64];
+        if constexpr (GMEM) return wd0 >= 0 ? *wl(d) : hbit[d * 64];
         else return lb[(nslot + d) * 64];
     }
     __device__ __forceinline__ void bst(int d, uint32_t v) const
     {
         if constexpr (GMEM) {
             if (wd0 >= 0) *wl(d) = v;
-            else hb[(lds0 + d) * 64] = v;
+            else hbit[d * 64] = v;
         } else {
             lb[(nslot + d) * 64] = v;
         }
@@ -214,14 +220,24 @@ template <class C>
 __device__ __forceinline__ void op_rep(const C &c, int k, int n, int pos)
 {
     const int s0 = c.lvl_off(k);
+    // value chain in two's complement (exact sums and 511 clamps, polar_sc_device.h); the
+    // exact SM chain only when some frame ends on a zero total (sign-of-zero rule)
     uint32_t acc = 0;
     for (int i = 0; i < n; i++) {
-        uint32_t lam = F_sm(c.ld(s0 + i), c.ld(s0 + n + i));
-        uint32_t t = row_add_tree(lam, c.ln);
-        acc = G_sm<511>(t, acc, 0u);
+        const uint32_t lam = F_sm(c.ld(s0 + i), c.ld(s0 + n + i));
+        const uint32_t sg = pk_sra(lam, 15);
+        acc = rep_acc(acc, row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
     }
-    uint32_t dflags = acc & SGN;
-    uint32_t full = ((dflags & 0x8000u) ? 0x0000FFFFu : 0u) | ((dflags & 0x80000000u) ? 0xFFFF0000u : 0u);
+    if (rep_any_zero(acc)) {
+        acc = 0;
+        for (int i = 0; i < n; i++) {
+            uint32_t lam = F_sm(c.ld(s0 + i), c.ld(s0 + n + i));
+            uint32_t t = row_add_tree(lam, c.ln);
+            acc = G_sm<511>(t, acc, 0u);
+        }
+    }
+    // two's complement or SM16: the decision is bit 15 / 31 either way
+    const uint32_t full = pk_sra(acc, 15);
     if (n >= 16) {
         for (int j = 0; j < n / 16; j++) c.bst((pos >> 4) + j, full);
     } else {
@@ -344,7 +360,10 @@ __global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
     c.lds0 = GMEM ? lds0 : 0;
     c.wd0 = -1;
     c.lb = smem + (size_t)gib * (size_t)lds_dwords + lane;
-    c.hb = GMEM ? scratch + (size_t)group * (size_t)group_dwords + lane : nullptr;
+    // HBM part of the group: lds0 slots of 64 u16 (SM8 pairs), then the bit dwords
+    uint32_t *const gbase = GMEM ? scratch + (size_t)group * (size_t)group_dwords : nullptr;
+    c.hs = GMEM ? (uint16_t *)gbase + lane : nullptr;
+    c.hbit = GMEM ? gbase + (size_t)lds0 * 32 + lane : nullptr;
     long f_lo = group * 8 + row, f_hi = group * 8 + 4 + row;
     const long f_lo_c = f_lo < batch ? f_lo : (long)batch - 1;
     const long f_hi_c = f_hi < batch ? f_hi : (long)batch - 1;
@@ -362,14 +381,20 @@ __global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
 
     bool prev_split = true;
     int win_d0 = -1;   // GMEM: first bit dword of the open partial-sum window
+    // the record of the next op is loaded while the current one runs (the schedule of a
+    // large N outgrows the scalar cache; the device copy ends with a spare END record)
+    Op cur = ops[0];
     for (int oi = 0;; oi++) {
-        const int code = __builtin_amdgcn_readfirstlane(ops[oi].code);
+        const int code = __builtin_amdgcn_readfirstlane(cur.code);
         if (code == OP_END) break;
-        const int k = __builtin_amdgcn_readfirstlane(ops[oi].level);
-        const int n = __builtin_amdgcn_readfirstlane(ops[oi].n);
-        const int pos = __builtin_amdgcn_readfirstlane(ops[oi].pos);
-        const int upos = __builtin_amdgcn_readfirstlane(ops[oi].upos);
-        const uint32_t fb = (uint32_t)__builtin_amdgcn_readfirstlane((int)ops[oi].fb);
+        const Op nxt = ops[oi + 1];
+        const int k = __builtin_amdgcn_readfirstlane(cur.level);
+        const int n = __builtin_amdgcn_readfirstlane(cur.n);
+        const int pos = __builtin_amdgcn_readfirstlane(cur.pos);
+        const int upos = __builtin_amdgcn_readfirstlane(cur.upos);
+        const uint32_t fb = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur.fb);
+        const int flag = __builtin_amdgcn_readfirstlane(cur.r0);
+        cur = nxt;
         const bool split = op_split(code, n, wpg);
         if (wpg > 1 && (split || prev_split)) __syncthreads();
         prev_split = split;
@@ -380,13 +405,13 @@ __global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
                     c.wd0 = pos >> 4;
                     for (int j = 0; j < WIN_DWORDS; j++) {
                         if (code == OP_WOPEN) *c.wl(c.wd0 + j) = 0u;
-                        else c.hb[(c.lds0 + c.wd0 + j) * 64] = *c.wl(c.wd0 + j);
+                        else c.hbit[(c.wd0 + j) * 64] = *c.wl(c.wd0 + j);
                     }
                 }
                 win_d0 = code == OP_WOPEN ? (pos >> 4) : -1;
                 continue;
             }
-            c.wd0 = __builtin_amdgcn_readfirstlane(ops[oi].r0) ? win_d0 : -1;
+            c.wd0 = flag ? win_d0 : -1;
         }
         if (!split && wi != 0) continue;
         // this wave's share of a split op (whole op otherwise)
