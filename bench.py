@@ -155,6 +155,11 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU frames")
     ap.add_argument("--ebn0", type=float, default=2.5)
+    ap.add_argument("--data", choices=["csim", "torch"], default="csim",
+                    help="csim: the reference testbench's own frame chain on the GPU (KAT codewords for "
+                         "N in {8, 512, 1024}, else all-zero; xorshift128 seed 0xF0; Box-Muller; beta 4, +-31), "
+                         "each rank taking the next frames of the global stream; torch: random information "
+                         "bits + torch AWGN")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", type=int, default=64, help="frames checked vs the oracle (rank 0)")
@@ -204,7 +209,23 @@ def main():
 
     dec = pkg.Decoder(mask)
     dec.prepare(per_gpu)
-    llr, x = gen_frames_torch(torch, mask, per_gpu, args.ebn0, sharding.frame_seed(0xF0, rank), dev)
+    xref = None
+    if args.data == "csim":
+        kat_key = {8: "cw8x4", 512: "cw512x256", 1024: "cw1024x512"}.get(N)
+        cws = np.array(util.kat()[kat_key], dtype=np.uint8) if kat_key else None
+        sigma = pkg.csim_sigma(args.ebn0, K / N)
+        # frames of this rank: the next per_gpu frames of the testbench's single stream
+        counts = [per_gpu]
+        if dist is not None:
+            t = torch.zeros(world, dtype=torch.float64, device=coll_dev)
+            t[rank] = per_gpu
+            dist.all_reduce(t)
+            counts = [int(v) for v in t.tolist()]
+        frame0 = int(sum(counts[:rank]))
+        llr, xref = pkg.csim_frames(N, per_gpu, sigma, seed=0xF0, frame0=frame0, codewords=cws, device=dev)
+        x = None
+    else:
+        llr, x = gen_frames_torch(torch, mask, per_gpu, args.ebn0, sharding.frame_seed(0xF0, rank), dev)
     out = torch.empty((per_gpu, dec.words), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
@@ -258,9 +279,18 @@ def main():
         scatter_res = time_scatter_gather(torch, pkg, sharding, dist, dec, mask, frames_all, rank, dev,
                                           coll_dev, args)
 
-    # frame error rate of this batch vs the transmitted codewords (informative)
-    xhat = pkg.unpack_bits(out[: min(per_gpu, 4096)].cpu().numpy(), N)
-    fer = float((xhat != x[: xhat.shape[0]].cpu().numpy()).any(axis=1).mean())
+    # error rates of the last decoded batch vs the transmitted codewords (informative)
+    if xref is not None:
+        # sc_error_counter semantics on the device (per-frame count mod 1024), whole batch
+        cnt = pkg.count_errors(out, xref, N)
+        torch.cuda.synchronize()
+        c = [float(v) for v in cnt.cpu().tolist()]
+        fer, ber = c[1] / per_gpu, c[2] / (per_gpu * N)
+    else:
+        xhat = pkg.unpack_bits(out[: min(per_gpu, 4096)].cpu().numpy(), N)
+        xs = x[: xhat.shape[0]].cpu().numpy()
+        fer = float((xhat != xs).any(axis=1).mean())
+        ber = float((xhat != xs).mean())
 
     if rank == 0:
         bytes_per_launch = 1.125 * N * per_gpu
@@ -297,7 +327,10 @@ def main():
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "int16 sign-magnitude (6-bit LLRs, u8 in / bit-packed out)",
-            "data": "synthetic AWGN frames generated on-device (BPSK, Eb/N0=%.1f dB, 4x quantizer, +-31)" % args.ebn0,
+            "data": (("synthetic: the reference testbench's C-sim chain generated on-device (KAT codewords, "
+                      "xorshift128 seed 0xF0, Box-Muller, Eb/N0=%.1f dB, beta 4, +-31)" if args.data == "csim" else
+                      "synthetic AWGN frames generated on-device (random info bits, BPSK, Eb/N0=%.1f dB, "
+                      "4x quantizer, +-31)") % args.ebn0),
             "config": {"workload": desc, "N": N, "K": K, "frames_per_gpu": per_gpu,
                        "mask": name, "parallelism": "frames sharded, dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -308,6 +341,7 @@ def main():
             "valu_roofline": valu,
             "scatter_gather": scatter_res,
             "frame_error_rate": fer,
+            "bit_error_rate": ber,
             "parity_check": check,
         }
         if world == 1 and not args.no_cpu_baseline:

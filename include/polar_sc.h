@@ -172,6 +172,34 @@ int polar_sc_plan_compile(const polar_sc_plan *plan);
 /* The generated per-mask kernel source (NUL-terminated, truncated to cap); *len = full size. */
 int polar_sc_plan_kernel_source(const polar_sc_plan *plan, char *buf, size_t cap, size_t *len);
 
+/* ---- Frame source and error accounting of the reference testbench ---- */
+
+/* The reference's C-sim frame chain for frames frame0 .. frame0+batch-1, generated on the
+ * current device (src/testbench/sc_top_module.h:101-160): encoder (frame f sends row
+ * f % ncw of `codewords`, [ncw][N] host bytes 0/1; ncw = 0 -> all-zero codewords, as the
+ * reference does for N not in {8, 512, 1024}, sc_encoder.h:91-122), BPSK (bit 1 -> -1),
+ * two xorshift128 streams seeded from the 8-bit `seed8` (sc_xorshift128.h:56-125),
+ * Box-Muller (sc_awgn.h:60-89), v = bpsk + noise * sigma (sc_adder.h:135-154), and
+ * (short)(v * beta) clamped to [vsatn, vsatp] (sc_quantizer.h:69-81; the testbench uses
+ * beta 4, -31, 31, sigma = 1/sqrt(2 R 10^(EbN0/10))).
+ *   llr_dev:  [batch][N] int8, the decoder input (16-byte aligned)
+ *   xref_dev: [batch][ceil(N/64)] uint64 sent codewords (bit i of word j = x[64j+i]), or NULL
+ * Synchronous. Frames are independent (per-frame stream states by GF(2) jump-ahead). */
+int polar_csim_frames(uint32_t N, uint32_t seed8, uint64_t frame0, size_t batch, float sigma,
+                      int beta, int vsatn, int vsatp, const uint8_t *codewords, uint32_t ncw,
+                      int8_t *llr_dev, uint64_t *xref_dev, void *stream);
+
+/* Host: the two xorshift128 stream states at the start of each frame, states[f][0..3] =
+ * stream 1 (x, y, z, w), states[f][4..7] = stream 2. */
+int polar_csim_states(uint32_t N, uint32_t seed8, uint64_t frame0, size_t batch, uint32_t *states);
+
+/* sc_error_counter (sc_error_counter.h:50-126) on the device: adds to counts_dev[3]
+ * (unsigned 64-bit): [0] per-frame bit errors taken modulo 1024 (the reference's
+ * sc_uint<10>), [1] frames whose wrapped count is non-zero, [2] exact bit errors.
+ * xhat_dev / xref_dev: [batch][ceil(N/64)] uint64 as polar_sc_decode writes. Asynchronous. */
+int polar_count_errors(const uint64_t *xhat_dev, const uint64_t *xref_dev, uint32_t N, size_t batch,
+                       unsigned long long *counts_dev, void *stream);
+
 /* GPU self-test of the cross-lane (DPP) exchange patterns the kernels rely on.
  * out_dev: 4*64 uint32 on the device; entry [h][lane] = source lane seen by `lane` for
  * partner distance 1<<h. Synchronous. */

@@ -22,8 +22,8 @@ NODE_R0, NODE_R1, NODE_REP, NODE_SPC, NODE_RN = 0x00, 0x0F, 0x02, 0x04, 0x08
 
 def build(force=False):
     """Compile the oracle with its Makefile (gcc); returns the .so path."""
-    src = os.path.join(_HERE, "polar_oracle.c")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("polar_oracle.c", "polar_channel_oracle.c", "Makefile")]
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < max(map(os.path.getmtime, srcs)):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH
 
@@ -105,3 +105,32 @@ def rep_add_tree16(llr_sm, old):
 def min_mask16(llr_sm):
     a = np.ascontiguousarray(llr_sm, dtype=np.uint32)
     return lib().orc_min_mask16(_ptr(a))
+
+
+def csim_states(N, seed, frame0):
+    """xorshift128 states (2 streams x 4 words) at the start of frame `frame0`."""
+    out = np.zeros(8, dtype=np.uint32)
+    lib().orc_csim_states(ctypes.c_uint32(N), ctypes.c_uint32(seed), ctypes.c_uint64(frame0), _ptr(out))
+    return out
+
+
+def csim_frames(N, seed, frame0, nframes, sigma, codewords=None, beta=4, vsatn=-31, vsatp=31):
+    """Reference C-sim chain frames (polar_channel_oracle.c): (llr int8 [n, N], x uint8 [n, N])."""
+    llr = np.zeros((nframes, N), dtype=np.int8)
+    x = np.zeros((nframes, N), dtype=np.uint8)
+    cw = None if codewords is None else np.ascontiguousarray(codewords, dtype=np.uint8)
+    lib().orc_csim_frames(ctypes.c_uint32(N), ctypes.c_uint32(seed), ctypes.c_uint64(frame0), ctypes.c_int(nframes),
+                          ctypes.c_float(sigma), ctypes.c_int(beta), ctypes.c_int(vsatn), ctypes.c_int(vsatp),
+                          None if cw is None else _ptr(cw), ctypes.c_int(0 if cw is None else cw.shape[0]),
+                          _ptr(llr), _ptr(x))
+    return llr, x
+
+
+def count_errors(xhat, xref):
+    """sc_error_counter semantics: [sum of per-frame errors mod 1024, frame errors, exact bit errors]."""
+    xhat = np.ascontiguousarray(xhat, dtype=np.uint8)
+    xref = np.ascontiguousarray(xref, dtype=np.uint8)
+    counts = np.zeros(3, dtype=np.uint64)
+    lib().orc_count_errors(ctypes.c_uint32(xhat.shape[1]), ctypes.c_int(xhat.shape[0]), _ptr(xhat), _ptr(xref),
+                           _ptr(counts))
+    return counts

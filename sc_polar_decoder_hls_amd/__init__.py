@@ -22,7 +22,8 @@ from . import _build
 
 __all__ = [
     "Decoder", "PolarError", "load_frozen_tab", "load_mask_file", "unpack_bits", "pack_bits",
-    "default_config", "lib", "selftest_lanes", "OPS", "build",
+    "default_config", "lib", "selftest_lanes", "OPS", "build", "csim_sigma", "csim_states", "csim_frames",
+    "count_errors",
 ]
 
 build = _build.build
@@ -71,6 +72,7 @@ EXPORTS = (
     "polar_load_mask_file", "polar_codeword_to_info", "polar_sc_plan_get_stats",
     "polar_sc_plan_get_schedule", "polar_sc_selftest_lanes", "polar_sc_strerror",
     "polar_sc_abi_version", "polar_sc_plan_compile", "polar_sc_plan_kernel_source",
+    "polar_csim_frames", "polar_csim_states", "polar_count_errors",
 )
 
 _lib = None
@@ -104,6 +106,9 @@ def lib():
         "polar_sc_plan_kernel_source": [p, ctypes.c_char_p, sz, ctypes.POINTER(sz)],
         "polar_sc_strerror": [i32],
         "polar_sc_abi_version": [],
+        "polar_csim_frames": [u32, u32, ctypes.c_uint64, sz, ctypes.c_float, i32, i32, i32, p, u32, p, p, p],
+        "polar_csim_states": [u32, u32, ctypes.c_uint64, sz, p],
+        "polar_count_errors": [p, p, u32, sz, p, p],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -311,3 +316,54 @@ def selftest_lanes():
     buf = torch.zeros(4 * 64, dtype=torch.int32, device="cuda")
     _check("polar_sc_selftest_lanes", lib().polar_sc_selftest_lanes(ctypes.c_void_p(buf.data_ptr())))
     return buf.view(4, 64).cpu().numpy()
+
+
+# ---------------------------------------------------------------------------------------
+# Frame source and error accounting of the reference testbench (include/polar_sc.h)
+# ---------------------------------------------------------------------------------------
+def csim_sigma(ebn0_db, rate):
+    """sigma of the testbench (src/testbench/main.cpp:91-98), in float32 like the reference."""
+    f32 = np.float32
+    return float(f32(1.0) / np.sqrt(f32(2.0) * f32(rate) * np.power(f32(10.0), f32(ebn0_db) / f32(10.0), dtype=f32),
+                                     dtype=f32))
+
+
+def csim_states(N, seed, frame0, batch):
+    """Host: xorshift128 states at the start of frames frame0.. ([batch, 8] uint32)."""
+    out = np.zeros((batch, 8), dtype=np.uint32)
+    _check("polar_csim_states", lib().polar_csim_states(ctypes.c_uint32(N), ctypes.c_uint32(seed), ctypes.c_uint64(frame0),
+                                   ctypes.c_size_t(batch), out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+def csim_frames(N, batch, sigma, seed=0xF0, frame0=0, codewords=None, beta=4, vsatn=-31, vsatp=31,
+                device=None, stream=None):
+    """The reference's C-sim frame chain on the GPU: (llr int8 [batch, N], x^ref int64
+    [batch, ceil(N/64)]) torch tensors on `device`."""
+    import torch
+    dev = torch.device("cuda") if device is None else device
+    llr = torch.empty((batch, N), dtype=torch.int8, device=dev)
+    xref = torch.empty((batch, (N + 63) // 64), dtype=torch.int64, device=dev)
+    cw = None if codewords is None else np.ascontiguousarray(codewords, dtype=np.uint8)
+    ncw = 0 if cw is None else cw.shape[0]
+    st = torch.cuda.current_stream(dev) if stream is None else stream
+    _check("polar_csim_frames", lib().polar_csim_frames(ctypes.c_uint32(N), ctypes.c_uint32(seed), ctypes.c_uint64(frame0),
+                                   ctypes.c_size_t(batch), ctypes.c_float(sigma), ctypes.c_int(beta),
+                                   ctypes.c_int(vsatn), ctypes.c_int(vsatp),
+                                   None if cw is None else cw.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(ncw),
+                                   ctypes.c_void_p(llr.data_ptr()), ctypes.c_void_p(xref.data_ptr()),
+                                   ctypes.c_void_p(st.cuda_stream)))
+    return llr, xref
+
+
+def count_errors(xhat, xref, N, counts=None, stream=None):
+    """sc_error_counter on the GPU: adds [bit errors mod 1024 per frame, frame errors, exact bit
+    errors] into `counts` (int64 tensor [3], created when None) and returns it."""
+    import torch
+    if counts is None:
+        counts = torch.zeros(3, dtype=torch.int64, device=xhat.device)
+    st = torch.cuda.current_stream(xhat.device) if stream is None else stream
+    _check("polar_count_errors", lib().polar_count_errors(ctypes.c_void_p(xhat.data_ptr()), ctypes.c_void_p(xref.data_ptr()),
+                                    ctypes.c_uint32(N), ctypes.c_size_t(xhat.shape[0]),
+                                    ctypes.c_void_p(counts.data_ptr()), ctypes.c_void_p(st.cuda_stream)))
+    return counts
