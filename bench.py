@@ -162,6 +162,8 @@ def main():
                          "bits + torch AWGN")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-io", action="store_true",
+                    help="also time polar_sc_decode_host (PCIe-inclusive, host buffers) on the batch")
     ap.add_argument("--check", type=int, default=64, help="frames checked vs the oracle (rank 0)")
     ap.add_argument("--io", choices=["resident", "scatter"], default="resident",
                     help="scatter: also time the C4 flow -- rank 0 holds the whole batch in HBM, "
@@ -344,6 +346,21 @@ def main():
             "bit_error_rate": ber,
             "parity_check": check,
         }
+        if world == 1 and args.host_io:
+            # PCIe-inclusive rate of the host-buffer entry point (polar_sc_decode_host):
+            # pageable host int8 frames in, packed x^ out, synchronous
+            host_llr = llr.cpu().numpy()
+            dec.decode_host(host_llr)
+            reps = 5
+            t0h = time.perf_counter()
+            for _ in range(reps):
+                dec.decode_host(host_llr)
+            elh = (time.perf_counter() - t0h) / reps
+            res["host_io"] = {"ms_per_step": elh * 1e3, "frames_per_sec": per_gpu / elh,
+                              "info_bits_per_s": per_gpu * K / elh,
+                              "note": "polar_sc_decode_host: %d frames from pageable host memory "
+                                      "(%.1f MB in, %.1f MB out), copies + decode, synchronous"
+                                      % (per_gpu, per_gpu * N / 1e6, per_gpu * dec.words * 8 / 1e6)}
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(mask, args.cpu_seconds, args.ebn0)
         print(json.dumps(res))

@@ -8,6 +8,7 @@
 // op list (polar_sc_op); the GPU kernel interprets the list with wave-uniform control.
 #include "polar_sc_plan.hpp"
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -372,6 +373,10 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
 int polar_sc_plan_destroy(polar_sc_plan *p)
 {
     if (!p) return -EINVAL;
+    for (auto &kv : p->host_bufs) {
+        if (kv.second.llr) (void)hipFree(kv.second.llr);
+        if (kv.second.out) (void)hipFree(kv.second.out);
+    }
     int cur = 0;
     bool have_dev = hipGetDevice(&cur) == hipSuccess;
     for (auto &kv : p->dev) {
@@ -416,20 +421,32 @@ int polar_sc_decode_host(const polar_sc_plan *p, const int8_t *llr, uint64_t *ha
         for (size_t i = 0; i < total; i++)
             if (llr[i] > 31 || llr[i] < -31) return -EINVAL;
     }
+    // chunks of at most ~256 MB of LLRs through device buffers cached in the plan (one host
+    // decode per plan at a time: the buffers are shared)
     const size_t words = (p->N + 63) / 64;
-    const size_t in_bytes = batch * (size_t)p->N, out_bytes = batch * words * 8u;
-    int8_t *d_llr = nullptr;
-    uint64_t *d_out = nullptr;
-    int rc = 0;
-    if (hipMalloc((void **)&d_llr, in_bytes) != hipSuccess) return -ENOMEM;
-    if (hipMalloc((void **)&d_out, out_bytes) != hipSuccess) { (void)hipFree(d_llr); return -ENOMEM; }
-    rc = hip_err(hipMemcpy(d_llr, llr, in_bytes, hipMemcpyHostToDevice));
-    if (!rc) rc = polar_sc_decode(p, d_llr, d_out, batch, nullptr);
-    if (!rc) rc = hip_err(hipDeviceSynchronize());
-    if (!rc) rc = hip_err(hipMemcpy(hard_bits, d_out, out_bytes, hipMemcpyDeviceToHost));
-    (void)hipFree(d_llr);
-    (void)hipFree(d_out);
-    return rc;
+    const size_t chunk = std::max<size_t>(8, std::min<size_t>(batch, (256u << 20) / p->N));
+    std::lock_guard<std::mutex> lk(p->host_mu);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -EIO;
+    polar_host::HostBufs &hb = p->host_bufs[dev];
+    if (hb.frames < chunk) {
+        if (hb.llr) (void)hipFree(hb.llr);
+        if (hb.out) (void)hipFree(hb.out);
+        hb.llr = nullptr;
+        hb.out = nullptr;
+        hb.frames = 0;
+        if (hipMalloc((void **)&hb.llr, chunk * p->N) != hipSuccess) return -ENOMEM;
+        if (hipMalloc((void **)&hb.out, chunk * words * 8u) != hipSuccess) return -ENOMEM;
+        hb.frames = chunk;
+    }
+    for (size_t f0 = 0; f0 < batch; f0 += chunk) {
+        const size_t n = std::min(chunk, batch - f0);
+        int rc = hip_err(hipMemcpy(hb.llr, llr + f0 * p->N, n * p->N, hipMemcpyHostToDevice));
+        if (!rc) rc = polar_sc_decode(p, hb.llr, hb.out, n, nullptr);
+        if (!rc) rc = hip_err(hipMemcpy(hard_bits + f0 * words, hb.out, n * words * 8u, hipMemcpyDeviceToHost));
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 int polar_load_frozen_tab(const char *path, uint32_t N, uint32_t K, uint8_t *mask_out, uint32_t cap,

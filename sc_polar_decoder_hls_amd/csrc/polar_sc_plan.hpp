@@ -25,6 +25,13 @@ struct DevState {
 
 enum JitMode { JIT_OFF = 0, JIT_AUTO = 1 };
 
+// device staging buffers of polar_sc_decode_host
+struct HostBufs {
+    int8_t *llr = nullptr;
+    uint64_t *out = nullptr;
+    size_t frames = 0;
+};
+
 // device-internal schedule records of HBM-scratch plans (never exported)
 enum { POLAR_OP_WOPEN = 11, POLAR_OP_WFLUSH = 12 };
 
@@ -47,6 +54,8 @@ struct polar_sc_plan {
     int jit = 0;                     // 1: decode with the per-mask kernel
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;
+    mutable std::mutex host_mu;                             // polar_sc_decode_host staging
+    mutable std::map<int, polar_host::HostBufs> host_bufs;
     mutable std::vector<char> jit_code;   // compiled code object (lazily built)
     mutable std::string jit_log;
 };
