@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define POLAR_SC_ABI_VERSION 1
+#define POLAR_SC_ABI_VERSION 2
 #define POLAR_SC_PAR 16
 
 /*
@@ -102,6 +102,13 @@ typedef struct polar_sc_plan_stats {
                                          partial sums; 1: the lower tree levels          */
     uint64_t scratch_bytes_per_wave;  /* HBM scratch of one 8-frame group (storage 1:
                                          upper tree levels + partial sums), else 0       */
+    uint32_t kernel;                  /* decode kernel: 0 = schedule interpreter,
+                                         1 = per-mask kernel (N <= 1024), 2 = hybrid
+                                         (interpreter for the upper tree levels, generated
+                                         code for every mixed subtree of sub_words)      */
+    uint32_t sub_words;               /* hybrid: subtree size in 16-LLR words, else 0     */
+    uint32_t n_sub_kinds;             /* hybrid: distinct generated subtree decoders      */
+    uint32_t n_sub_calls;             /* hybrid: subtree decoder calls per frame group    */
 } polar_sc_plan_stats;
 
 /* Fill *cfg with the reference configuration (config.h as shipped). */

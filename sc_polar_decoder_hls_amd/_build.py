@@ -12,7 +12,8 @@ LIB = os.path.join(PKG, "lib", "libpolar_sc.so")
 SOURCES = [os.path.join(PKG, "csrc", "polar_sc_kernels.hip"), os.path.join(PKG, "csrc", "polar_sc_host.cpp"),
            os.path.join(PKG, "csrc", "polar_sc_jit.cpp"), os.path.join(PKG, "csrc", "polar_sc_channel.hip")]
 DEVICE_H = os.path.join(PKG, "csrc", "polar_sc_device.h")
-HEADERS = [os.path.join(ROOT, "include", "polar_sc.h"), DEVICE_H, os.path.join(PKG, "csrc", "polar_sc_plan.hpp")]
+INTERP_H = os.path.join(PKG, "csrc", "polar_sc_interp.h")
+HEADERS = [os.path.join(ROOT, "include", "polar_sc.h"), DEVICE_H, INTERP_H, os.path.join(PKG, "csrc", "polar_sc_plan.hpp")]
 GEN_DIR = os.path.join(PKG, "build")
 CLI_SRC = os.path.join(ROOT, "examples", "polar_decode_cli.c")
 CLI = os.path.join(PKG, "lib", "polar_decode_cli")
@@ -51,12 +52,14 @@ def build(force=False, verbose=False):
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     os.makedirs(GEN_DIR, exist_ok=True)
-    # embed the device header for hipRTC (per-mask kernels are compiled at plan time)
-    with open(DEVICE_H) as f:
-        dev_src = f.read()
-    assert ")POLARSRC\"" not in dev_src
-    with open(os.path.join(GEN_DIR, "polar_sc_device_src.inc"), "w") as f:
-        f.write("static const char kPolarDeviceSrc[] = R\"POLARSRC(" + dev_src + ")POLARSRC\";\n")
+    # embed the device headers for hipRTC (per-mask kernels are compiled at plan time)
+    for path, inc, name in ((DEVICE_H, "polar_sc_device_src.inc", "kPolarDeviceSrc"),
+                            (INTERP_H, "polar_sc_interp_src.inc", "kPolarInterpSrc")):
+        with open(path) as f:
+            src = f.read()
+        assert ")POLARSRC\"" not in src
+        with open(os.path.join(GEN_DIR, inc), "w") as f:
+            f.write("static const char " + name + "[] = R\"POLARSRC(" + src + ")POLARSRC\";\n")
     tmp = LIB + ".tmp.%d" % os.getpid()
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
            "-I" + os.path.join(ROOT, "include"), "-I" + GEN_DIR] + SOURCES + ["-o", tmp, "-lhiprtc"]

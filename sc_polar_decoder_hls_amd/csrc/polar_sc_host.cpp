@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -70,7 +71,7 @@ uint32_t node_class(const polar_sc_plan &p, uint32_t g0, uint32_t cnt)
     return NODE_RN;
 }
 
-void emit(polar_sc_plan &p, int code, int level, int n, int pos, int upos, uint32_t fb)
+void emit(std::vector<polar_sc_op> &out, int code, int level, int n, int pos, int upos, uint32_t fb)
 {
     polar_sc_op o{};
     o.code = code;
@@ -79,8 +80,16 @@ void emit(polar_sc_plan &p, int code, int level, int n, int pos, int upos, uint3
     o.pos = pos;
     o.upos = upos;
     o.fb = fb;
-    p.ops.push_back(o);
+    out.push_back(o);
 }
+
+// hybrid plans: distinct subtree schedules (keyed by their bytes) collected while compiling
+struct SubCtx {
+    uint32_t words = 0;
+    std::map<std::string, int> ids;
+    std::vector<std::vector<polar_sc_op>> lists;
+    uint32_t calls = 0;
+};
 
 // HBM-scratch plans: the device copy of the schedule brackets every subtree of <= 128 words
 // (LDS_LOW_SLOTS) with POLAR_OP_WOPEN / POLAR_OP_WFLUSH and flags its ops (reserved[0] = 1):
@@ -88,7 +97,7 @@ void emit(polar_sc_plan &p, int code, int level, int n, int pos, int upos, uint3
 // flush). The subtree's ops are contiguous in the schedule and touch only bits of their own
 // subtree; the ops of larger nodes run after the flush and use the HBM copy. The exported
 // schedule (polar_sc_plan_get_schedule) stays the plain one.
-void window_schedule(polar_sc_plan &p)
+void window_schedule(polar_sc_plan &p, const std::vector<polar_sc_op> &ops)
 {
     const int W = LDS_LOW_SLOTS;
     p.dev_ops.clear();
@@ -100,9 +109,11 @@ void window_schedule(polar_sc_plan &p)
         o.upos = -1;
         p.dev_ops.push_back(o);
     };
-    for (const polar_sc_op &op : p.ops) {
+    for (const polar_sc_op &op : ops) {
         int win = -1;
-        if (op.code != POLAR_OP_END && 2 * op.n <= W) {
+        if (op.code == polar_host::POLAR_OP_SUB) {
+            if (op.n <= W) win = (op.pos / W) * W;   // the subtree's own words [pos, pos + n)
+        } else if (op.code != POLAR_OP_END && 2 * op.n <= W) {
             const bool right = op.code == POLAR_OP_G || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC ||
                                op.code == POLAR_OP_GLEAF;
             const int node = right ? op.pos - op.n : op.pos;
@@ -127,8 +138,34 @@ void window_schedule(polar_sc_plan &p)
 //  * right child R1 -> G_R1_STATE, SPC -> G_SPC_STATE (selected from the node-type stack,
 //    my_module.h:614-664, 939-997)
 //  * the root's children are never pruned: INIT pushes (RN,RN) (my_module.h:328)
-void compile_node(polar_sc_plan &p, int level, uint32_t g0, uint32_t cnt, bool is_root)
+// Hybrid plans (sc != NULL): a node of sc->words words that is not the root becomes one
+// POLAR_OP_SUB record; its own schedule, rebased to the subtree root, is kept once per
+// distinct content.
+void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int level, uint32_t g0, uint32_t cnt,
+                  bool is_root, SubCtx *sc)
 {
+    if (sc && !is_root && cnt == sc->words) {
+        std::vector<polar_sc_op> sub;
+        compile_node(p, sub, level, g0, cnt, false, nullptr);
+        for (polar_sc_op &o : sub) {
+            o.level -= level;
+            o.pos -= (int)g0;
+            if (o.upos >= 0) o.upos -= (int)g0;
+        }
+        std::string key((const char *)sub.data(), sub.size() * sizeof(polar_sc_op));
+        auto it = sc->ids.find(key);
+        int id;
+        if (it == sc->ids.end()) {
+            id = (int)sc->lists.size();
+            sc->ids.emplace(key, id);
+            sc->lists.push_back(std::move(sub));
+        } else {
+            id = it->second;
+        }
+        sc->calls++;
+        emit(out, polar_host::POLAR_OP_SUB, level, (int)cnt, (int)g0, -1, (uint32_t)id);
+        return;
+    }
     const uint32_t h = cnt / 2;
     const uint32_t tl = is_root ? NODE_RN : node_class(p, g0, h);
     const uint32_t tr = is_root ? NODE_RN : node_class(p, g0 + h, h);
@@ -136,25 +173,25 @@ void compile_node(polar_sc_plan &p, int level, uint32_t g0, uint32_t cnt, bool i
     if (tl == NODE_R0) {
         left_zero = true;
     } else if (tl == NODE_REP) {
-        emit(p, POLAR_OP_REP, level, (int)h, (int)g0, -1, 0);
+        emit(out, POLAR_OP_REP, level, (int)h, (int)g0, -1, 0);
     } else if (h == 1) {
-        emit(p, POLAR_OP_FLEAF, level, 1, (int)g0, -1, p.fb[g0]);
+        emit(out, POLAR_OP_FLEAF, level, 1, (int)g0, -1, p.fb[g0]);
     } else {
-        emit(p, POLAR_OP_F, level, (int)h, (int)g0, -1, 0);
-        compile_node(p, level + 1, g0, h, false);
+        emit(out, POLAR_OP_F, level, (int)h, (int)g0, -1, 0);
+        compile_node(p, out, level + 1, g0, h, false, sc);
     }
     const int upos = left_zero ? -1 : (int)g0;
     if (tr == NODE_R1) {
-        emit(p, POLAR_OP_R1, level, (int)h, (int)(g0 + h), upos, 0);
+        emit(out, POLAR_OP_R1, level, (int)h, (int)(g0 + h), upos, 0);
     } else if (tr == NODE_SPC) {
-        emit(p, POLAR_OP_SPC, level, (int)h, (int)(g0 + h), upos, 0);
+        emit(out, POLAR_OP_SPC, level, (int)h, (int)(g0 + h), upos, 0);
     } else if (h == 1) {
-        emit(p, POLAR_OP_GLEAF, level, 1, (int)(g0 + h), upos, p.fb[g0 + h]);
+        emit(out, POLAR_OP_GLEAF, level, 1, (int)(g0 + h), upos, p.fb[g0 + h]);
     } else {
-        emit(p, POLAR_OP_G, level, (int)h, (int)(g0 + h), upos, 0);
-        compile_node(p, level + 1, g0 + h, h, false);
+        emit(out, POLAR_OP_G, level, (int)h, (int)(g0 + h), upos, 0);
+        compile_node(p, out, level + 1, g0 + h, h, false, sc);
     }
-    emit(p, left_zero ? POLAR_OP_H0 : POLAR_OP_H, level, (int)h, (int)g0, -1, 0);
+    emit(out, left_zero ? POLAR_OP_H0 : POLAR_OP_H, level, (int)h, (int)g0, -1, 0);
 }
 
 bool config_supported(const polar_sc_config &c)
@@ -183,11 +220,13 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
         st.simds = 4 * cus;
     }
-    if (p->jit) {
+    if (p->jit || p->hybrid) {
         int rc = polar_host::jit_load(*p, st);
         if (rc) return rc;
-        *out = &st;
-        return 0;
+        if (p->jit) {
+            *out = &st;
+            return 0;
+        }
     }
     if (!st.ops) {
         // device copy (+ a spare END: the interpreter loads record i+1 while running i)
@@ -223,13 +262,13 @@ int waves_per_group(const polar_sc_plan *p, size_t batch, int simds)
     const char *env = std::getenv("POLAR_SC_WAVES_PER_GROUP");
     if (env && *env) {
         int w = std::atoi(env);
-        if (w >= 1 && w <= 16 && (w & (w - 1)) == 0) return w;
+        if (w >= 1 && w <= 16 && (w & (w - 1)) == 0) return p->hybrid && w > polar_host::HYBRID_MAX_WAVES ? polar_host::HYBRID_MAX_WAVES : w;
     }
+    const int wmax = p->hybrid ? polar_host::HYBRID_MAX_WAVES : 16;
     const size_t groups = (batch + 7) / 8;
     const size_t target = 2u * (size_t)(simds > 0 ? simds : 1024);
     int w = 1;
-    while (w < 16 && groups * (size_t)w < target) w *= 2;
-    (void)p;
+    while (w < wmax && groups * (size_t)w < target) w *= 2;
     return w;
 }
 
@@ -244,6 +283,7 @@ int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size
     if (rc) return rc;
     if (p->jit) return polar_host::jit_launch(*p, *st, llr, out, (long)batch, out_stride, stream);
     const int wpg = waves_per_group(p, batch, st->simds);
+    if (p->hybrid) return polar_host::jit_launch_hybrid(*p, *st, llr, out, (long)batch, out_stride, wpg, stream);
     rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, (uint32_t *)st->scratch, (int)p->N, (long)batch,
                                 out_stride, wpg, 1, p->hbm_group_dwords, p->lds_group_dwords, p->lds0, stream);
     return rc ? -EIO : 0;
@@ -333,8 +373,8 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         default: s.n_rn++; break;
         }
     }
-    compile_node(*p, 0, 0, p->G, true);
-    emit(*p, POLAR_OP_END, 0, 0, 0, -1, 0);
+    compile_node(*p, p->ops, 0, 0, p->G, true, nullptr);
+    emit(p->ops, POLAR_OP_END, 0, 0, 0, -1, 0);
 
     s.N = N;
     s.K = p->K;
@@ -353,16 +393,41 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         p->lds0 = (int)p->G - LDS_LOW_SLOTS;
         p->hbm_group_dwords = p->lds0 * 32 + (int)nbd * 64;   // SM8-pair slots + bit dwords
         p->lds_group_dwords = ((int)nslot - p->lds0 + LDS_LOW_SLOTS / 16) * 64;
-        window_schedule(*p);
     } else {
         p->lds0 = 0;
         p->hbm_group_dwords = 0;
         p->lds_group_dwords = (int)(nslot + nbd) * 64;
     }
     while ((1u << p->lg) < p->G) p->lg++;
-    // per-mask register kernel for N <= 1024 unless POLAR_SC_JIT=0 (schedule interpreter)
+    // per-mask register kernel for N <= 1024; above, the hybrid kernel (interpreter + generated
+    // subtree decoders of POLAR_SC_SUB_WORDS words, default 64 = 1024 LLRs). POLAR_SC_JIT=0
+    // selects the plain schedule interpreter for every N.
     const char *jit_env = std::getenv("POLAR_SC_JIT");
-    p->jit = (polar_host::jit_supported(N) && !(jit_env && jit_env[0] == '0')) ? 1 : 0;
+    const bool jit_on = !(jit_env && jit_env[0] == '0');
+    p->jit = (polar_host::jit_supported(N) && jit_on) ? 1 : 0;
+    int sub_words = 64;
+    if (const char *e = std::getenv("POLAR_SC_SUB_WORDS")) {
+        if (*e) sub_words = std::atoi(e);
+    }
+    const bool sub_ok = sub_words >= 2 && sub_words <= 64 && (sub_words & (sub_words - 1)) == 0;
+    std::vector<polar_sc_op> dev_sched;
+    if (!p->jit && jit_on && sub_ok && (uint32_t)sub_words < p->G) {
+        SubCtx sc;
+        sc.words = (uint32_t)sub_words;
+        compile_node(*p, dev_sched, 0, 0, p->G, true, &sc);
+        emit(dev_sched, POLAR_OP_END, 0, 0, 0, -1, 0);
+        p->hybrid = 1;
+        p->sub_words = sub_words;
+        p->subs = std::move(sc.lists);
+        s.sub_words = (uint32_t)sub_words;
+        s.n_sub_kinds = (uint32_t)p->subs.size();
+        s.n_sub_calls = sc.calls;
+    } else {
+        dev_sched = p->ops;
+    }
+    if (p->gmem) window_schedule(*p, dev_sched);
+    else if (p->hybrid) p->dev_ops = dev_sched;
+    s.kernel = p->jit ? 1u : (p->hybrid ? 2u : 0u);
     s.storage = p->jit ? 2u : (uint32_t)p->gmem;
     s.lds_bytes_per_wave = p->jit ? 8u * (N + 16u) : (uint32_t)p->lds_group_dwords * 4u;
     s.scratch_bytes_per_wave = p->jit ? 0u : (uint64_t)p->hbm_group_dwords * 4u;
@@ -541,7 +606,7 @@ int polar_sc_plan_get_schedule(const polar_sc_plan *p, polar_sc_op *ops, uint32_
 int polar_sc_plan_compile(const polar_sc_plan *p)
 {
     if (!p) return -EINVAL;
-    if (!p->jit) return -ENOTSUP;
+    if (!p->jit && !p->hybrid) return -ENOTSUP;
     std::lock_guard<std::mutex> lk(p->mu);
     return polar_host::jit_compile(*p);
 }
@@ -549,7 +614,7 @@ int polar_sc_plan_compile(const polar_sc_plan *p)
 int polar_sc_plan_kernel_source(const polar_sc_plan *p, char *buf, size_t cap, size_t *len)
 {
     if (!p || !len) return -EINVAL;
-    if (!p->jit) return -ENOTSUP;
+    if (!p->jit && !p->hybrid) return -ENOTSUP;
     const std::string src = polar_host::jit_source(*p);
     *len = src.size();
     if (buf && cap) {

@@ -7,8 +7,10 @@
 // compiled schedule (polar_sc_op list) is unrolled into straight-line HIP: every stage
 // buffer is a register array with compile-time indices, every partial-sum position and
 // every leaf frozen pattern is a constant, and there is no interpreter loop at all.
-// Used for N <= 1024 (all stage buffers fit in VGPRs); larger N use the schedule
-// interpreter in polar_sc_kernels.hip.
+// Used for N <= 1024 (all stage buffers fit in VGPRs). Larger N use hybrid kernels: the
+// schedule interpreter (polar_sc_interp.h) for the upper tree levels, with every mixed
+// subtree of sub_words words (1024 LLRs by default) decoded by generated straight-line code
+// of the same kind.
 #include "polar_sc_plan.hpp"
 
 #include <hip/hiprtc.h>
@@ -20,6 +22,7 @@
 
 namespace {
 #include "polar_sc_device_src.inc"   // kPolarDeviceSrc: polar_sc_device.h as a string
+#include "polar_sc_interp_src.inc"   // kPolarInterpSrc: polar_sc_interp.h as a string
 }
 
 namespace polar_host {
@@ -29,10 +32,10 @@ bool jit_supported(uint32_t N) { return N >= 32 && N <= 1024; }
 namespace {
 
 struct Gen {
-    const polar_sc_plan &p;
+    const std::vector<polar_sc_op> &ops;   // schedule of the code (or subtree) of 16 * 2^LG LLRs
     std::ostringstream o;
     int LG;
-    explicit Gen(const polar_sc_plan &pp) : p(pp), LG(pp.lg) {}
+    Gen(const std::vector<polar_sc_op> &ops_, int lg) : ops(ops_), LG(lg) {}
 
     // Partial sums: u32 bw[max(1, G / 16)], dword j = groups 16 j .. 16 j + 15, low frame in
     // bits 0..15 and high frame in bits 16..31 (the layout every consumer wants, so H ops
@@ -127,11 +130,32 @@ struct Gen {
             o << "    X_[" << k << "] = " << P(sd, 16 * k) << " ^ " << P(sd, n + 16 * k) << " ^ " << U(upos, k) << ";\n";
     }
 
+    // A subtree decoder's root children can be REP / R1 / SPC (the root of a whole code's
+    // never are): those ops read split words, so the root words are split into m<LG> / s<LG>
+    // from CH() first.
+    bool root_split_needed() const
+    {
+        for (const polar_sc_op &op : ops)
+            if (op.level == 0 && (op.code == POLAR_OP_REP || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC))
+                return true;
+        return false;
+    }
+    void root_split(int words)
+    {
+        for (int k = 0; k < planes(words); k++) o << "    s" << LG << "[" << k << "] = 0u;\n";
+        for (int i = 0; i < words; i++) {
+            o << "    { const u32 v_ = CH(" << i << "); " << M(LG, i) << " = v_ & MAG; s" << LG << "[" << i / 16
+              << "] = plane_put<" << i % 16 << ">(s" << LG << "[" << i / 16 << "], v_); }\n";
+            chunk_fence(i, words);
+        }
+    }
+
     void op(const polar_sc_op &op)
     {
         const int sd = LG - op.level, cd = sd - 1, n = op.n, np = planes(n);
         const bool root = sd == LG;
         fence();
+        if (root && (op.code == POLAR_OP_REP || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC)) root_split(2 * n);
         switch (op.code) {
         case POLAR_OP_F:
             o << "  { // F level " << op.level << " n " << n << "\n";
@@ -303,7 +327,46 @@ struct Gen {
         }
     }
 
-    std::string run()
+    void stage_arrays(bool with_root)
+    {
+        for (int d = 1; d < LG; d++)
+            o << "  u32 m" << d << "[" << (1 << d) << "], s" << d << "[" << planes(1 << d) << "];\n";
+        if (with_root) o << "  u32 m" << LG << "[" << (1 << LG) << "], s" << LG << "[" << planes(1 << LG) << "];\n";
+    }
+    void all_ops()
+    {
+        for (const polar_sc_op &op : ops) {
+            if (op.code == POLAR_OP_END) break;
+            this->op(op);
+        }
+    }
+
+    // Subtree decoder `id` of a hybrid plan (polar_sc_interp.h, OP_SUB): the root words come
+    // from the interpreter's LDS stage slot (SM16), the partial sums go back to its bit
+    // storage at word `pos`.
+    void sub_function(int id, bool gmem)
+    {
+        const int words = 1 << LG;
+        const char *ctx = gmem ? "Ctx<true>" : "Ctx<false>";
+        o << "__device__ __noinline__ void polar_sub_" << id << "(const " << ctx << " &c, int ldo, int pos)\n{\n"
+          << "  extern __shared__ __attribute__((aligned(16))) u32 smem[];\n"
+          << "  const u32 *cin_ = smem + ldo;\n"
+          << "  const Lanes ln = c.ln;\n"
+          << "  u32 bw[" << (words >= 16 ? words / 16 : 1) << "] = {};\n";
+        stage_arrays(root_split_needed());
+        all_ops();
+        if (words >= 16) {
+            for (int j = 0; j < words / 16; j++) o << "  c.bst((pos >> 4) + " << j << ", bw[" << j << "]);\n";
+        } else {
+            const unsigned m = (1u << words) - 1u;
+            o << "  { const u32 m_ = 0x" << std::hex << (m | (m << 16)) << std::dec << "u << (pos & 15);\n"
+              << "    const u32 d_ = c.bld(pos >> 4);\n"
+              << "    c.bst(pos >> 4, (d_ & ~m_) | ((bw[0] << (pos & 15)) & m_)); }\n";
+        }
+        o << "}\n\n";
+    }
+
+    std::string run_mask(const polar_sc_plan &p)
     {
         const int N = (int)p.N, G = (int)p.G;
         // Channel staging: each wave copies its 8 frames (8 x N bytes, contiguous rows of the
@@ -345,12 +408,8 @@ struct Gen {
           << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
           << " + ln.pos;\n"
           << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
-        for (int d = 1; d < LG; d++)
-            o << "  u32 m" << d << "[" << (1 << d) << "], s" << d << "[" << planes(1 << d) << "];\n";
-        for (const polar_sc_op &op : p.ops) {
-            if (op.code == POLAR_OP_END) break;
-            this->op(op);
-        }
+        stage_arrays(false);
+        all_ops();
         // END (my_module.h:1848-1869) + wrapper_out: x^ words in natural order
         o << "  const bool st_lo = f_lo < batch, st_hi = f_hi < batch;\n"
           << "  unsigned short *o_lo = out + (size_t)f_lo * out_stride, *o_hi = out + (size_t)f_hi * out_stride;\n";
@@ -367,16 +426,50 @@ struct Gen {
 
 }  // namespace
 
-std::string jit_source(const polar_sc_plan &p) { return Gen(p).run(); }
+// Hybrid plan: the schedule interpreter (polar_sc_interp.h, with OP_SUB) plus one generated
+// subtree decoder per distinct mixed subtree of p.sub_words words.
+std::string hybrid_source(const polar_sc_plan &p)
+{
+    std::ostringstream o;
+    const bool gm = p.gmem != 0;
+    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_SC_SUBS 1\n#include \"polar_sc_interp.h\"\n"
+      << "namespace polar {\n#define CH(w) cin_[(w) * 64]\n";
+    int lg = 0;
+    while ((1 << lg) < p.sub_words) lg++;
+    for (size_t id = 0; id < p.subs.size(); id++) {
+        Gen g(p.subs[id], lg);
+        g.sub_function((int)id, gm);
+        o << g.o.str();
+    }
+    const char *ctx = gm ? "Ctx<true>" : "Ctx<false>";
+    o << "#undef CH\ntemplate <>\n__device__ void polar_sub_call<" << (gm ? "true" : "false") << ">(const " << ctx
+      << " &c, int id, int ldo, int pos)\n{\n  switch (id) {\n";
+    for (size_t id = 0; id < p.subs.size(); id++)
+        o << "  case " << id << ": polar_sub_" << id << "(c, ldo, pos); return;\n";
+    o << "  default: return;\n  }\n}\n}  // namespace polar\n"
+      << "extern \"C\" __global__ void __launch_bounds__(" << HYBRID_MAX_WAVES * 64 << ") polar_sc_hybrid_kernel(\n"
+      << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
+      << "    unsigned int *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb, int group_dwords,\n"
+      << "    int lds_dwords, int lds0)\n{\n"
+      << "  polar::decode_body<" << (gm ? "true" : "false")
+      << ">(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords, lds0);\n}\n";
+    return o.str();
+}
+
+std::string jit_source(const polar_sc_plan &p)
+{
+    if (p.hybrid) return hybrid_source(p);
+    return Gen(p.ops, p.lg).run_mask(p);
+}
 
 int jit_compile(const polar_sc_plan &p)
 {
     if (!p.jit_code.empty()) return 0;
     const std::string src = jit_source(p);
     hiprtcProgram prog;
-    const char *hdrs[] = {kPolarDeviceSrc};
-    const char *names[] = {"polar_sc_device.h"};
-    if (hiprtcCreateProgram(&prog, src.c_str(), "polar_sc_mask.hip", 1, hdrs, names) != HIPRTC_SUCCESS) return -EIO;
+    const char *hdrs[] = {kPolarDeviceSrc, kPolarInterpSrc};
+    const char *names[] = {"polar_sc_device.h", "polar_sc_interp.h"};
+    if (hiprtcCreateProgram(&prog, src.c_str(), "polar_sc_mask.hip", 2, hdrs, names) != HIPRTC_SUCCESS) return -EIO;
     const char *opts[] = {"--gpu-architecture=gfx950", "-O3", "-std=c++17"};
     hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
     size_t log_size = 0;
@@ -403,7 +496,9 @@ int jit_load(const polar_sc_plan &p, DevState &st)
     int rc = jit_compile(p);
     if (rc) return rc;
     if (hipModuleLoadData(&st.module, p.jit_code.data()) != hipSuccess) return -EIO;
-    if (hipModuleGetFunction(&st.fn, st.module, "polar_sc_mask_kernel") != hipSuccess) return -EIO;
+    if (hipModuleGetFunction(&st.fn, st.module, p.hybrid ? "polar_sc_hybrid_kernel" : "polar_sc_mask_kernel") !=
+        hipSuccess)
+        return -EIO;
     return 0;
 }
 
@@ -416,6 +511,22 @@ int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, ui
     int b = (int)batch;
     void *args[] = {(void *)&llr, (void *)&out, (void *)&b, (void *)&out_stride};
     hipError_t e = hipModuleLaunchKernel(st.fn, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream, args, nullptr);
+    return e == hipSuccess ? 0 : -EIO;
+}
+
+// hybrid kernel: the interpreter's launch shape (polar_sc_kernels.hip, polar_sc_launch_decode)
+int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
+                      int out_stride, int wpg, void *stream)
+{
+    const long groups = (batch + 7) / 8;
+    const unsigned lds = (unsigned)p.lds_group_dwords * 4u;
+    const void *ops = st.ops;
+    void *scratch = st.scratch;
+    int N = (int)p.N, b = (int)batch, gpb = 1, gd = p.hbm_group_dwords, ld = p.lds_group_dwords, l0 = p.lds0;
+    void *args[] = {(void *)&llr, (void *)&out, (void *)&ops, (void *)&scratch, (void *)&N, (void *)&b,
+                    (void *)&out_stride, (void *)&wpg, (void *)&gpb, (void *)&gd, (void *)&ld, (void *)&l0};
+    hipError_t e = hipModuleLaunchKernel(st.fn, (unsigned)groups, 1, 1, (unsigned)(64 * wpg), 1, 1, lds,
+                                         (hipStream_t)stream, args, nullptr);
     return e == hipSuccess ? 0 : -EIO;
 }
 

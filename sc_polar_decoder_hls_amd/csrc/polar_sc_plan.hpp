@@ -32,8 +32,13 @@ struct HostBufs {
     size_t frames = 0;
 };
 
-// device-internal schedule records of HBM-scratch plans (never exported)
-enum { POLAR_OP_WOPEN = 11, POLAR_OP_WFLUSH = 12 };
+// device-internal schedule records (never exported): the partial-sum window of HBM-scratch
+// plans, and the generated-subtree call of hybrid plans
+enum { POLAR_OP_WOPEN = 11, POLAR_OP_WFLUSH = 12, POLAR_OP_SUB = 13 };
+
+// hybrid kernels: at most 4 waves per 8-frame group (one block), so the subtree decoders get
+// the register budget of a 256-thread block
+constexpr int HYBRID_MAX_WAVES = 4;
 
 }  // namespace polar_host
 
@@ -52,6 +57,12 @@ struct polar_sc_plan {
     // first stage slot held in LDS (polar_sc_kernels.hip, Ctx)
     int hbm_group_dwords = 0, lds_group_dwords = 0, lds0 = 0;
     int jit = 0;                     // 1: decode with the per-mask kernel
+    // hybrid plans (N > 1024): the device schedule stops at every mixed node of sub_words
+    // words with a POLAR_OP_SUB record; subs[id] is that subtree's own schedule (levels and
+    // positions relative to the subtree root), compiled to straight-line code
+    int hybrid = 0;
+    int sub_words = 0;
+    std::vector<std::vector<polar_sc_op>> subs;
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;
     mutable std::mutex host_mu;                             // polar_sc_decode_host staging
@@ -68,5 +79,7 @@ int jit_compile(const polar_sc_plan &p);                 // fills p.jit_code (id
 int jit_load(const polar_sc_plan &p, DevState &st);      // module + function on this device
 int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out,
                long batch, int out_stride, void *stream);
+int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
+                      int out_stride, int wpg, void *stream);
 bool jit_supported(uint32_t N);
 }  // namespace polar_host

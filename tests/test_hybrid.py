@@ -1,0 +1,113 @@
+"""Hybrid plans (N > 1024): the schedule interpreter for the upper tree levels plus generated
+straight-line decoders for every mixed subtree of POLAR_SC_SUB_WORDS words
+(polar_sc_interp.h OP_SUB, polar_sc_jit.cpp hybrid_source).
+
+CPU tests: plan statistics and hipRTC compilation of the generated source (no GPU needed).
+GPU tests: bit-exact against the oracle for every subtree size, including subtrees whose root
+children are REP / R1 / SPC nodes (the root-split path of the generator), and against the
+plain interpreter on a full C3 batch."""
+import os
+
+import numpy as np
+import pytest
+
+import util
+
+
+def make(pkg, mask, jit="1", sub_words=None):
+    keys = {"POLAR_SC_JIT": jit, "POLAR_SC_SUB_WORDS": None if sub_words is None else str(sub_words)}
+    old = {k: os.environ.get(k) for k in keys}
+    try:
+        for k, v in keys.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        return pkg.Decoder(mask)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def structured_mask(rng, N):
+    """16-bit groups drawn from the pruned node patterns (R0, R1, REP, SPC) and random ones,
+    so subtree roots get REP / R1 / SPC children."""
+    pats = [0, 0xFFFF, 0x8000, 0xFFFE, int(rng.integers(0, 65536))]
+    groups = rng.choice(pats, N // 16)
+    return np.concatenate([[(int(p) >> k) & 1 for k in range(16)] for p in groups]).astype(np.uint8)
+
+
+def test_hybrid_plan_stats(pkg):
+    s = make(pkg, util.mask("frozen_n_65536_k_32768")).stats
+    assert (s["kernel"], s["sub_words"], s["n_sub_kinds"], s["n_sub_calls"]) == (2, 64, 43, 47)
+    assert s["storage"] == 1
+    s = make(pkg, util.mask("FB_N1024_K512")).stats
+    assert s["kernel"] == 1 and s["sub_words"] == 0
+    s = make(pkg, util.mask("frozen_n_65536_k_32768"), jit="0").stats
+    assert s["kernel"] == 0 and s["n_sub_calls"] == 0
+    s = make(pkg, util.mask("frozen_n_8192_k_4096"), sub_words=8).stats
+    assert s["kernel"] == 2 and s["sub_words"] == 8 and s["n_sub_calls"] >= s["n_sub_kinds"] > 0
+
+
+def test_hybrid_schedule_export_unchanged(pkg):
+    """The exported schedule stays the plain op list (no device-internal records)."""
+    mask = util.mask("frozen_n_8192_k_4096")
+    a = make(pkg, mask).schedule()
+    b = make(pkg, mask, jit="0").schedule()
+    assert a == b and all(o["op"] in ("F", "G", "FLEAF", "GLEAF", "REP", "R1", "SPC", "H", "H0", "END") for o in a)
+
+
+@pytest.mark.parametrize("sub_words", [2, 8, 64])
+def test_hybrid_source_compiles(pkg, sub_words):
+    rng = np.random.default_rng(sub_words)
+    dec = make(pkg, structured_mask(rng, 4096), sub_words=sub_words)
+    src = dec.kernel_source()
+    assert "polar_sc_hybrid_kernel" in src and "polar_sub_0(" in src
+    dec.compile()   # hipRTC for gfx950 on the host
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sub_words", [2, 4, 8, 16, 32, 64])
+def test_hybrid_parity_sub_sizes(pkg, cuda, oracle_mod, sub_words):
+    rng = np.random.default_rng(100 + sub_words)
+    cases = [structured_mask(rng, 2048), structured_mask(rng, 4096), util.mask("frozen_n_4096_k_2048"),
+             (rng.random(2048) < np.linspace(0, 1, 2048) ** 0.5).astype(np.uint8)]
+    for ci, mask in enumerate(cases):
+        dec = make(pkg, mask, sub_words=sub_words)
+        assert dec.stats["kernel"] == 2
+        llr = rng.integers(-32, 32, size=(11, mask.size)).astype(np.int8)
+        out = dec.decode(cuda.from_numpy(llr).cuda())
+        cuda.cuda.synchronize()
+        got = pkg.unpack_bits(out.cpu().numpy(), mask.size)
+        ref = oracle_mod.decode_fsm(mask, llr)
+        bad = np.nonzero((got != ref).any(axis=1))[0]
+        assert bad.size == 0, "sub_words %d case %d: frames %s differ" % (sub_words, ci, bad[:8])
+
+
+@pytest.mark.gpu
+def test_hybrid_hbm_scratch_sub_sizes(pkg, cuda, oracle_mod):
+    """HBM-scratch plans (N = 8192): subtrees inside and across the LDS partial-sum window."""
+    mask = util.mask("frozen_n_8192_k_4096")
+    llr, _ = util.synth_frames(mask, 9, ebn0_db=1.0, seed=8192)
+    ref = oracle_mod.decode_fsm(mask, llr)
+    for sw in (4, 32, 64):
+        dec = make(pkg, mask, sub_words=sw)
+        assert dec.stats["storage"] == 1 and dec.stats["kernel"] == 2
+        out = dec.decode(cuda.from_numpy(llr).cuda())
+        cuda.cuda.synchronize()
+        np.testing.assert_array_equal(pkg.unpack_bits(out.cpu().numpy(), mask.size), ref, err_msg="sub %d" % sw)
+
+
+@pytest.mark.gpu
+def test_hybrid_equals_interpreter_full_c3(pkg, cuda):
+    """Full BASELINE C3 batch (4096 frames of N = 65536): hybrid == plain interpreter."""
+    import bench
+    mask = util.mask("frozen_n_65536_k_32768")
+    llr, _ = bench.gen_frames_torch(cuda, mask, 4096, 2.0, 3, cuda.device("cuda"))
+    outs = [make(pkg, mask, jit=j).decode(llr) for j in ("1", "0")]
+    cuda.cuda.synchronize()
+    assert cuda.equal(outs[0], outs[1])
