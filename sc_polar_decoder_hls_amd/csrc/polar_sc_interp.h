@@ -84,6 +84,8 @@ struct Ctx {
     __device__ __forceinline__ void stl(int slot, uint32_t v) const { lb[(slot - lds0) * 64] = v; }
     __device__ __forceinline__ void sth(int slot, uint32_t v) const { hs[slot * 64] = (uint16_t)sm16_to_sm8x2(v); }
     __device__ __forceinline__ uint32_t ld(int slot) const { return in_lds(slot) ? ldl(slot) : ldh(slot); }
+    // storage known at compile time (callers branch once per op on in_lds)
+    template <bool L> __device__ __forceinline__ uint32_t ldx(int slot) const { return L ? ldl(slot) : ldh(slot); }
     __device__ __forceinline__ void st(int slot, uint32_t v) const
     {
         if (in_lds(slot)) stl(slot, v);
@@ -156,33 +158,35 @@ __device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int
         else c.sth(dst + w, v);
     };
     int i = i0;
-    // 8 words per iteration: 16 independent source loads in flight (HBM latency)
-    for (; i + 8 <= i1; i += 8) {
-        uint32_t a[8], b[8], r[8];
+    // CH words per iteration: 2 CH independent source loads in flight (16 for HBM sources:
+    // the upper levels are latency-bound on the few waves of a group)
+    constexpr int CH = (SL || ROOT) ? 8 : 16;
+    for (; i + CH <= i1; i += CH) {
+        uint32_t a[CH], b[CH], r[CH];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < CH; j++) {
             a[j] = src(i + j);
             b[j] = src(n + i + j);
         }
         if constexpr (ISG) {
-            // partial sums of words upos+i .. upos+i+7 (at most two bit dwords)
+            // partial sums of words upos+i .. upos+i+CH-1 (at most two bit dwords)
             uint32_t u0 = 0, u1 = 0;
             if (upos >= 0) {
                 u0 = c.bld((upos + i) >> 4);
-                u1 = c.bld((upos + i + 7) >> 4);
+                u1 = c.bld((upos + i + CH - 1) >> 4);
             }
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
+            for (int j = 0; j < CH; j++) {
                 const int q = upos + i + j;
                 const uint32_t u = (upos >= 0) ? ubit(((q >> 4) == ((upos + i) >> 4)) ? u0 : u1, q) : 0u;
                 r[j] = G_sm<15>(a[j], b[j], u);
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < 8; j++) r[j] = F_sm(a[j], b[j]);
+            for (int j = 0; j < CH; j++) r[j] = F_sm(a[j], b[j]);
         }
 #pragma unroll
-        for (int j = 0; j < 8; j++) put(i + j, r[j]);
+        for (int j = 0; j < CH; j++) put(i + j, r[j]);
     }
     for (; i < i1; i++) {
         const uint32_t a = src(i), b = src(n + i);
@@ -239,22 +243,33 @@ __device__ __forceinline__ void op_leaf(const C &c, int k, int pos, int upos, ui
 // F_REP_STATE (my_module.h:1292-1390): lambda = F(parent); per word the 16-lane exact SM
 // adder tree, accumulated over words in order by the 11-bit saturating SM adder
 // (ADDER_TREE_16, functions.h:3190-3205); x = all sign(acc).
-template <class C>
-__device__ __forceinline__ void op_rep(const C &c, int k, int n, int pos)
+template <bool L, class C>
+__device__ __forceinline__ void rep_body(const C &c, int s0, int n, int pos)
 {
-    const int s0 = c.lvl_off(k);
     // value chain in two's complement (exact sums and 511 clamps, polar_sc_device.h); the
-    // exact SM chain only when some frame ends on a zero total (sign-of-zero rule)
+    // exact SM chain only when some frame ends on a zero total (sign-of-zero rule). Source
+    // words are loaded 8 at a time (one round trip per 8 words for HBM slots).
     uint32_t acc = 0;
-    for (int i = 0; i < n; i++) {
-        const uint32_t lam = F_sm(c.ld(s0 + i), c.ld(s0 + n + i));
+    auto word = [&](uint32_t lam) {
         const uint32_t sg = pk_sra(lam, 15);
         acc = rep_acc(acc, row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
+    };
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint32_t a[8], b[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a[j] = c.template ldx<L>(s0 + i + j);
+            b[j] = c.template ldx<L>(s0 + n + i + j);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) word(F_sm(a[j], b[j]));
     }
+    for (; i < n; i++) word(F_sm(c.template ldx<L>(s0 + i), c.template ldx<L>(s0 + n + i)));
     if (rep_any_zero(acc)) {
         acc = 0;
-        for (int i = 0; i < n; i++) {
-            uint32_t lam = F_sm(c.ld(s0 + i), c.ld(s0 + n + i));
+        for (i = 0; i < n; i++) {
+            uint32_t lam = F_sm(c.template ldx<L>(s0 + i), c.template ldx<L>(s0 + n + i));
             uint32_t t = row_add_tree(lam, c.ln);
             acc = G_sm<511>(t, acc, 0u);
         }
@@ -268,24 +283,31 @@ __device__ __forceinline__ void op_rep(const C &c, int k, int n, int pos)
     }
 }
 
+template <class C>
+__device__ __forceinline__ void op_rep(const C &c, int k, int n, int pos)
+{
+    const int s0 = c.lvl_off(k);
+    if (c.in_lds(s0)) rep_body<true>(c, s0, n, pos);
+    else rep_body<false>(c, s0, n, pos);
+}
+
 // G_R1_STATE (my_module.h:1571-1642) and G_SPC_STATE (my_module.h:1737-1842):
 // lambda = G(parent, bits[upos..]); x = sign(lambda); SPC additionally flips the first
 // minimum-|lambda| position (lexicographic (|l|, word, bitrev4(lane)) == Min_Mask_16_SM
 // tournament + strict '<' across words) when the parity of x is odd.
 // [i0, i1): the words of this wave (R1 split in whole 16-word chunks; SPC is never split).
-template <bool SPC, class C>
-__device__ __forceinline__ void op_r1spc(const C &c, int k, int n, int upos, int pos, int i0, int i1)
+template <bool SPC, bool L, class C>
+__device__ __forceinline__ void r1spc_body(const C &c, int s0, int n, int upos, int pos, int i0, int i1)
 {
-    const int s0 = c.lvl_off(k);
     uint32_t ud = 0, acc = 0, par = 0;
     uint32_t key_lo = 0xFFFFFFFFu, key_hi = 0xFFFFFFFFu;
-    for (int i = i0; i < i1; i++) {
+    auto word = [&](int i, uint32_t a, uint32_t b) {
         uint32_t u = 0;
         if (upos >= 0) {
             if (((upos + i) & 15) == 0 || i == i0) ud = c.bld((upos + i) >> 4);
             u = ubit(ud, upos + i);
         }
-        uint32_t lam = G_sm<15>(c.ld(s0 + i), c.ld(s0 + n + i), u);
+        uint32_t lam = G_sm<15>(a, b, u);
         uint32_t h = lam & SGN;
         int q = (pos + i) & 15;
         acc |= h >> (15 - q);
@@ -297,7 +319,20 @@ __device__ __forceinline__ void op_r1spc(const C &c, int k, int n, int upos, int
             key_lo = __builtin_elementwise_min(key_lo, klo);
             key_hi = __builtin_elementwise_min(key_hi, khi);
         }
+    };
+    // source words 8 at a time (one round trip per 8 words for HBM slots), used in order
+    int i = i0;
+    for (; i + 8 <= i1; i += 8) {
+        uint32_t a[8], b[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a[j] = c.template ldx<L>(s0 + i + j);
+            b[j] = c.template ldx<L>(s0 + n + i + j);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) word(i + j, a[j], b[j]);
     }
+    for (; i < i1; i++) word(i, c.template ldx<L>(s0 + i), c.template ldx<L>(s0 + n + i));
     if (n < 16) bits_put_small(c, pos, n, acc);
     if constexpr (SPC) {
         par = row_xor(par);
@@ -316,6 +351,19 @@ __device__ __forceinline__ void op_r1spc(const C &c, int k, int n, int upos, int
     }
 }
 
+// G_R1_STATE (my_module.h:1571-1642) and G_SPC_STATE (my_module.h:1737-1842):
+// lambda = G(parent, bits[upos..]); x = sign(lambda); SPC additionally flips the first
+// minimum-|lambda| position (lexicographic (|l|, word, bitrev4(lane)) == Min_Mask_16_SM
+// tournament + strict '<' across words) when the parity of x is odd.
+// [i0, i1): the words of this wave (R1 split in whole 16-word chunks; SPC is never split).
+template <bool SPC, class C>
+__device__ __forceinline__ void op_r1spc(const C &c, int k, int n, int upos, int pos, int i0, int i1)
+{
+    const int s0 = c.lvl_off(k);
+    if (c.in_lds(s0)) r1spc_body<SPC, true>(c, s0, n, upos, pos, i0, i1);
+    else r1spc_body<SPC, false>(c, s0, n, upos, pos, i0, i1);
+}
+
 // H_STATE / H0_STATE (my_module.h:903-932, 1020-1042):
 // bits[pos..pos+n) = bits[pos..pos+n) ^ bits[pos+n..pos+2n)   (H)
 //                  = bits[pos+n..pos+2n)                      (H0)
@@ -325,7 +373,18 @@ __device__ __forceinline__ void op_h(const C &c, int pos, int n, int j0, int j1)
 {
     if (n >= 16) {
         const int da = pos >> 4, db = (pos + n) >> 4;
-        for (int j = j0; j < j1; j++) {
+        int j = j0;
+        for (; j + 8 <= j1; j += 8) {   // 8 dwords per round trip
+            uint32_t a[8], b[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                b[t] = c.bld(db + j + t);
+                a[t] = H0 ? 0u : c.bld(da + j + t);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; t++) c.bst(da + j + t, a[t] ^ b[t]);
+        }
+        for (; j < j1; j++) {
             uint32_t b = c.bld(db + j);
             c.bst(da + j, H0 ? b : (c.bld(da + j) ^ b));
         }

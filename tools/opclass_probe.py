@@ -4,8 +4,8 @@
 build (container):  python tools/opclass_probe.py build
     Builds variants of libpolar_sc.so into build_tools/opclass/ from a patched temporary
     copy of csrc/polar_sc_interp.h in which one class of ops is skipped (results are
-    wrong; the product sources are not modified). Plain interpreter only: run with
-    POLAR_SC_JIT=0 for N > 1024 (hybrid plans compile the unpatched header with hipRTC).
+    wrong; the product sources are not modified). The patched header is also embedded for
+    hipRTC, so hybrid plans (N > 1024) run the patched loop too.
 run (GPU box):      python tools/opclass_probe.py run [--mask M --batch B]
     Times the decode with every variant (each in its own process) and prints JSON lines.
 """
@@ -27,6 +27,9 @@ VARIANTS = {
     "no_h": "if (code == OP_H || code == OP_H0) continue;",
     "no_narrow_fg": "if ((code == OP_F || code == OP_G) && !split) continue;",
     "no_wide_fg": "if ((code == OP_F || code == OP_G) && split) continue;",
+    # hybrid plans (POLAR_SC_JIT=1, N > 1024): the generated subtree calls vs the rest
+    "no_sub": "if (code == OP_SUB) continue;",
+    "only_sub": "if (code != OP_SUB) continue;",
 }
 ANCHOR = "        if (!split && wi != lead) continue;\n"
 # cycle-accounting variant: s_memtime around every op and barrier; wave 0 of group 0 prints
@@ -61,6 +64,16 @@ CYC_PATCHES = [
 ]
 
 
+def copy_sources(tmp, name):
+    """csrc/ and include/ in the repository layout (polar_sc_plan.hpp includes ../../include)."""
+    from sc_polar_decoder_hls_amd import _build
+    base = os.path.join(tmp, name)
+    kdir = os.path.join(base, "pkg", "csrc")
+    shutil.copytree(os.path.join(_build.PKG, "csrc"), kdir)
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(base, "include"))
+    return kdir
+
+
 def build_cycles():
     """libpolar_sc_cycles.so: the interpreter with per-op-type cycle accounting (printf)."""
     sys.path.insert(0, ROOT)
@@ -71,8 +84,7 @@ def build_cycles():
     for a, b in CYC_PATCHES:
         assert a in src, a
         src = src.replace(a, b, 1)
-    kdir = os.path.join(tmp, "cyc")
-    shutil.copytree(os.path.join(_build.PKG, "csrc"), kdir)
+    kdir = copy_sources(tmp, "cyc")
     with open(os.path.join(kdir, "polar_sc_interp.h"), "w") as f:
         f.write(src)
     out = os.path.join(OUTD, "libpolar_sc_cycles.so")
@@ -93,13 +105,19 @@ def build():
     src = open(os.path.join(_build.PKG, "csrc", "polar_sc_interp.h")).read()
     assert ANCHOR in src
     for name, skip in VARIANTS.items():
-        kdir = os.path.join(tmp, name)
-        shutil.copytree(os.path.join(_build.PKG, "csrc"), kdir)
+        kdir = copy_sources(tmp, name)
+        patched = src.replace(ANCHOR, ANCHOR + ("        " + skip + "\n" if skip else ""))
         with open(os.path.join(kdir, "polar_sc_interp.h"), "w") as f:
-            f.write(src.replace(ANCHOR, ANCHOR + ("        " + skip + "\n" if skip else "")))
+            f.write(patched)
+        # the hybrid kernel compiles the embedded header text with hipRTC: embed the patched one
+        gen = os.path.join(kdir, "gen")
+        os.makedirs(gen)
+        shutil.copy(os.path.join(_build.GEN_DIR, "polar_sc_device_src.inc"), gen)
+        with open(os.path.join(gen, "polar_sc_interp_src.inc"), "w") as f:
+            f.write("static const char kPolarInterpSrc[] = R\"POLARSRC(" + patched + ")POLARSRC\";\n")
         out = os.path.join(OUTD, "libpolar_sc_%s.so" % name)
         cmd = [_build.hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-I" + os.path.join(ROOT, "include"), "-I" + _build.GEN_DIR,
+               "-I" + os.path.join(ROOT, "include"), "-I" + gen,
                os.path.join(kdir, "polar_sc_kernels.hip"), os.path.join(kdir, "polar_sc_host.cpp"),
                os.path.join(kdir, "polar_sc_jit.cpp"), os.path.join(kdir, "polar_sc_channel.hip"), "-o", out,
                "-lhiprtc"]
