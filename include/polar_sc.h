@@ -207,6 +207,30 @@ int polar_csim_states(uint32_t N, uint32_t seed8, uint64_t frame0, size_t batch,
 int polar_count_errors(const uint64_t *xhat_dev, const uint64_t *xref_dev, uint32_t N, size_t batch,
                        unsigned long long *counts_dev, void *stream);
 
+/* ---- Frozen-table tooling: Frozen_Bit_Generator (main.cpp:12-52, src/Writer.h:21-167) ---- */
+
+/* Writer.h:61-93: keep the entries of a reliability order (most reliable first) that are
+ * < N; the first K of them are information bits. mask_out: N bytes (cap >= N), 1 = info.
+ * -EINVAL unless exactly N distinct entries remain. */
+int polar_mask_from_order(const uint32_t *order, uint32_t count, uint32_t N, uint32_t K, uint8_t *mask_out,
+                          uint32_t cap);
+
+/* Writer.h:71-79: the FB_N{N}_K{K}.txt ("affect") text of that subset order. Text goes to
+ * buf (NUL-terminated, truncated to cap); *len = full length. */
+int polar_write_frozen_tab(const uint32_t *order, uint32_t count, uint32_t N, char *buf, size_t cap,
+                           size_t *len);
+
+/* Writer.h:110-162: polar_parameters.h for an information mask, byte for byte as the
+ * reference generator writes it. par: PAR (power of two <= N); concat: the generator's En
+ * (1 = PAR-wide strings, 0 = one sc_bv<1> per bit). Output as for polar_write_frozen_tab. */
+int polar_write_parameters_h(const uint8_t *info_mask, uint32_t N, uint32_t par, int32_t concat, char *buf,
+                             size_t cap, size_t *len);
+
+/* Read a polar_parameters.h (either form) back: mask_out (cap >= N bytes, 1 = info),
+ * *N_out = _NBITS, *par_out = PAR. */
+int polar_parse_parameters_h(const char *path, uint8_t *mask_out, uint32_t cap, uint32_t *N_out,
+                             uint32_t *par_out);
+
 /* GPU self-test of the cross-lane (DPP) exchange patterns the kernels rely on.
  * out_dev: 4*64 uint32 on the device; entry [h][lane] = source lane seen by `lane` for
  * partner distance 1<<h. Synchronous. */

@@ -28,6 +28,18 @@ def build(force=False):
     return _LIB_PATH
 
 
+REF_SRC = "/root/reference"
+FBGEN = os.path.join(_HERE, "_ref", "fb_generator")
+
+
+def build_ref():
+    """Compile the reference's Frozen_Bit_Generator into oracle/_ref/ (only where the reference
+    sources exist, i.e. in the build container); returns the binary path or None."""
+    if os.path.exists(os.path.join(REF_SRC, "Frozen_Bit_Generator", "main.cpp")):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "ref", "REF=" + REF_SRC])
+    return FBGEN if os.path.exists(FBGEN) else None
+
+
 def lib():
     global _lib
     if _lib is None:

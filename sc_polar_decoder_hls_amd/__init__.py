@@ -74,6 +74,7 @@ EXPORTS = (
     "polar_sc_plan_get_schedule", "polar_sc_selftest_lanes", "polar_sc_strerror",
     "polar_sc_abi_version", "polar_sc_plan_compile", "polar_sc_plan_kernel_source",
     "polar_csim_frames", "polar_csim_states", "polar_count_errors",
+    "polar_mask_from_order", "polar_write_frozen_tab", "polar_write_parameters_h", "polar_parse_parameters_h",
 )
 
 _lib = None
@@ -110,6 +111,10 @@ def lib():
         "polar_csim_frames": [u32, u32, ctypes.c_uint64, sz, ctypes.c_float, i32, i32, i32, p, u32, p, p, p],
         "polar_csim_states": [u32, u32, ctypes.c_uint64, sz, p],
         "polar_count_errors": [p, p, u32, sz, p, p],
+        "polar_mask_from_order": [p, u32, u32, u32, p, u32],
+        "polar_write_frozen_tab": [p, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)],
+        "polar_write_parameters_h": [p, u32, u32, i32, ctypes.c_char_p, sz, ctypes.POINTER(sz)],
+        "polar_parse_parameters_h": [ctypes.c_char_p, p, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -152,6 +157,46 @@ def load_mask_file(path):
     _check("polar_load_mask_file",
            lib().polar_load_mask_file(os.fsencode(path), _np_ptr(buf), cap, ctypes.byref(n)))
     return buf[:n.value].copy()
+
+
+def _text_call(name, *args):
+    n = ctypes.c_size_t(0)
+    _check(name, getattr(lib(), name)(*args, None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value + 1)
+    _check(name, getattr(lib(), name)(*args, buf, n.value + 1, ctypes.byref(n)))
+    return buf.raw[:n.value].decode("ascii")
+
+
+def mask_from_order(order, N, K):
+    """Reliability order (most reliable first) -> information mask of N bits, K info bits.
+    Entries >= N are dropped first (Writer.h:61-93)."""
+    o = np.ascontiguousarray(order, dtype=np.uint32)
+    out = np.zeros(N, dtype=np.uint8)
+    _check("polar_mask_from_order", lib().polar_mask_from_order(_np_ptr(o), o.size, N, K, _np_ptr(out), N))
+    return out
+
+
+def frozen_tab_text(order, N):
+    """FB_N{N}_K{K}.txt text of the order's subset < N (Writer.h:71-79)."""
+    o = np.ascontiguousarray(order, dtype=np.uint32)
+    return _text_call("polar_write_frozen_tab", _np_ptr(o), o.size, N)
+
+
+def parameters_h_text(info_mask, par=16, concat=False):
+    """polar_parameters.h for an information mask, as Frozen_Bit_Generator writes it
+    (Writer.h:110-162); concat = the generator's En flag."""
+    m = np.ascontiguousarray(np.asarray(info_mask) != 0, dtype=np.uint8)
+    return _text_call("polar_write_parameters_h", _np_ptr(m), m.size, par, 1 if concat else 0)
+
+
+def load_parameters_h(path):
+    """polar_parameters.h -> (information mask, PAR)."""
+    cap = 1 << 21
+    buf = np.zeros(cap, dtype=np.uint8)
+    n, par = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    _check("polar_parse_parameters_h", lib().polar_parse_parameters_h(os.fsencode(path), _np_ptr(buf), cap,
+                                                                       ctypes.byref(n), ctypes.byref(par)))
+    return buf[:n.value].copy(), par.value
 
 
 def unpack_bits(words, N):

@@ -10,7 +10,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "lib", "libpolar_sc.so")
 SOURCES = [os.path.join(PKG, "csrc", "polar_sc_kernels.hip"), os.path.join(PKG, "csrc", "polar_sc_host.cpp"),
-           os.path.join(PKG, "csrc", "polar_sc_jit.cpp"), os.path.join(PKG, "csrc", "polar_sc_channel.hip")]
+           os.path.join(PKG, "csrc", "polar_sc_jit.cpp"), os.path.join(PKG, "csrc", "polar_sc_channel.hip"),
+           os.path.join(PKG, "csrc", "polar_sc_tables.cpp")]
 DEVICE_H = os.path.join(PKG, "csrc", "polar_sc_device.h")
 INTERP_H = os.path.join(PKG, "csrc", "polar_sc_interp.h")
 HEADERS = [os.path.join(ROOT, "include", "polar_sc.h"), DEVICE_H, INTERP_H, os.path.join(PKG, "csrc", "polar_sc_plan.hpp")]
