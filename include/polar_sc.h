@@ -32,9 +32,12 @@ extern "C" {
 
 /*
  * Decoder configuration. Mirrors the compile-time switches of the reference's
- * src/module/config.h:2-30 (+ PAR from polar_parameters.h:8). The reference ships ONE
- * configuration and parity is defined for exactly that one; it is the default
- * (polar_sc_default_config). Any other value is rejected with -ENOTSUP in this version.
+ * src/module/config.h:2-30 (+ PAR from polar_parameters.h:8). The default
+ * (polar_sc_default_config) is the configuration the reference ships. Also accepted: the
+ * pruning sweep of script/script_tests.sh:103-122, i.e. pruning_level 0/1/2 with any
+ * combination of elag_r1 / elag_rep / elag_spc / elag_rep2 / elag_spc2 / elag_h0.
+ * elag_rare = 1 (does not compile in the reference, my_module.h:255 vs :1511) and any other
+ * llr_bits / par / sigmag / extended are rejected with -ENOTSUP in this version.
  */
 typedef struct polar_sc_config {
     int32_t llr_bits;       /* LLR_BITS            (config.h:2)      default 6  */
@@ -70,7 +73,8 @@ typedef struct polar_sc_op {
     int32_t n;      /* words (16 LLRs / 16 bits) per operand half */
     int32_t pos;    /* first bit_mem word written (or combined, for H/H0) */
     int32_t upos;   /* first bit_mem word of partial sums for G-type ops, -1 = zero (H0 route) */
-    uint32_t fb;    /* 16-bit frozen pattern of the group, leaf ops only */
+    uint32_t fb;    /* leaf ops only: bits 0..15 frozen pattern of the group, bits 16..18 the
+                       leaf decoder (POLAR_LEAF_*; non-plain only at pruning_level 1) */
     int32_t reserved[2];
 } polar_sc_op;
 
@@ -85,6 +89,15 @@ enum {
     POLAR_OP_H = 8,      /* H_STATE                  (my_module.h:881-998)   */
     POLAR_OP_H0 = 9,     /* H0_STATE                 (my_module.h:1002-1104) */
     POLAR_OP_END = 10    /* END                      (my_module.h:1848-1869) */
+};
+
+/* leaf decoders of R_STATE at PRUNING_LEVEL 1 (my_module.h:566-593) */
+enum {
+    POLAR_LEAF_PLAIN = 0,   /* Spec_Polar_Decoder (library.h:149-172); also R0 / R1 groups   */
+    POLAR_LEAF_REP = 1,     /* Spec_REP_Node (library.h:189-210, functions.h:1167-1176)     */
+    POLAR_LEAF_SPC = 2,     /* Spec_SPC_Node (library.h:235-256, functions.h:2111-2136)     */
+    POLAR_LEAF_REP2 = 3,    /* Spec_REP_REP2_Node, sel 1 (library.h:212-233, functions.h:1353-1420) */
+    POLAR_LEAF_SPC2 = 4     /* Spec_SPC_SPC2_Node, sel 1 (library.h:258-280, functions.h:2786-2811) */
 };
 
 typedef struct polar_sc_plan_stats {

@@ -15,7 +15,7 @@ _LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
 _lib = None
 
 # FSM state indices of orc_decode_fsm's state_counts (polar_oracle.c)
-STATES = ("INIT", "F", "R", "G", "H", "H0", "F_REP", "G_R1", "G_SPC", "END")
+STATES = ("INIT", "F", "R", "G", "H", "H0", "F_REP", "G_R1", "G_SPC", "END", "F_R0")
 
 NODE_R0, NODE_R1, NODE_REP, NODE_SPC, NODE_RN = 0x00, 0x0F, 0x02, 0x04, 0x08
 
@@ -58,6 +58,13 @@ def lib():
         L.orc_decode_fsm.restype = i32
         L.orc_decode_rec.argtypes = [i32, p, p, p, i32]
         L.orc_decode_rec.restype = i32
+        L.orc_decode_fsm_cfg.argtypes = [i32, p, p, p, i32, p, p]
+        L.orc_decode_fsm_cfg.restype = i32
+        L.orc_decode_rec_cfg.argtypes = [i32, p, p, p, i32, p]
+        L.orc_decode_rec_cfg.restype = i32
+        for name in ("orc_leaf_rep16", "orc_leaf_spc16"):
+            getattr(L, name).argtypes = [p, i32]
+            getattr(L, name).restype = u32
         L.orc_encode.argtypes = [i32, p, p, i32]
         L.orc_encode.restype = None
         _lib = L
@@ -68,14 +75,35 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def decode_fsm(mask, llr, return_counts=False):
-    """Literal FSM decode. mask: (N,) 0/1; llr: (B, N) int8. Returns xhat (B, N) uint8."""
+# The reference's pruning sweep (script/script_tests.sh:103-122), in its order:
+# (PRUNING_LEVEL, ELAG_R1, ELAG_REP, ELAG_SPC, ELAG_REP2, ELAG_SPC2, ELAG_H0)
+SWEEP_CONFIGS = (
+    (0, 0, 0, 0, 0, 0, 0), (1, 0, 0, 0, 0, 0, 0), (1, 1, 0, 0, 0, 0, 0), (1, 1, 1, 0, 0, 0, 0),
+    (1, 1, 1, 1, 0, 0, 0), (1, 1, 1, 1, 1, 0, 0), (1, 1, 1, 1, 1, 1, 0), (2, 0, 0, 0, 0, 0, 1),
+    (2, 1, 0, 0, 0, 0, 1), (2, 1, 1, 0, 0, 0, 1), (2, 1, 1, 1, 0, 0, 1),
+)
+DEFAULT_CONFIG = (2, 1, 1, 1, 0, 0, 1)
+
+
+def _cfg(config):
+    if config is None:
+        return None
+    c = np.ascontiguousarray(config, dtype=np.int32)
+    assert c.shape == (7,)
+    return c
+
+
+def decode_fsm(mask, llr, return_counts=False, config=None):
+    """Literal FSM decode. mask: (N,) 0/1; llr: (B, N) int8. Returns xhat (B, N) uint8.
+    config: 7-tuple (see SWEEP_CONFIGS) or None for the shipped config.h."""
     mask = np.ascontiguousarray(mask, dtype=np.uint8)
     llr = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
     B, N = llr.shape
     out = np.zeros((B, N), dtype=np.uint8)
     counts = np.zeros(len(STATES), dtype=np.int64)
-    rc = lib().orc_decode_fsm(N, _ptr(mask), _ptr(llr), _ptr(out), B, _ptr(counts))
+    c = _cfg(config)
+    rc = lib().orc_decode_fsm_cfg(N, _ptr(mask), _ptr(llr), _ptr(out), B, _ptr(counts),
+                                  None if c is None else _ptr(c))
     if rc != 0:
         raise RuntimeError("orc_decode_fsm failed: %d" % rc)
     if return_counts:
@@ -83,16 +111,29 @@ def decode_fsm(mask, llr, return_counts=False):
     return out
 
 
-def decode_rec(mask, llr):
+def decode_rec(mask, llr, config=None):
     """Recursive-restatement decode (same I/O as decode_fsm)."""
     mask = np.ascontiguousarray(mask, dtype=np.uint8)
     llr = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
     B, N = llr.shape
     out = np.zeros((B, N), dtype=np.uint8)
-    rc = lib().orc_decode_rec(N, _ptr(mask), _ptr(llr), _ptr(out), B)
+    c = _cfg(config)
+    rc = lib().orc_decode_rec_cfg(N, _ptr(mask), _ptr(llr), _ptr(out), B, None if c is None else _ptr(c))
     if rc != 0:
         raise RuntimeError("orc_decode_rec failed: %d" % rc)
     return out
+
+
+def leaf_rep16(word, sel=0):
+    """REP_REP2_16_SM on 16 six-bit SM patterns -> 16-bit x."""
+    w = np.ascontiguousarray(word, dtype=np.uint32)
+    return int(lib().orc_leaf_rep16(_ptr(w), sel))
+
+
+def leaf_spc16(word, sel=0):
+    """SPC_SPC2_Node_16 (SM) on 16 six-bit SM patterns -> 16-bit x."""
+    w = np.ascontiguousarray(word, dtype=np.uint32)
+    return int(lib().orc_leaf_spc16(_ptr(w), sel))
 
 
 def encode(u):

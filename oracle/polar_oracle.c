@@ -213,12 +213,13 @@ uint32_t orc_rep_add_tree16(const uint32_t *llr, uint32_t old_sum)
 
 /* Min_Mask_16_SM<5> via Min_Mask_TREE_16<6> (functions.h:3652-3747, 3900-3913).
  * Returns (min << 16) | one-hot mask. */
-static void min_mask_rec(int n, const uint32_t *mag, uint32_t *min_out, uint32_t *mask_out)
+static void min_mask_rec(int n, const uint32_t *mag, uint32_t *min_out, uint32_t *mask_out, int sel)
 {
     if (n == 2) {   /* Min_Mask_2_SM: is_min = mb < ma ; mask = (is_min, ~is_min) */
         uint32_t is_min = (mag[1] < mag[0]) ? 1u : 0u;
         *min_out = is_min ? mag[1] : mag[0];
         *mask_out = (is_min << 1) | (is_min ^ 1u);
+        if (sel) *mask_out = 3u;   /* SPC_SPC2_Min_Mask_2_SM, sel 1: mask2 = 11 (functions.h:2534-2551) */
         return;
     }
     int h = n / 2;
@@ -230,7 +231,7 @@ static void min_mask_rec(int n, const uint32_t *mag, uint32_t *min_out, uint32_t
     }
     uint32_t mask_a = (is_min << h) | ((~is_min) & msk(h));
     uint32_t rmin, imask;
-    min_mask_rec(h, m, &rmin, &imask);
+    min_mask_rec(h, m, &rmin, &imask, sel);
     uint32_t mask_b = (imask << h) | imask;
     *min_out = rmin;
     *mask_out = mask_a & mask_b;
@@ -241,7 +242,7 @@ uint32_t orc_min_mask16(const uint32_t *llr)
     uint32_t mag[16];
     for (int i = 0; i < 16; i++) mag[i] = llr[i] & msk(LLR_BITS - 1);
     uint32_t mn, mask;
-    min_mask_rec(16, mag, &mn, &mask);
+    min_mask_rec(16, mag, &mn, &mask, 0);
     return (mn << 16) | (mask & 0xFFFFu);
 }
 
@@ -255,6 +256,92 @@ int orc_classify_group(uint32_t fb)
     if (fb == 0x8000u) return NODE_REP;            /* last bit 1, others 0 */
     if (fb == 0xFFFEu) return NODE_SPC;            /* first bit 0, others 1 */
     return NODE_RN;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Configurations of the reference's pruning sweep (config.h:16-28,                        */
+/* script/script_tests.sh:103-122) and the PRUNING_LEVEL 1 leaf decoders                  */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { int pr, r1, rep, spc, rep2, spc2, h0; } orc_cfg_t;
+static const orc_cfg_t ORC_DEFAULT_CFG = { 2, 1, 1, 1, 0, 0, 1 };
+
+/* do_prunning classification with the ELAG switches (my_module.h:86-153): R0 > R1 > REP >
+ * SPC > REP2 > SPC2 > RN, nothing but RN at PRUNING_LEVEL 0 */
+static uint32_t classify_cfg(uint32_t fb, const orc_cfg_t *c)
+{
+    fb &= 0xFFFFu;
+    if (c->pr == 0) return NODE_RN;
+    if (fb == 0) return NODE_R0;
+    if (c->r1 && fb == 0xFFFFu) return NODE_R1;
+    if (c->rep && fb == 0x8000u) return NODE_REP;       /* REP_last & ~REP_R0 */
+    if (c->spc && fb == 0xFFFEu) return NODE_SPC;       /* ~SPC_1st & SPC_R1 */
+    if (c->rep2 && fb == 0xC000u) return NODE_REP2;     /* REP_2Last & ~REP_2Last_R0 */
+    if (c->spc2 && fb == 0xFFFCu) return NODE_SPC2;     /* ~SPC_2nd & SPC_2nd_R1 */
+    return NODE_RN;
+}
+
+/* REP_REP2_16_SM<Q> (functions.h:1353-1420); sel = 0 is REP_16_SM (functions.h:996-1060):
+ * exact SM pair sums (j, j+h), a = lower half, down to two values, then REP_REP2_2_SM:
+ * sel 0 -> 16 copies of (|a| < |b| ? sign b : sign a); sel 1 -> (sign b, sign a) repeated,
+ * i.e. even positions take sign a, odd positions sign b. */
+uint32_t orc_leaf_rep16(const uint32_t *llr, int sel)
+{
+    uint32_t v[16];
+    int n = 16, Q = LLR_BITS;
+    for (int i = 0; i < 16; i++) v[i] = llr[i] & msk(Q);
+    while (n > 2) {
+        int h = n / 2;
+        for (int j = 0; j < h; j++) v[j] = orc_full_adder_sm(Q, v[j], v[j + h]);
+        n = h;
+        Q += 1;
+    }
+    uint32_t siga = (v[0] >> (Q - 1)) & 1u, sigb = (v[1] >> (Q - 1)) & 1u;
+    uint32_t is_min = ((v[0] & msk(Q - 1)) < (v[1] & msk(Q - 1))) ? 1u : 0u;
+    uint32_t sig = is_min ? sigb : siga, x = 0;
+    for (int i = 0; i < 16; i++) x |= (sel ? ((i & 1) ? sigb : siga) : sig) << i;
+    return x;
+}
+
+/* SPC_SPC2_Node_16 SM path (functions.h:2786-2811); sel = 0 is SPC_Node_16
+ * (functions.h:2111-2136): x = sign ^ (parity & min_mask). Parity: XOR folds of the sign
+ * halves down to two bits (SPC_SPC2_Parity_*, :2254-2300), then sel 0 -> both = their XOR,
+ * sel 1 -> kept per position class. Min mask: the Min_Mask tournament, last stage
+ * (is_min, ~is_min) or, sel 1, 11. */
+uint32_t orc_leaf_spc16(const uint32_t *llr, int sel)
+{
+    uint32_t sign = 0, mag[16];
+    for (int i = 0; i < 16; i++) {
+        sign |= ((llr[i] >> (LLR_BITS - 1)) & 1u) << i;
+        mag[i] = llr[i] & msk(LLR_BITS - 1);
+    }
+    uint32_t f = sign;
+    for (int n = 16; n > 2; n /= 2) f = (f & msk(n / 2)) ^ ((f >> (n / 2)) & msk(n / 2));
+    uint32_t p2 = sel ? (f & 3u) : (((f ^ (f >> 1)) & 1u) * 3u);
+    uint32_t parity = 0;
+    for (int i = 0; i < 16; i++) parity |= ((p2 >> (i & 1)) & 1u) << i;
+    uint32_t mn, mask;
+    min_mask_rec(16, mag, &mn, &mask, sel);
+    return (sign ^ (parity & mask)) & 0xFFFFu;
+}
+
+/* R_STATE decoder of a group (my_module.h:566-596): the plain leaf, or at PRUNING_LEVEL 1
+ * the node decoder of the group's class (type = Node[3:1], sel = Node[0]) */
+static uint32_t leaf_cfg(const uint32_t *llr, uint32_t fb, uint32_t node, const orc_cfg_t *c)
+{
+    if (c->pr == 1) {
+        uint32_t type = (node >> 1) & 7u, sel = node & 1u;
+        switch (type) {
+        case 0x0: return 0;                                        /* Spec_Node_R0 */
+        case 0x7: if (c->r1) { uint32_t x = 0;                      /* Spec_Node_R1: VECTOR_SIGN */
+                      for (int i = 0; i < 16; i++) x |= ((llr[i] >> (LLR_BITS - 1)) & 1u) << i;
+                      return x; }
+                  break;
+        case 0x1: if (c->rep) return orc_leaf_rep16(llr, c->rep2 ? (int)sel : 0); break;
+        case 0x2: if (c->spc) return orc_leaf_spc16(llr, c->spc2 ? (int)sel : 0); break;
+        default: break;
+        }
+    }
+    return orc_leaf16(llr, fb);
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -272,7 +359,7 @@ static uint32_t stk_read(const stk_t *s, int adr) { return s->e[adr - 1]; }
 /* ------------------------------------------------------------------------------------ */
 typedef uint32_t word_t[PAR];   /* one TYPE_LLRS: 16 six-bit SM patterns */
 
-enum { ST_INIT, ST_F, ST_R, ST_G, ST_H, ST_H0, ST_F_REP, ST_G_R1, ST_G_SPC, ST_END, ST_COUNT };
+enum { ST_INIT, ST_F, ST_R, ST_G, ST_H, ST_H0, ST_F_REP, ST_G_R1, ST_G_SPC, ST_END, ST_F_R0, ST_COUNT };
 
 typedef struct {
     int N, NDIV, DEPTH_DIV;
@@ -283,6 +370,7 @@ typedef struct {
     uint8_t *node_type;
     stk_t nts;                      /* Node_type_stack: 8-bit entries, never reset by INIT */
     long state_count[ST_COUNT];
+    orc_cfg_t cfg;                  /* config.h switches (#if branches taken at run time) */
 } fsm_t;
 
 static int ilog2(int v) { int l = 0; while ((1 << l) < v) l++; return l; }
@@ -294,7 +382,7 @@ static void fsm_prune(fsm_t *m, const uint8_t *mask)
         uint32_t tab = 0;
         for (int k = 0; k < PAR; k++) tab |= (uint32_t)(mask[i * PAR + k] & 1u) << k;
         m->bit_frozen[i] = (uint16_t)tab;
-        m->node_type[i] = (uint8_t)orc_classify_group(tab);
+        m->node_type[i] = (uint8_t)classify_cfg(tab, &m->cfg);
     }
 }
 
@@ -322,6 +410,16 @@ static void word_G(word_t r, const word_t a, const word_t b, uint32_t sa)
 { for (int l = 0; l < PAR; l++) r[l] = orc_G_sm(LLR_BITS, a[l], b[l], (sa >> l) & 1u); }
 static uint32_t word_sign(const word_t a)
 { uint32_t s = 0; for (int l = 0; l < PAR; l++) s |= ((a[l] >> (LLR_BITS - 1)) & 1u) << l; return s; }
+
+/* the G-type state chosen from the right child's class (my_module.h:495-502, 623-652,
+ * 965-993, 1165-1190, 1360-1388): pruned G only at PRUNING_LEVEL 2 with the switch on */
+static int g_next(const fsm_t *m, uint32_t rn)
+{
+    if (m->cfg.pr != 2) return ST_G;
+    if (rn == NODE_R1 && m->cfg.r1) return ST_G_R1;
+    if (rn == NODE_SPC && m->cfg.spc) return ST_G_SPC;
+    return ST_G;
+}
 
 #define CNT(x) ((x) & m->cmask)
 #define CHK(i) do { if ((uint32_t)(i) >= (uint32_t)m->NDIV) return -100; } while (0)
@@ -403,8 +501,9 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             else     stk_write(&m->nts, (left_Node << 4) | right_Node);
 
             if (N_REG > 1) {
-                switch (left_Node) {
-                case NODE_R0: {                                     /* H0 route :481-507 */
+                if (m->cfg.pr != 2) {                               /* :529-531, 866-868 */
+                    next = ST_F;
+                } else if (left_Node == NODE_R0 && m->cfg.h0) {     /* H0 route :481-507 */
                     N_REG = CNT(N_REG >> 1);
                     stk_push(&stack, 0);
                     stk_push(&m->nts, 0x00);
@@ -413,13 +512,13 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
                     uint32_t rn = stk_read(&m->nts, 2) & 0xFu;
                     ps_adr = CNT(adr_s - N_REG);
                     G_stack_value = 2;
-                    if (rn == NODE_R1) next = ST_G_R1;
-                    else if (rn == NODE_SPC) next = ST_G_SPC;
-                    else next = ST_G;
-                    break;
-                }
-                case NODE_REP: next = ST_F_REP; break;
-                default: next = ST_F; break;
+                    next = g_next(m, rn);
+                } else if (left_Node == NODE_R0) {                  /* ELAG_H0 = 0: :508-511 */
+                    next = ST_F_R0;
+                } else if (left_Node == NODE_REP && m->cfg.rep) {
+                    next = ST_F_REP;
+                } else {
+                    next = ST_F;
                 }
             } else {
                 adr_a = CNT(adr_a - 1); adr_b = CNT(adr_b - 1);
@@ -431,8 +530,9 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
         case ST_R: {                                                /* :544-665 */
             CHK(ptr_FB);
             uint32_t is_frozen = m->bit_frozen[ptr_FB];
+            uint32_t node = m->node_type[ptr_FB];
             ptr_FB = CNT(ptr_FB + 1);
-            uint32_t ps = orc_leaf16(reg_result, is_frozen);
+            uint32_t ps = leaf_cfg(reg_result, is_frozen, node, &m->cfg);
             CHK(adr_s);
             m->bit_mem_1[adr_s] = (uint16_t)ps; m->bit_mem_2[adr_s] = (uint16_t)ps;
             adr_s = CNT(adr_s + 1);
@@ -441,13 +541,13 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             if (R_state_condition) {
                 ps_adr = CNT(adr_s - N_REG);
                 G_stack_value = 1;
-                if (rn == NODE_R1) next = ST_G_R1;
-                else if (rn == NODE_SPC) next = ST_G_SPC;
-                else next = ST_G;
+                next = g_next(m, rn);
             } else {
                 ps_adr_a = CNT(adr_s - (N_REG << 1));
                 ps_adr_b = CNT(adr_s - N_REG);
-                next = (condition == 1) ? ST_H : ST_H0;
+                if (condition == 1) next = ST_H;
+                else if (m->cfg.pr == 2 && m->cfg.h0) next = ST_H0;
+                else return -103;   /* next_state left unchanged: never reached (stack top is 1) */
             }
             break;
         }
@@ -472,7 +572,7 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             if (condition == 1) {
                 ps_adr_a = CNT(adr_s - (N_REG << 1)); ps_adr_b = CNT(adr_s - N_REG);
                 next = ST_H;
-            } else if (condition == 2) {
+            } else if (condition == 2 && m->cfg.pr == 2 && m->cfg.h0) {
                 ps_adr_a = CNT(adr_s - (N_REG << 1)); ps_adr_b = CNT(adr_s - N_REG);
                 next = ST_H0;
             } else if (ptr_FB == (uint32_t)NDIV) {
@@ -480,9 +580,7 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             } else {
                 ps_adr = CNT(adr_s - N_REG);
                 G_stack_value = 1;
-                if (rn == NODE_R1) next = ST_G_R1;
-                else if (rn == NODE_SPC) next = ST_G_SPC;
-                else next = ST_G;
+                next = g_next(m, rn);
             }
             break;
         }
@@ -513,9 +611,25 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             uint32_t rn = stk_read(&m->nts, 2) & 0xFu;
             ps_adr = CNT(adr_s - N_REG);
             G_stack_value = 1;
-            if (rn == NODE_R1) next = ST_G_R1;
-            else if (rn == NODE_SPC) next = ST_G_SPC;
-            else next = ST_G;
+            next = g_next(m, rn);
+            break;
+        }
+        case ST_F_R0: {                                             /* :1111-1200 (ELAG_H0 = 0) */
+            NB_ITER = CNT(N_REG >> 1);
+            N_REG = CNT(N_REG >> 1);
+            stk_push(&stack, 0);
+            stk_push(&m->nts, 0x00);
+            for (uint32_t i = 0; i < NB_ITER; i++) {
+                CHK(adr_s);
+                m->bit_mem_1[adr_s] = 0; m->bit_mem_2[adr_s] = 0;
+                adr_a = CNT(adr_a + 1); adr_b = CNT(adr_b + 1); adr_s = CNT(adr_s + 1);
+            }
+            ptr_FB = CNT(ptr_FB + NB_ITER);
+            adr_a = CNT(adr_a - NB_ITER); adr_b = CNT(adr_b - NB_ITER);
+            uint32_t rn = stk_read(&m->nts, 2) & 0xFu;
+            ps_adr = CNT(adr_s - N_REG);
+            G_stack_value = 1;
+            next = g_next(m, rn);
             break;
         }
         case ST_G_R1:                                               /* :1571-1642 */
@@ -554,7 +668,9 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             adr_a = CNT(adr_a - NB_ITER); adr_b = CNT(adr_b - NB_ITER);
             ps_adr_a = CNT(adr_s - (N_REG << 1)); ps_adr_b = CNT(adr_s - N_REG);
             uint32_t condition = stk_read(&stack, 1);
-            next = (condition == 1) ? ST_H : ST_H0;
+            if (condition == 1) next = ST_H;
+            else if (m->cfg.h0) next = ST_H0;                       /* :1634-1639 */
+            else return -103;
             break;
         }
         case ST_END: {                                              /* :1848-1869 */
@@ -580,12 +696,32 @@ static void wrap_in(const int8_t *llr, int N, word_t *w)
  * llr: nframes*N int8 (2's complement, low 6 bits used as sc_bigint<6>).
  * xhat: nframes*N bytes 0/1 (wrapper_out order). Returns 0 or a negative error.
  * state_counts (optional, ST_COUNT longs): per-state visit counts over all frames. */
+static int cfg_from(const int32_t *c7, orc_cfg_t *c)
+{
+    *c = ORC_DEFAULT_CFG;
+    if (!c7) return 0;
+    c->pr = c7[0]; c->r1 = c7[1]; c->rep = c7[2]; c->spc = c7[3]; c->rep2 = c7[4]; c->spc2 = c7[5]; c->h0 = c7[6];
+    return (c->pr < 0 || c->pr > 2) ? -22 : 0;
+}
+
+int orc_decode_fsm_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
+                       long *state_counts, const int32_t *cfg7);
+
 int orc_decode_fsm(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
                    long *state_counts)
+{
+    return orc_decode_fsm_cfg(N, mask, llr, xhat, nframes, state_counts, NULL);
+}
+
+/* cfg7 = {PRUNING_LEVEL, ELAG_R1, ELAG_REP, ELAG_SPC, ELAG_REP2, ELAG_SPC2, ELAG_H0}, NULL =
+ * the shipped config.h */
+int orc_decode_fsm_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
+                       long *state_counts, const int32_t *cfg7)
 {
     if (N < 32 || (N & (N - 1)) != 0) return -22;
     fsm_t m;
     memset(&m, 0, sizeof m);
+    if (cfg_from(cfg7, &m.cfg)) return -22;
     m.N = N; m.NDIV = N / PAR;
     m.DEPTH_DIV = ilog2(m.NDIV) + 1;           /* Writer.h:121: log2(N/PAR) + 1 */
     m.cmask = msk(ilog2(N) + 1);               /* COUNTER = sc_uint<_DEPTH>, _DEPTH = log2N+1 */
@@ -623,6 +759,7 @@ typedef struct {
     const uint16_t *fb;     /* per group */
     const uint8_t *type;    /* per group */
     uint16_t *x;            /* per group, encoded bits */
+    orc_cfg_t cfg;
 } rec_t;
 
 static uint32_t node_type(const rec_t *r, int g0, int cnt)
@@ -645,10 +782,16 @@ static uint32_t node_type(const rec_t *r, int g0, int cnt)
 /* decode node covering groups [g0, g0+cnt) with LLR words lam[0..cnt) (6-bit SM) */
 static void rec_node(rec_t *r, int g0, int cnt, const word_t *lam, int is_root)
 {
-    if (cnt == 1) { r->x[g0] = (uint16_t)orc_leaf16(lam[0], r->fb[g0]); return; }
+    if (cnt == 1) { r->x[g0] = (uint16_t)leaf_cfg(lam[0], r->fb[g0], r->type[g0], &r->cfg); return; }
     int h = cnt / 2;
-    uint32_t tl = is_root ? NODE_RN : node_type(r, g0, h);
-    uint32_t tr = is_root ? NODE_RN : node_type(r, g0 + h, h);
+    /* node pruning at PRUNING_LEVEL 2 only, each kind behind its switch; REP2 / SPC2
+     * classes are never pruned above the leaves (node_type returns RN for them) */
+    const int prune = r->cfg.pr == 2;
+    uint32_t tl = (is_root || !prune) ? NODE_RN : node_type(r, g0, h);
+    uint32_t tr = (is_root || !prune) ? NODE_RN : node_type(r, g0 + h, h);
+    if (tl == NODE_REP && !r->cfg.rep) tl = NODE_RN;
+    if (tr == NODE_R1 && !r->cfg.r1) tr = NODE_RN;
+    if (tr == NODE_SPC && !r->cfg.spc) tr = NODE_RN;
     word_t *child = (word_t *)malloc((size_t)h * sizeof(word_t));
     int left_zero = 0;
     if (tl == NODE_R0) {
@@ -691,9 +834,20 @@ static void rec_node(rec_t *r, int g0, int cnt, const word_t *lam, int is_root)
     free(child);
 }
 
+int orc_decode_rec_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
+                       const int32_t *cfg7);
+
 int orc_decode_rec(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes)
 {
+    return orc_decode_rec_cfg(N, mask, llr, xhat, nframes, NULL);
+}
+
+int orc_decode_rec_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
+                       const int32_t *cfg7)
+{
     if (N < 32 || (N & (N - 1)) != 0) return -22;
+    orc_cfg_t cfg;
+    if (cfg_from(cfg7, &cfg)) return -22;
     int G = N / PAR;
     uint16_t *fb = (uint16_t *)calloc((size_t)G, 2);
     uint8_t *type = (uint8_t *)calloc((size_t)G, 1);
@@ -703,9 +857,9 @@ int orc_decode_rec(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat,
     for (int g = 0; g < G; g++) {
         uint32_t t = 0;
         for (int k = 0; k < PAR; k++) t |= (uint32_t)(mask[g * PAR + k] & 1u) << k;
-        fb[g] = (uint16_t)t; type[g] = (uint8_t)orc_classify_group(t);
+        fb[g] = (uint16_t)t; type[g] = (uint8_t)classify_cfg(t, &cfg);
     }
-    rec_t r = { G, fb, type, x };
+    rec_t r = { G, fb, type, x, cfg };
     for (int f = 0; f < nframes; f++) {
         wrap_in(llr + (size_t)f * N, N, in);
         rec_node(&r, 0, G, in, 1);

@@ -243,6 +243,59 @@ __device__ __forceinline__ u32 row_transpose16(u32 v, const Lanes &ln)
 }
 
 // ---------------------------------------------------------------------------------------
+// PRUNING_LEVEL 1 leaf decoders (R_STATE, my_module.h:566-593). SM16 word in, sign-position
+// flags per lane out (like leaf16).
+// ---------------------------------------------------------------------------------------
+// Spec_REP_Node -> REP_16_SM (functions.h:1049-1060, 996-1016): exact SM pair sums at
+// distance 8, 4, 2, then the sign rule of REP_2_SM (|a| < |b| ? sign b : sign a) -- the sign
+// of the full pair-tree total; x = 16 copies.
+__device__ __forceinline__ u32 leaf_rep(u32 L, const Lanes &ln) { return row_add_tree(L, ln) & SGN; }
+
+// Spec_REP_REP2_Node with sel = 1 -> REP_REP2_16_SM (functions.h:1353-1420): the same folds
+// at distance 8, 4, 2 leave the exact totals of the even and the odd positions; x[i] = the
+// SM sign of its class total (res2 = (sigb, siga), repeated).
+__device__ __forceinline__ u32 leaf_rep2(u32 v, const Lanes &ln)
+{
+    u32 p;
+    p = xorlane<8>(v); v = G_sm<0>(bsel(ln.a8, v, p), bsel(ln.a8, p, v), 0u);
+    p = xorlane<4>(v); v = G_sm<0>(bsel(ln.a4, v, p), bsel(ln.a4, p, v), 0u);
+    p = xorlane<2>(v); v = G_sm<0>(bsel(ln.a2, v, p), bsel(ln.a2, p, v), 0u);
+    return v & SGN;
+}
+
+// Spec_SPC_Node -> SPC_Node_16 (functions.h:2111-2136; SPC_Parity_16 :1633-1644,
+// SPC_Min_Mask_16_SM :1919-1937): h = signs; flip h at the minimum |lambda| (tournament at
+// distance 8, 4, 2, 1, the upper lane winning only when strictly smaller: ties -> smallest
+// bitrev4(position)) when the parity of h is odd. SPC2 (SPC_SPC2_Node_16 with sel = 1,
+// :2786-2811, :2254-2300, :2534-2580): parity and minimum per class of even / odd positions
+// (folds at distance 8, 4, 2 only), both class minima may flip.
+template <bool SPC2>
+__device__ __forceinline__ u32 leaf_spc(u32 L, const Lanes &ln)
+{
+    const u32 h = L & SGN;
+    u32 par = h;
+    par ^= xorlane<8>(par);
+    par ^= xorlane<4>(par);
+    par ^= xorlane<2>(par);
+    if constexpr (!SPC2) par ^= xorlane<1>(par);
+    u32 klo = ((L & 0x7FFFu) << 4) | ln.br, khi = (((L >> 16) & 0x7FFFu) << 4) | ln.br;
+    const u32 mlo0 = klo, mhi0 = khi;
+    klo = __builtin_elementwise_min(klo, xorlane<8>(klo));
+    khi = __builtin_elementwise_min(khi, xorlane<8>(khi));
+    klo = __builtin_elementwise_min(klo, xorlane<4>(klo));
+    khi = __builtin_elementwise_min(khi, xorlane<4>(khi));
+    klo = __builtin_elementwise_min(klo, xorlane<2>(klo));
+    khi = __builtin_elementwise_min(khi, xorlane<2>(khi));
+    if constexpr (!SPC2) {
+        klo = __builtin_elementwise_min(klo, xorlane<1>(klo));
+        khi = __builtin_elementwise_min(khi, xorlane<1>(khi));
+    }
+    const u32 flo = (klo == mlo0) ? (par & 0x8000u) : 0u;
+    const u32 fhi = (khi == mhi0) ? (par & 0x80000000u) : 0u;
+    return h ^ flo ^ fhi;
+}
+
+// ---------------------------------------------------------------------------------------
 // Channel LLR -> SM16: wrapper_in + Adapt_format/qconv_format (wrapper_in.h:34,
 // library.h:18-28, scalar.h:229-239). The LLR is the low 6 bits (sc_bigint<6>); -32 -> +0.
 // ---------------------------------------------------------------------------------------

@@ -40,14 +40,37 @@ constexpr int LDS_LOW_SLOTS = 128;                  // HBM mode: nodes <= 128 wo
 
 namespace {
 
-// do_prunning (my_module.h:75-155): group class, priority R0 > R1 > REP > SPC > RN
-uint32_t classify_group(uint32_t fb)
+// do_prunning (my_module.h:75-155): group class, priority R0 > R1 > REP > SPC > REP2 > SPC2
+// > RN, each recognised only when PRUNING_LEVEL > 0 and its ELAG_* switch is on
+// (my_module.h:129-153). REP2 = only the last two bits information, SPC2 = only the first
+// two frozen (my_module.h:108-125).
+constexpr uint32_t NODE_REP2 = 0x03, NODE_SPC2 = 0x05;
+uint32_t classify_group(uint32_t fb, const polar_sc_config &c)
 {
+    if (c.pruning_level == 0) return NODE_RN;
     if (fb == 0u) return NODE_R0;
-    if (fb == 0xFFFFu) return NODE_R1;
-    if (fb == 0x8000u) return NODE_REP;
-    if (fb == 0xFFFEu) return NODE_SPC;
+    if (c.elag_r1 && fb == 0xFFFFu) return NODE_R1;
+    if (c.elag_rep && fb == 0x8000u) return NODE_REP;
+    if (c.elag_spc && fb == 0xFFFEu) return NODE_SPC;
+    if (c.elag_rep2 && fb == 0xC000u) return NODE_REP2;
+    if (c.elag_spc2 && fb == 0xFFFCu) return NODE_SPC2;
     return NODE_RN;
+}
+
+// PRUNING_LEVEL 1 leaf decoders selected in R_STATE by the group's class
+// (my_module.h:566-593; library.h:175-280): REP / SPC, or with ELAG_REP2 / ELAG_SPC2 the
+// REP_REP2 / SPC_SPC2 decoders (sel = class bit 0). R0 and R1 groups give the plain leaf's
+// result (all zero / the hard decisions), so they keep the plain leaf.
+uint32_t leaf_kind(const polar_sc_plan &p, uint32_t g)
+{
+    if (p.cfg.pruning_level != 1) return POLAR_LEAF_PLAIN;
+    switch (p.type[g]) {
+    case NODE_REP: return POLAR_LEAF_REP;
+    case NODE_SPC: return POLAR_LEAF_SPC;
+    case NODE_REP2: return p.cfg.elag_rep ? POLAR_LEAF_REP2 : POLAR_LEAF_PLAIN;
+    case NODE_SPC2: return p.cfg.elag_spc ? POLAR_LEAF_SPC2 : POLAR_LEAF_PLAIN;
+    default: return POLAR_LEAF_PLAIN;
+    }
 }
 
 // Node class of a multi-group node as aggregated in the F/G loops
@@ -167,15 +190,18 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
         return;
     }
     const uint32_t h = cnt / 2;
-    const uint32_t tl = is_root ? NODE_RN : node_class(p, g0, h);
-    const uint32_t tr = is_root ? NODE_RN : node_class(p, g0 + h, h);
+    // node pruning only at PRUNING_LEVEL 2 (my_module.h:478-531, 623-652, 815-868, 965-993);
+    // REP2 / SPC2 classes fall through to the plain F / G transitions there
+    const bool prune = p.cfg.pruning_level == 2;
+    const uint32_t tl = (is_root || !prune) ? NODE_RN : node_class(p, g0, h);
+    const uint32_t tr = (is_root || !prune) ? NODE_RN : node_class(p, g0 + h, h);
     bool left_zero = false;
     if (tl == NODE_R0) {
         left_zero = true;
     } else if (tl == NODE_REP) {
         emit(out, POLAR_OP_REP, level, (int)h, (int)g0, -1, 0);
     } else if (h == 1) {
-        emit(out, POLAR_OP_FLEAF, level, 1, (int)g0, -1, p.fb[g0]);
+        emit(out, POLAR_OP_FLEAF, level, 1, (int)g0, -1, p.fb[g0] | leaf_kind(p, g0) << 16);
     } else {
         emit(out, POLAR_OP_F, level, (int)h, (int)g0, -1, 0);
         compile_node(p, out, level + 1, g0, h, false, sc);
@@ -186,7 +212,7 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
     } else if (tr == NODE_SPC) {
         emit(out, POLAR_OP_SPC, level, (int)h, (int)(g0 + h), upos, 0);
     } else if (h == 1) {
-        emit(out, POLAR_OP_GLEAF, level, 1, (int)(g0 + h), upos, p.fb[g0 + h]);
+        emit(out, POLAR_OP_GLEAF, level, 1, (int)(g0 + h), upos, p.fb[g0 + h] | leaf_kind(p, g0 + h) << 16);
     } else {
         emit(out, POLAR_OP_G, level, (int)h, (int)(g0 + h), upos, 0);
         compile_node(p, out, level + 1, g0 + h, h, false, sc);
@@ -194,16 +220,18 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
     emit(out, left_zero ? POLAR_OP_H0 : POLAR_OP_H, level, (int)h, (int)g0, -1, 0);
 }
 
+// The reference's swept configurations (script/script_tests.sh:103-122) at its shipped
+// arithmetic: PRUNING_LEVEL 0/1/2 with any ELAG_R1/REP/SPC/REP2/SPC2/H0 switches.
+// ELAG_RARE = 1 does not compile in the reference (my_module.h:255 vs :1511); LLR_BITS,
+// PAR, CA2 and EXTENDED = 0 change the arithmetic and are not built yet.
 bool config_supported(const polar_sc_config &c)
 {
     polar_sc_config d;
     polar_sc_default_config(&d);
-    return c.llr_bits == d.llr_bits && c.par == d.par && c.sigmag == d.sigmag &&
-           c.extended == d.extended && c.pruning_level == d.pruning_level &&
-           c.elag_r1 == d.elag_r1 && c.elag_rep == d.elag_rep && c.elag_spc == d.elag_spc &&
-           c.elag_rep2 == d.elag_rep2 && c.elag_spc2 == d.elag_spc2 &&
-           c.elag_rare == d.elag_rare && c.elag_h0 == d.elag_h0 &&
-           (c.strict_llr == 0 || c.strict_llr == 1);
+    auto sw = [](int32_t v) { return v == 0 || v == 1; };
+    return c.llr_bits == d.llr_bits && c.par == d.par && c.sigmag == d.sigmag && c.extended == d.extended &&
+           c.pruning_level >= 0 && c.pruning_level <= 2 && sw(c.elag_r1) && sw(c.elag_rep) && sw(c.elag_spc) &&
+           sw(c.elag_rep2) && sw(c.elag_spc2) && c.elag_rare == 0 && sw(c.elag_h0) && sw(c.strict_llr);
 }
 
 int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
@@ -364,13 +392,13 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         uint32_t t = 0;
         for (uint32_t k = 0; k < POLAR_SC_PAR; k++) t |= (uint32_t)p->mask[g * 16 + k] << k;
         p->fb[g] = (uint16_t)t;
-        p->type[g] = (uint8_t)classify_group(t);
+        p->type[g] = (uint8_t)classify_group(t, c);
         switch (p->type[g]) {
         case NODE_R0: s.n_r0++; break;
         case NODE_R1: s.n_r1++; break;
         case NODE_REP: s.n_rep++; break;
         case NODE_SPC: s.n_spc++; break;
-        default: s.n_rn++; break;
+        default: s.n_rn++; break;   // RN, REP2, SPC2
         }
     }
     compile_node(*p, p->ops, 0, 0, p->G, true, nullptr);
@@ -404,14 +432,18 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     // selects the plain schedule interpreter for every N.
     const char *jit_env = std::getenv("POLAR_SC_JIT");
     const bool jit_on = !(jit_env && jit_env[0] == '0');
-    p->jit = (polar_host::jit_supported(N) && jit_on) ? 1 : 0;
+    // PRUNING_LEVEL 1 leaf decoders other than the plain leaf run on the interpreter only
+    bool kinds = false;
+    for (const polar_sc_op &o : p->ops)
+        if ((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && (o.fb >> 16)) kinds = true;
+    p->jit = (polar_host::jit_supported(N) && jit_on && !kinds) ? 1 : 0;
     int sub_words = 64;
     if (const char *e = std::getenv("POLAR_SC_SUB_WORDS")) {
         if (*e) sub_words = std::atoi(e);
     }
     const bool sub_ok = sub_words >= 2 && sub_words <= 64 && (sub_words & (sub_words - 1)) == 0;
     std::vector<polar_sc_op> dev_sched;
-    if (!p->jit && jit_on && sub_ok && (uint32_t)sub_words < p->G) {
+    if (!p->jit && jit_on && !kinds && sub_ok && (uint32_t)sub_words < p->G) {
         SubCtx sc;
         sc.words = (uint32_t)sub_words;
         compile_node(*p, dev_sched, 0, 0, p->G, true, &sc);

@@ -233,7 +233,15 @@ __device__ __forceinline__ void op_leaf(const C &c, int k, int pos, int upos, ui
     } else {
         L = F_sm(a, b);
     }
-    uint32_t x = leaf16(L, fb, c.ln);
+    // fb bits 16..18: PRUNING_LEVEL 1 leaf decoder (POLAR_LEAF_*, include/polar_sc.h)
+    uint32_t x;
+    switch (fb >> 16) {
+    case 1: x = leaf_rep(L, c.ln); break;
+    case 2: x = leaf_spc<false>(L, c.ln); break;
+    case 3: x = leaf_rep2(L, c.ln); break;
+    case 4: x = leaf_spc<true>(L, c.ln); break;
+    default: x = leaf16(L, fb & 0xFFFFu, c.ln); break;
+    }
     int b4 = pos & 15;
     uint32_t m = 0x10001u << b4;
     uint32_t d = c.bld(pos >> 4);

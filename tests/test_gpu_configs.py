@@ -1,0 +1,56 @@
+"""GPU parity over the reference's pruning sweep (script/script_tests.sh:103-122): every
+config decodes on the device bit-exact with the config-aware literal FSM oracle. Configs
+without PRUNING_LEVEL 1 leaf decoders run on the per-mask / hybrid kernels like the default;
+PRUNING_LEVEL 1 plans with REP / SPC / REP2 / SPC2 leaves run on the schedule interpreter."""
+import numpy as np
+import pytest
+
+import util
+from test_gpu_parity import _assert_same
+
+pytestmark = pytest.mark.gpu
+
+EXTRA = ((2, 1, 1, 1, 0, 0, 0), (2, 1, 1, 1, 1, 1, 1))
+
+
+def _cfg(pkg, c7):
+    c = pkg.default_config()
+    (c.pruning_level, c.elag_r1, c.elag_rep, c.elag_spc, c.elag_rep2, c.elag_spc2, c.elag_h0) = c7
+    return c
+
+
+def _special_mask(rng, N):
+    pats = [0, 0xFFFF, 0x8000, 0xFFFE, 0xC000, 0xFFFC]
+    mask = (rng.random(N) < 0.5).astype(np.uint8)
+    for g in range(N // 16):
+        if rng.random() < 0.6:
+            p = int(rng.choice(pats))
+            mask[16 * g:16 * g + 16] = [(p >> k) & 1 for k in range(16)]
+    return mask
+
+
+def _run(pkg, torch, mask, llr, c7):
+    dec = pkg.Decoder(mask, config=_cfg(pkg, c7))
+    out = dec.decode(torch.from_numpy(np.ascontiguousarray(llr)).cuda())
+    torch.cuda.synchronize()
+    return pkg.unpack_bits(out.cpu().numpy(), mask.size), dec.stats["kernel"]
+
+
+@pytest.mark.parametrize("name", ["FB_N128_K64", "FB_N1024_K512", "frozen_n_2048_k_1024", "frozen_n_8192_k_4096"])
+def test_sweep_configs_awgn(pkg, cuda, oracle_mod, name):
+    mask = util.mask(name)
+    batch = 41 if mask.size <= 1024 else 11
+    llr, _ = util.synth_frames(mask, batch, ebn0_db=1.0, seed=99)
+    for c7 in oracle_mod.SWEEP_CONFIGS + EXTRA:
+        got, kernel = _run(pkg, cuda, mask, llr, c7)
+        _assert_same(got, oracle_mod.decode_fsm(mask, llr, config=c7), "%s %s kernel %d" % (name, c7, kernel))
+
+
+def test_sweep_configs_planted_groups(pkg, cuda, oracle_mod):
+    rng = np.random.default_rng(8)
+    for N in (32, 256, 1024, 4096):
+        mask = _special_mask(rng, N)
+        llr = rng.integers(-32, 32, size=(19, N)).astype(np.int8)
+        for c7 in oracle_mod.SWEEP_CONFIGS + EXTRA:
+            got, kernel = _run(pkg, cuda, mask, llr, c7)
+            _assert_same(got, oracle_mod.decode_fsm(mask, llr, config=c7), "N=%d %s kernel %d" % (N, c7, kernel))

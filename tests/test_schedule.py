@@ -73,3 +73,89 @@ def test_schedule_shapes(pkg):
             assert o["pos"] % (2 * o["n"]) == 0
         if o["op"] in ("G", "GLEAF", "R1", "SPC") and o["upos"] >= 0:
             assert o["pos"] - o["upos"] == o["n"]
+
+
+# ---- the reference's pruning sweep (script/script_tests.sh:103-122) -------------------------
+def _config(pkg, c7):
+    c = pkg.default_config()
+    (c.pruning_level, c.elag_r1, c.elag_rep, c.elag_spc, c.elag_rep2, c.elag_spc2, c.elag_h0) = c7
+    return c
+
+
+def _special_mask(rng, N):
+    """random mask with planted R0 / R1 / REP / SPC / REP2 / SPC2 groups"""
+    pats = [0, 0xFFFF, 0x8000, 0xFFFE, 0xC000, 0xFFFC]
+    mask = (rng.random(N) < rng.choice([0.2, 0.5, 0.8])).astype(np.uint8)
+    for g in range(N // 16):
+        if rng.random() < 0.6:
+            p = int(rng.choice(pats))
+            mask[16 * g:16 * g + 16] = [(p >> k) & 1 for k in range(16)]
+    return mask
+
+
+SWEEP_EXTRA = ((2, 1, 1, 1, 0, 0, 0), (2, 1, 1, 1, 1, 1, 1), (1, 0, 1, 0, 1, 0, 0), (1, 0, 0, 1, 0, 1, 0))
+
+
+def test_sweep_configs_fsm_equals_recursive(oracle_mod):
+    rng = np.random.default_rng(5)
+    for trial in range(40):
+        N = int(2 ** rng.integers(5, 12))
+        mask = _special_mask(rng, N)
+        llr = rng.integers(-32, 32, size=(6, N)).astype(np.int8)
+        for c7 in oracle_mod.SWEEP_CONFIGS + SWEEP_EXTRA:
+            np.testing.assert_array_equal(oracle_mod.decode_fsm(mask, llr, config=c7),
+                                          oracle_mod.decode_rec(mask, llr, config=c7), err_msg=str((trial, c7)))
+
+
+def test_sweep_configs_schedule_equals_fsm(pkg, oracle_mod):
+    rng = np.random.default_rng(6)
+    for trial in range(24):
+        N = int(2 ** rng.integers(5, 12))
+        mask = _special_mask(rng, N)
+        llr = rng.integers(-32, 32, size=(4, N)).astype(np.int8)
+        for c7 in oracle_mod.SWEEP_CONFIGS + SWEEP_EXTRA:
+            dec = pkg.Decoder(mask, config=_config(pkg, c7))
+            np.testing.assert_array_equal(util.run_schedule(dec.schedule(), N, llr),
+                                          oracle_mod.decode_fsm(mask, llr, config=c7), err_msg=str((trial, c7)))
+
+
+@pytest.mark.parametrize("c7", [(0, 0, 0, 0, 0, 0, 0), (1, 1, 1, 1, 1, 1, 0), (2, 1, 0, 0, 0, 0, 1),
+                                (2, 1, 1, 1, 0, 0, 0)])
+def test_sweep_op_census_matches_fsm_states(pkg, oracle_mod, c7):
+    mask = util.mask("frozen_n_2048_k_1024")
+    dec = pkg.Decoder(mask, config=_config(pkg, c7))
+    oc = dec.stats["op_count"]
+    _, st = oracle_mod.decode_fsm(mask, np.zeros((1, mask.size), np.int8), return_counts=True, config=c7)
+    assert oc.get("FLEAF", 0) + oc.get("GLEAF", 0) == st["R"]
+    assert oc.get("REP", 0) == st["F_REP"] and oc.get("R1", 0) == st["G_R1"] and oc.get("SPC", 0) == st["G_SPC"]
+    assert oc.get("G", 0) + oc.get("GLEAF", 0) == st["G"]
+    if c7[0] == 2 and not c7[6]:
+        # ELAG_H0 = 0: F_R0 states instead of the H0 route; the schedule keeps the
+        # equivalent H0 ops (H over zeros == H0)
+        assert oc.get("H", 0) + oc.get("H0", 0) == st["H"] and st["H0"] == 0
+        assert oc.get("H0", 0) == st["F_R0"]
+    else:
+        assert oc.get("H", 0) == st["H"] and oc.get("H0", 0) == st["H0"]
+    if c7[0] < 2:
+        assert st["F_REP"] == st["G_R1"] == st["G_SPC"] == st["H0"] == 0
+
+
+def test_sweep_configs_change_results(pkg, oracle_mod):
+    """the sweep points are different decoders (pruned decoders differ from plain SC on noisy
+    frames); every config still decodes noiseless codewords"""
+    mask = util.mask("FB_N1024_K512")
+    llr, x = util.synth_frames(mask, 200, ebn0_db=1.0, seed=3)
+    outs = {c7: oracle_mod.decode_fsm(mask, llr, config=c7) for c7 in oracle_mod.SWEEP_CONFIGS}
+    assert len({o.tobytes() for o in outs.values()}) >= 3
+    clean = np.where(x == 1, -20, 20).astype(np.int8)
+    for c7 in oracle_mod.SWEEP_CONFIGS:
+        np.testing.assert_array_equal(oracle_mod.decode_fsm(mask, clean[:8], config=c7), x[:8])
+
+
+def test_unsupported_configs(pkg):
+    mask = util.mask("FB_N128_K64")
+    for field, val in (("elag_rare", 1), ("llr_bits", 8), ("par", 64), ("sigmag", 0), ("pruning_level", 3)):
+        c = pkg.default_config()
+        setattr(c, field, val)
+        with pytest.raises(pkg.PolarError):
+            pkg.Decoder(mask, config=c)

@@ -101,6 +101,34 @@ def leaf(lam, fb):
     return np.concatenate([xa ^ xb, xb], axis=1)
 
 
+def leaf_kind(lam, kind):
+    """PRUNING_LEVEL 1 leaf decoders (POLAR_LEAF_REP/SPC/REP2/SPC2) on lam = (s, m) [B, 16]."""
+    s, m = lam
+    B = s.shape[0]
+    if kind in (1, 3):                      # REP_REP2_16_SM: folds 8, 4, 2 (exact), then REP_2
+        ts, tm = s, m
+        n = 16
+        while n > 2:
+            h = n // 2
+            ts, tm = G((ts[:, :h], tm[:, :h]), (ts[:, h:n], tm[:, h:n]), 0)
+            n = h
+        if kind == 1:
+            sig = np.where(tm[:, 0] < tm[:, 1], ts[:, 1], ts[:, 0])
+            return np.repeat(sig[:, None], 16, axis=1)
+        return np.tile(ts[:, :2], (1, 8))
+    # SPC / SPC2: flip the tournament minimum (ties -> smallest bitrev4) of the whole word or
+    # of each class of even / odd positions when its sign parity is odd
+    br = np.array([int("{:04b}".format(l)[::-1], 2) for l in range(16)])
+    key = (m << 4) | br[None, :]
+    x = s.copy()
+    classes = [np.arange(16)] if kind == 2 else [np.arange(0, 16, 2), np.arange(1, 16, 2)]
+    for c in classes:
+        par = s[:, c].sum(axis=1) & 1
+        j = c[key[:, c].argmin(axis=1)]
+        x[np.arange(B), j] ^= par
+    return x
+
+
 def rep_tree(lam):
     s, m = lam
     n = s.shape[1]
@@ -140,7 +168,8 @@ def run_schedule(ops, N, llr):
             buf[k + 1] = G(a, b, ubits(upos, n), 15)
         elif code in ("FLEAF", "GLEAF"):
             lam = F(a, b) if code == "FLEAF" else G(a, b, ubits(upos, 1), 15)
-            bits[:, pos] = leaf((lam[0][:, 0], lam[1][:, 0]), fb)
+            w = (lam[0][:, 0], lam[1][:, 0])
+            bits[:, pos] = leaf(w, fb & 0xFFFF) if (fb >> 16) == 0 else leaf_kind(w, fb >> 16)
         elif code == "REP":
             lam = F(a, b)
             acc = (np.zeros(B, np.int32), np.zeros(B, np.int32))
