@@ -220,6 +220,29 @@ int polar_csim_states(uint32_t N, uint32_t seed8, uint64_t frame0, size_t batch,
 int polar_count_errors(const uint64_t *xhat_dev, const uint64_t *xref_dev, uint32_t N, size_t batch,
                        unsigned long long *counts_dev, void *stream);
 
+/* ---- Per-op monitor ----
+ * The analogue of the reference's latency monitor (sc_monitor.h:50-140 over my_module's
+ * Fct_ID / N_value ports, my_module.h:21-30): one synchronous decode of `batch` resident
+ * frames (hard_bits_dev receives the same x^ as polar_sc_decode) with the schedule
+ * interpreter instrumented (hybrid plans: the hybrid kernel; per-mask plans are profiled
+ * on the interpreter, which runs the same schedule). For every device op, the shader-clock
+ * cycles from its start to the next op's start, measured on the lead wave of frame group 0
+ * while the rest of the batch runs. recs == NULL: only *count (the number of device ops,
+ * END included) is returned. Device ops are the schedule of polar_sc_plan_get_schedule plus,
+ * for HBM-scratch plans, partial-sum window records (code 11 open / 12 flush) and, for hybrid
+ * plans, generated-subtree calls (code 13) in place of the subtree's ops. */
+typedef struct polar_sc_trace_rec {
+    int32_t code;       /* POLAR_OP_* (or 11 / 12 / 13, see above) */
+    int32_t level;      /* source stage level (node of N >> level LLRs) */
+    int32_t n;          /* words per operand half */
+    int32_t pos;
+    uint64_t cycles;    /* shader clock cycles of this op (0 for END) */
+} polar_sc_trace_rec;
+
+int polar_sc_trace(const polar_sc_plan *plan, const int8_t *llr_dev, uint64_t *hard_bits_dev, size_t batch,
+                   polar_sc_trace_rec *recs, uint32_t cap, uint32_t *count, double *clock_ghz,
+                   uint64_t *total_cycles);
+
 /* ---- Frozen-table tooling: Frozen_Bit_Generator (main.cpp:12-52, src/Writer.h:21-167) ---- */
 
 /* Writer.h:61-93: keep the entries of a reliability order (most reliable first) that are

@@ -29,6 +29,8 @@ __all__ = [
 build = _build.build
 
 OPS = {1: "F", 2: "G", 3: "FLEAF", 4: "GLEAF", 5: "REP", 6: "R1", 7: "SPC", 8: "H", 9: "H0", 10: "END"}
+# device-only records of polar_sc_trace (include/polar_sc.h)
+TRACE_OPS = {**OPS, 11: "WOPEN", 12: "WFLUSH", 13: "SUB"}
 
 _ERRNO = {22: "EINVAL", 12: "ENOMEM", 95: "ENOTSUP", 2: "ENOENT", 5: "EIO"}
 
@@ -56,6 +58,11 @@ class polar_sc_op(ctypes.Structure):
                 ("reserved", ctypes.c_int32 * 2)]
 
 
+class polar_sc_trace_rec(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int32), ("level", ctypes.c_int32), ("n", ctypes.c_int32),
+                ("pos", ctypes.c_int32), ("cycles", ctypes.c_uint64)]
+
+
 class polar_sc_plan_stats(ctypes.Structure):
     _fields_ = [("N", ctypes.c_uint32), ("K", ctypes.c_uint32), ("groups", ctypes.c_uint32),
                 ("n_r0", ctypes.c_uint32), ("n_r1", ctypes.c_uint32), ("n_rep", ctypes.c_uint32),
@@ -75,6 +82,7 @@ EXPORTS = (
     "polar_sc_abi_version", "polar_sc_plan_compile", "polar_sc_plan_kernel_source",
     "polar_csim_frames", "polar_csim_states", "polar_count_errors",
     "polar_mask_from_order", "polar_write_frozen_tab", "polar_write_parameters_h", "polar_parse_parameters_h",
+    "polar_sc_trace",
 )
 
 _lib = None
@@ -112,6 +120,8 @@ def lib():
         "polar_csim_states": [u32, u32, ctypes.c_uint64, sz, p],
         "polar_count_errors": [p, p, u32, sz, p, p],
         "polar_mask_from_order": [p, u32, u32, u32, p, u32],
+        "polar_sc_trace": [p, p, p, sz, p, u32, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_double),
+                           ctypes.POINTER(ctypes.c_uint64)],
         "polar_write_frozen_tab": [p, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)],
         "polar_write_parameters_h": [p, u32, u32, i32, ctypes.c_char_p, sz, ctypes.POINTER(sz)],
         "polar_parse_parameters_h": [ctypes.c_char_p, p, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)],
@@ -326,6 +336,33 @@ class Decoder:
             self._plan, ctypes.c_void_p(llr.data_ptr()), ctypes.c_void_p(out.data_ptr()), B,
             ctypes.c_void_p(s.cuda_stream)))
         return out
+
+    def trace(self, llr, out=None):
+        """Per-op monitor: decode `llr` (as decode(), synchronously) with the instrumented
+        kernel and return (records, info). records: one dict per device op (op, level, n, pos,
+        nodeN = LLRs of the source node, cycles); info: clock_ghz, total_cycles, us."""
+        torch = _torch()
+        if not (isinstance(llr, torch.Tensor) and llr.is_cuda and llr.dtype == torch.int8 and llr.is_contiguous()
+                and llr.dim() == 2 and llr.shape[1] == self.N):
+            raise TypeError("llr must be a contiguous CUDA int8 tensor [B, %d]" % self.N)
+        B = llr.shape[0]
+        if out is None:
+            out = torch.empty((B, self.words), dtype=torch.int64, device=llr.device)
+        torch.cuda.synchronize(llr.device)
+        n = ctypes.c_uint32(0)
+        _check("polar_sc_trace", lib().polar_sc_trace(self._plan, ctypes.c_void_p(llr.data_ptr()),
+                                                      ctypes.c_void_p(out.data_ptr()), B, None, 0,
+                                                      ctypes.byref(n), None, None))
+        recs = (polar_sc_trace_rec * n.value)()
+        ghz, tot = ctypes.c_double(0), ctypes.c_uint64(0)
+        _check("polar_sc_trace", lib().polar_sc_trace(self._plan, ctypes.c_void_p(llr.data_ptr()),
+                                                      ctypes.c_void_p(out.data_ptr()), B, recs, n.value,
+                                                      ctypes.byref(n), ctypes.byref(ghz), ctypes.byref(tot)))
+        rows = [dict(op=TRACE_OPS.get(r.code, r.code), level=r.level, n=r.n, pos=r.pos, nodeN=self.N >> r.level,
+                     cycles=int(r.cycles)) for r in recs]
+        info = dict(clock_ghz=ghz.value, total_cycles=int(tot.value),
+                    us=(tot.value / ghz.value / 1e3) if ghz.value > 0 else None, frames=B, out=out)
+        return rows, info
 
     def decode_u16(self, llr, out=None, stream=None):
         """As decode(), output int16 [B, N/16]: the TYPE_BITS tokens of my_module's `s` port."""

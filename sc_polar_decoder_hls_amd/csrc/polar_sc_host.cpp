@@ -22,7 +22,7 @@
 extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out, const void *ops,
                                       uint32_t *scratch, int N, long batch, int out_stride,
                                       int waves_per_group, int groups_per_block, int group_dwords,
-                                      int lds_dwords, int lds0, void *stream);
+                                      int lds_dwords, int lds0, void *stream, unsigned long long *trace);
 extern "C" int polar_sc_launch_selftest(uint32_t *out_dev);
 
 using polar_host::DevState;
@@ -237,7 +237,9 @@ bool config_supported(const polar_sc_config &c)
 int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
 
 // device state for the current device: schedule upload (+ scratch for `batch` frames)
-int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
+// interp: also upload the interpreter schedule of a per-mask plan (the per-op monitor runs
+// the schedule interpreter for those)
+int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool interp = false)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -EIO;
@@ -251,7 +253,7 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out)
     if (p->jit || p->hybrid) {
         int rc = polar_host::jit_load(*p, st);
         if (rc) return rc;
-        if (p->jit) {
+        if (p->jit && !interp) {
             *out = &st;
             return 0;
         }
@@ -313,8 +315,62 @@ int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size
     const int wpg = waves_per_group(p, batch, st->simds);
     if (p->hybrid) return polar_host::jit_launch_hybrid(*p, *st, llr, out, (long)batch, out_stride, wpg, stream);
     rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, (uint32_t *)st->scratch, (int)p->N, (long)batch,
-                                out_stride, wpg, 1, p->hbm_group_dwords, p->lds_group_dwords, p->lds0, stream);
+                                out_stride, wpg, 1, p->hbm_group_dwords, p->lds_group_dwords, p->lds0, stream,
+                                nullptr);
     return rc ? -EIO : 0;
+}
+
+// The per-op monitor (the analogue of the reference's sc_monitor latency report,
+// src/rtl_simu_testbench/sc_monitor/sc_monitor.h:50-140, fed by my_module's Fct_ID / N_value
+// ports, my_module.h:21-30): one decode with the traced interpreter (hybrid plans: the
+// traced hybrid kernel), per device op the shader-clock cycles of frame group 0's lead wave.
+int trace_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size_t batch, int out_stride,
+                 polar_sc_trace_rec *recs, uint32_t cap, uint32_t *count, double *clock_ghz, uint64_t *total)
+{
+    if (!p || !count || batch == 0 || !llr || !out) return -EINVAL;
+    if (batch > (size_t)0x7FFFFFF8) return -EINVAL;
+    const std::vector<polar_sc_op> &dops = (p->hybrid || p->gmem) && !p->dev_ops.empty() ? p->dev_ops : p->ops;
+    *count = (uint32_t)dops.size();
+    if (!recs) return 0;
+    DevState *st = nullptr;
+    int rc = ensure_device(p, batch, &st, true);
+    if (rc) return rc;
+    const size_t slots = dops.size() + 3;
+    unsigned long long *dtrace = nullptr;
+    if (hipMalloc(&dtrace, slots * sizeof(unsigned long long)) != hipSuccess) return -ENOMEM;
+    std::vector<unsigned long long> h(slots, 0);
+    rc = hipMemset(dtrace, 0, slots * sizeof(unsigned long long)) == hipSuccess ? 0 : -EIO;
+    const int wpg = waves_per_group(p, batch, st->simds);
+    if (!rc) {
+        if (p->hybrid)
+            rc = polar_host::jit_launch_hybrid(*p, *st, llr, out, (long)batch, out_stride, wpg, nullptr, dtrace);
+        else
+            rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, (uint32_t *)st->scratch, (int)p->N,
+                                        (long)batch, out_stride, wpg, 1, p->hbm_group_dwords, p->lds_group_dwords,
+                                        p->lds0, nullptr, dtrace) ? -EIO : 0;
+    }
+    if (!rc && hipDeviceSynchronize() != hipSuccess) rc = -EIO;
+    if (!rc && hipMemcpy(h.data(), dtrace, slots * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = -EIO;
+    (void)hipFree(dtrace);
+    if (rc) return rc;
+    const size_t n = dops.size();   // the last record is END: its slot holds the finish time
+    const uint64_t t0 = h[2], t1 = h[2 + n - 1];
+    for (size_t i = 0; i < n && i < cap; i++) {
+        polar_sc_trace_rec r{};
+        r.code = dops[i].code;
+        r.level = dops[i].level;
+        r.n = dops[i].n;
+        r.pos = dops[i].pos;
+        r.cycles = i + 1 < n ? h[2 + i + 1] - h[2 + i] : 0;
+        recs[i] = r;
+    }
+    if (total) *total = t1 - t0;
+    if (clock_ghz) {
+        const double wall_ns = (double)(h[1] - h[0]) * 10.0;   // s_memrealtime: 100 MHz
+        *clock_ghz = wall_ns > 0 ? (double)(t1 - t0) / wall_ns : 0.0;
+    }
+    return 0;
 }
 
 bool read_text(const char *path, std::string &s)
@@ -500,6 +556,16 @@ int polar_sc_decode(const polar_sc_plan *p, const int8_t *llr_dev, uint64_t *har
     if (!p) return -EINVAL;
     const int stride16 = (int)(4 * ((p->G + 3) / 4));
     return decode_common(p, llr_dev, (uint16_t *)hard_bits_dev, batch, stride16, stream);
+}
+
+int polar_sc_trace(const polar_sc_plan *p, const int8_t *llr_dev, uint64_t *hard_bits_dev, size_t batch,
+                   polar_sc_trace_rec *recs, uint32_t cap, uint32_t *count, double *clock_ghz,
+                   uint64_t *total_cycles)
+{
+    if (!p) return -EINVAL;
+    const int stride16 = (int)(4 * ((p->G + 3) / 4));
+    return trace_common(p, llr_dev, (uint16_t *)hard_bits_dev, batch, stride16, recs, cap, count, clock_ghz,
+                        total_cycles);
 }
 
 int polar_sc_decode_u16(const polar_sc_plan *p, const int8_t *llr_dev, uint16_t *bits_dev,

@@ -428,11 +428,15 @@ __device__ __forceinline__ bool op_split(int code, int n, int wpg)
     }
 }
 
-template <bool GMEM>
+// TRACE (the per-op monitor, polar_sc_trace): the lead wave of group 0 stamps the shader
+// clock (s_memtime) when each op starts, after its barrier: trace[2 + i] for device op i, the
+// END record's slot holding the finish time; trace[0] / trace[1] = s_memrealtime (100 MHz)
+// at start and finish, to calibrate the clock.
+template <bool GMEM, bool TRACE = false>
 __device__ __forceinline__ void decode_body(
     const int8_t *__restrict__ llr, uint16_t *__restrict__ out, const Op *__restrict__ ops,
     uint32_t *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb,
-    int group_dwords, int lds_dwords, int lds0)
+    int group_dwords, int lds_dwords, int lds0, unsigned long long *__restrict__ trace = nullptr)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int lane = threadIdx.x & 63;
@@ -472,6 +476,8 @@ __device__ __forceinline__ void decode_body(
     if (wi == lead)
         for (int d = 0; d < nbd; d++) c.bst(d, 0u);
 
+    const bool tracer = TRACE && group == 0 && wi == lead && lane == 0;
+    if (tracer) trace[0] = __builtin_amdgcn_s_memrealtime();
     bool prev_split = true;
     int win_d0 = -1;   // GMEM: first bit dword of the open partial-sum window
     // the record of the next op is loaded while the current one runs (the schedule of a
@@ -479,7 +485,13 @@ __device__ __forceinline__ void decode_body(
     Op cur = ops[0];
     for (int oi = 0;; oi++) {
         const int code = __builtin_amdgcn_readfirstlane(cur.code);
-        if (code == OP_END) break;
+        if (code == OP_END) {
+            if (tracer) {
+                trace[2 + oi] = __builtin_readcyclecounter();
+                trace[1] = __builtin_amdgcn_s_memrealtime();
+            }
+            break;
+        }
         const Op nxt = ops[oi + 1];
         const int k = __builtin_amdgcn_readfirstlane(cur.level);
         const int n = __builtin_amdgcn_readfirstlane(cur.n);
@@ -490,6 +502,7 @@ __device__ __forceinline__ void decode_body(
         cur = nxt;
         const bool split = op_split(code, n, wpg);
         if (wpg > 1 && (split || prev_split)) __syncthreads();
+        if (tracer) trace[2 + oi] = __builtin_readcyclecounter();
         prev_split = split;
         if constexpr (GMEM) {
             if (code == OP_WOPEN || code == OP_WFLUSH) {

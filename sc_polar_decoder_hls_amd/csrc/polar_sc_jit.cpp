@@ -452,7 +452,14 @@ std::string hybrid_source(const polar_sc_plan &p)
       << "    unsigned int *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb, int group_dwords,\n"
       << "    int lds_dwords, int lds0)\n{\n"
       << "  polar::decode_body<" << (gm ? "true" : "false")
-      << ">(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords, lds0);\n}\n";
+      << ">(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords, lds0);\n}\n"
+      // the per-op monitor variant (polar_sc_trace)
+      << "extern \"C\" __global__ void __launch_bounds__(" << HYBRID_MAX_WAVES * 64 << ") polar_sc_hybrid_trace_kernel(\n"
+      << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
+      << "    unsigned int *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb, int group_dwords,\n"
+      << "    int lds_dwords, int lds0, unsigned long long *__restrict__ trace)\n{\n"
+      << "  polar::decode_body<" << (gm ? "true" : "false")
+      << ", true>(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords, lds0, trace);\n}\n";
     return o.str();
 }
 
@@ -499,6 +506,8 @@ int jit_load(const polar_sc_plan &p, DevState &st)
     if (hipModuleGetFunction(&st.fn, st.module, p.hybrid ? "polar_sc_hybrid_kernel" : "polar_sc_mask_kernel") !=
         hipSuccess)
         return -EIO;
+    if (p.hybrid && hipModuleGetFunction(&st.fn_trace, st.module, "polar_sc_hybrid_trace_kernel") != hipSuccess)
+        return -EIO;
     return 0;
 }
 
@@ -516,7 +525,7 @@ int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, ui
 
 // hybrid kernel: the interpreter's launch shape (polar_sc_kernels.hip, polar_sc_launch_decode)
 int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
-                      int out_stride, int wpg, void *stream)
+                      int out_stride, int wpg, void *stream, unsigned long long *trace)
 {
     const long groups = (batch + 7) / 8;
     const unsigned lds = (unsigned)p.lds_group_dwords * 4u;
@@ -524,9 +533,10 @@ int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *
     void *scratch = st.scratch;
     int N = (int)p.N, b = (int)batch, gpb = 1, gd = p.hbm_group_dwords, ld = p.lds_group_dwords, l0 = p.lds0;
     void *args[] = {(void *)&llr, (void *)&out, (void *)&ops, (void *)&scratch, (void *)&N, (void *)&b,
-                    (void *)&out_stride, (void *)&wpg, (void *)&gpb, (void *)&gd, (void *)&ld, (void *)&l0};
-    hipError_t e = hipModuleLaunchKernel(st.fn, (unsigned)groups, 1, 1, (unsigned)(64 * wpg), 1, 1, lds,
-                                         (hipStream_t)stream, args, nullptr);
+                    (void *)&out_stride, (void *)&wpg, (void *)&gpb, (void *)&gd, (void *)&ld, (void *)&l0,
+                    (void *)&trace};
+    hipError_t e = hipModuleLaunchKernel(trace ? st.fn_trace : st.fn, (unsigned)groups, 1, 1, (unsigned)(64 * wpg), 1,
+                                         1, lds, (hipStream_t)stream, args, nullptr);
     return e == hipSuccess ? 0 : -EIO;
 }
 

@@ -17,6 +17,17 @@ __global__ void __launch_bounds__(1024) polar_sc_decode_kernel(
     decode_body<GMEM>(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords, lds0);
 }
 
+// the same with the per-op monitor (polar_sc_trace)
+template <bool GMEM>
+__global__ void __launch_bounds__(1024) polar_sc_decode_trace_kernel(
+    const int8_t *__restrict__ llr, uint16_t *__restrict__ out, const Op *__restrict__ ops,
+    uint32_t *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb,
+    int group_dwords, int lds_dwords, int lds0, unsigned long long *__restrict__ trace)
+{
+    decode_body<GMEM, true>(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords,
+                            lds0, trace);
+}
+
 // DPP exchange self-test: out[h*64 + lane] = lane id seen through xorlane<1<<h>
 __global__ void polar_sc_lane_selftest_kernel(uint32_t *out)
 {
@@ -35,7 +46,7 @@ __global__ void polar_sc_lane_selftest_kernel(uint32_t *out)
 extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out, const void *ops,
                                       uint32_t *scratch, int N, long batch, int out_stride,
                                       int waves_per_group, int groups_per_block, int group_dwords,
-                                      int lds_dwords, int lds0, void *stream)
+                                      int lds_dwords, int lds0, void *stream, unsigned long long *trace)
 {
     const long groups = (batch + 7) / 8;
     const long blocks = (groups + groups_per_block - 1) / groups_per_block;
@@ -43,13 +54,24 @@ extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out
     hipStream_t s = (hipStream_t)stream;
     const polar::Op *o = (const polar::Op *)ops;
     const size_t lds = (size_t)groups_per_block * (size_t)lds_dwords * 4u;
-    const void *fn = gmem ? (const void *)polar::polar_sc_decode_kernel<true>
-                          : (const void *)polar::polar_sc_decode_kernel<false>;
+    const void *fn = trace ? (gmem ? (const void *)polar::polar_sc_decode_trace_kernel<true>
+                                   : (const void *)polar::polar_sc_decode_trace_kernel<false>)
+                           : (gmem ? (const void *)polar::polar_sc_decode_kernel<true>
+                                   : (const void *)polar::polar_sc_decode_kernel<false>);
     if (lds > 65536) {
         hipError_t ae = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (ae != hipSuccess) return -(int)ae - 1000;
     }
-    if (gmem) {
+    if (trace) {
+        if (gmem)
+            hipLaunchKernelGGL(polar::polar_sc_decode_trace_kernel<true>, grid, block, lds, s, llr, out, o, scratch,
+                               N, (int)batch, out_stride, waves_per_group, groups_per_block, group_dwords,
+                               lds_dwords, lds0, trace);
+        else
+            hipLaunchKernelGGL(polar::polar_sc_decode_trace_kernel<false>, grid, block, lds, s, llr, out, o, scratch,
+                               N, (int)batch, out_stride, waves_per_group, groups_per_block, group_dwords,
+                               lds_dwords, lds0, trace);
+    } else if (gmem) {
         hipLaunchKernelGGL(polar::polar_sc_decode_kernel<true>, grid, block, lds, s, llr, out, o, scratch, N,
                            (int)batch, out_stride, waves_per_group, groups_per_block, group_dwords, lds_dwords,
                            lds0);

@@ -20,6 +20,7 @@ struct DevState {
     size_t scratch_bytes = 0;
     hipModule_t module = nullptr; // per-mask kernel
     hipFunction_t fn = nullptr;
+    hipFunction_t fn_trace = nullptr;   // hybrid plans: the per-op monitor variant
     int simds = 0;                // SIMDs of the device (4 per CU), for launch sizing
 };
 
@@ -80,6 +81,6 @@ int jit_load(const polar_sc_plan &p, DevState &st);      // module + function on
 int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out,
                long batch, int out_stride, void *stream);
 int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
-                      int out_stride, int wpg, void *stream);
+                      int out_stride, int wpg, void *stream, unsigned long long *trace = nullptr);
 bool jit_supported(uint32_t N);
 }  // namespace polar_host

@@ -1,0 +1,48 @@
+"""Per-op monitor: report aggregation on the host (CPU) and the traced
+decode on the GPU (same x^ as the plain decode, one record per device op, cycles summing to
+the total)."""
+import numpy as np
+import pytest
+
+import util
+from sc_polar_decoder_hls_amd import monitor
+
+
+def test_report_aggregation():
+    rows = [dict(op="F", level=0, n=4, pos=0, nodeN=128, cycles=100),
+            dict(op="F", level=1, n=2, pos=0, nodeN=64, cycles=50),
+            dict(op="FLEAF", level=2, n=1, pos=0, nodeN=32, cycles=30),
+            dict(op="GLEAF", level=2, n=1, pos=1, nodeN=32, cycles=40),
+            dict(op="H", level=2, n=1, pos=0, nodeN=32, cycles=5),
+            dict(op="G", level=1, n=2, pos=2, nodeN=64, cycles=60),
+            dict(op="SPC", level=1, n=2, pos=2, nodeN=64, cycles=20),
+            dict(op="END", level=0, n=0, pos=0, nodeN=128, cycles=0)]
+    rep = monitor.report(rows, dict(total_cycles=305, clock_ghz=2.0, us=0.1525))
+    assert rep["by_level"] == {128: 100, 64: 130, 32: 75}
+    assert rep["by_function"]["F"] == 150 and rep["by_function"]["R"] == 70 and rep["by_function"]["G_SPC"] == 20
+    assert rep["ops"]["R"] == 2
+    # sc_monitor counts a new occurrence whenever the (function, level) pair changes
+    assert rep["occurrences"]["R@32"] == 1 and rep["occurrences"]["F@128"] == 1 and rep["occurrences"]["F@64"] == 1
+    assert "Latency by Function" in monitor.format_report(rep)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,batch", [("FB_N1024_K512", 64), ("FB_N128_K64", 8), ("frozen_n_4096_k_2048", 24),
+                                        ("frozen_n_16384_k_8192", 16)])
+def test_trace_decode(pkg, cuda, oracle_mod, name, batch):
+    mask = util.mask(name)
+    llr, _ = util.synth_frames(mask, batch, ebn0_db=2.0, seed=5)
+    dec = pkg.Decoder(mask)
+    t = cuda.from_numpy(llr).cuda()
+    rows, info = dec.trace(t)
+    got = pkg.unpack_bits(info["out"].cpu().numpy(), mask.size)
+    np.testing.assert_array_equal(got, oracle_mod.decode_fsm(mask, llr))
+    assert rows[-1]["op"] == "END"
+    body = [r for r in rows if r["op"] != "END"]
+    assert all(r["cycles"] > 0 for r in body)
+    assert sum(r["cycles"] for r in body) == info["total_cycles"]
+    assert 0.5 < info["clock_ghz"] < 3.5
+    if dec.stats["kernel"] == 2:
+        assert any(r["op"] == "SUB" for r in rows)
+    rep = monitor.report(rows, info)
+    assert sum(rep["by_function"].values()) == info["total_cycles"]
