@@ -292,9 +292,9 @@ int waves_per_group(const polar_sc_plan *p, size_t batch, int simds)
     const char *env = std::getenv("POLAR_SC_WAVES_PER_GROUP");
     if (env && *env) {
         int w = std::atoi(env);
-        if (w >= 1 && w <= 16 && (w & (w - 1)) == 0) return p->hybrid && w > polar_host::HYBRID_MAX_WAVES ? polar_host::HYBRID_MAX_WAVES : w;
+        if (w >= 1 && w <= 16 && (w & (w - 1)) == 0) return p->hybrid && w > p->hybrid_waves ? p->hybrid_waves : w;
     }
-    const int wmax = p->hybrid ? polar_host::HYBRID_MAX_WAVES : 16;
+    const int wmax = p->hybrid ? p->hybrid_waves : 16;
     const size_t groups = (batch + 7) / 8;
     const size_t target = 2u * (size_t)(simds > 0 ? simds : 1024);
     int w = 1;
@@ -505,6 +505,11 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         compile_node(*p, dev_sched, 0, 0, p->G, true, &sc);
         emit(dev_sched, POLAR_OP_END, 0, 0, 0, -1, 0);
         p->hybrid = 1;
+        p->hybrid_waves = polar_host::HYBRID_MAX_WAVES;
+        if (const char *e = std::getenv("POLAR_SC_HYBRID_WAVES")) {
+            const int w = std::atoi(e);
+            if (w == 4 || w == 8) p->hybrid_waves = w;
+        }
         p->sub_words = sub_words;
         p->subs = std::move(sc.lists);
         s.sub_words = (uint32_t)sub_words;

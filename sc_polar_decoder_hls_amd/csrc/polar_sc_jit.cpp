@@ -447,14 +447,14 @@ std::string hybrid_source(const polar_sc_plan &p)
     for (size_t id = 0; id < p.subs.size(); id++)
         o << "  case " << id << ": polar_sub_" << id << "(c, ldo, pos); return;\n";
     o << "  default: return;\n  }\n}\n}  // namespace polar\n"
-      << "extern \"C\" __global__ void __launch_bounds__(" << HYBRID_MAX_WAVES * 64 << ") polar_sc_hybrid_kernel(\n"
+      << "extern \"C\" __global__ void __launch_bounds__(" << p.hybrid_waves * 64 << ") polar_sc_hybrid_kernel(\n"
       << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
       << "    unsigned int *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb, int group_dwords,\n"
       << "    int lds_dwords, int lds0)\n{\n"
       << "  polar::decode_body<" << (gm ? "true" : "false")
       << ">(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords, lds0);\n}\n"
       // the per-op monitor variant (polar_sc_trace)
-      << "extern \"C\" __global__ void __launch_bounds__(" << HYBRID_MAX_WAVES * 64 << ") polar_sc_hybrid_trace_kernel(\n"
+      << "extern \"C\" __global__ void __launch_bounds__(" << p.hybrid_waves * 64 << ") polar_sc_hybrid_trace_kernel(\n"
       << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
       << "    unsigned int *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb, int group_dwords,\n"
       << "    int lds_dwords, int lds0, unsigned long long *__restrict__ trace)\n{\n"

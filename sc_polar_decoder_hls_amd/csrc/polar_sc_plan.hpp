@@ -37,9 +37,12 @@ struct HostBufs {
 // plans, and the generated-subtree call of hybrid plans
 enum { POLAR_OP_WOPEN = 11, POLAR_OP_WFLUSH = 12, POLAR_OP_SUB = 13 };
 
-// hybrid kernels: at most 4 waves per 8-frame group (one block), so the subtree decoders get
-// the register budget of a 256-thread block
-constexpr int HYBRID_MAX_WAVES = 4;
+// hybrid kernels: by default at most 8 waves per 8-frame group (one 512-thread block, the
+// kernel's launch bound); POLAR_SC_HYBRID_WAVES (4 or 8) at plan creation changes it.
+// Measured (tools/wpg_sweep.py): C5 (512 frames) 6.50 -> 5.99 ms from 4 to 8 waves, C3
+// (4096 frames, which keeps 4 waves per group) unchanged; 16 waves (1024-thread blocks with
+// spilled subtree code) failed to launch (HSA_STATUS_ERROR_INVALID_ISA).
+constexpr int HYBRID_MAX_WAVES = 8;
 
 }  // namespace polar_host
 
@@ -62,6 +65,7 @@ struct polar_sc_plan {
     // words with a POLAR_OP_SUB record; subs[id] is that subtree's own schedule (levels and
     // positions relative to the subtree root), compiled to straight-line code
     int hybrid = 0;
+    int hybrid_waves = 8;            // waves per group cap = launch bound / 64 of the hybrid kernel
     int sub_words = 0;
     std::vector<std::vector<polar_sc_op>> subs;
     mutable std::mutex mu;
