@@ -64,6 +64,11 @@ struct Op {            // == polar_sc_op (include/polar_sc.h)
 // pointers include the lane offset; slot / bit-dword indices are wave-uniform.
 // ---------------------------------------------------------------------------------------
 template <bool GMEM>
+struct Ctx;
+template <class C> struct GMEM_OF;
+template <bool GMEM> struct GMEM_OF<Ctx<GMEM>> { static constexpr bool value = GMEM; };
+
+template <bool GMEM>
 struct Ctx {
     uint16_t *hs;          // HBM scratch (GMEM): slots [0, lds0) as SM8 pairs (128 B rows)
     uint32_t *hbit;        // HBM scratch (GMEM): bit dwords (256 B rows)
@@ -96,6 +101,13 @@ struct Ctx {
     __device__ __forceinline__ uint32_t bld(int d) const
     {
         if constexpr (GMEM) return wd0 >= 0 ? *wl(d) : hbit[d * 64];
+        else return lb[(nslot + d) * 64];
+    }
+    // bit dword of an op that is never windowed (its node is wider than the window): a plain
+    // load, not a flat one through a selected pointer (which would also wait for the LDS)
+    __device__ __forceinline__ uint32_t bld_nowin(int d) const
+    {
+        if constexpr (GMEM) return hbit[d * 64];
         else return lb[(nslot + d) * 64];
     }
     __device__ __forceinline__ void bst(int d, uint32_t v) const
@@ -172,8 +184,14 @@ __device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int
             // partial sums of words upos+i .. upos+i+CH-1 (at most two bit dwords)
             uint32_t u0 = 0, u1 = 0;
             if (upos >= 0) {
-                u0 = c.bld((upos + i) >> 4);
-                u1 = c.bld((upos + i + CH - 1) >> 4);
+                // ops wider than the partial-sum window (2n > 128 words) are never windowed
+                if (GMEM_OF<C>::value && n > 64) {
+                    u0 = c.bld_nowin((upos + i) >> 4);
+                    u1 = c.bld_nowin((upos + i + CH - 1) >> 4);
+                } else {
+                    u0 = c.bld((upos + i) >> 4);
+                    u1 = c.bld((upos + i + CH - 1) >> 4);
+                }
             }
 #pragma unroll
             for (int j = 0; j < CH; j++) {
@@ -440,7 +458,7 @@ __device__ __forceinline__ void decode_body(
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int lane = threadIdx.x & 63;
-    const int wib = threadIdx.x >> 6;
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar loop control
     const int wi = wib % wpg;                       // wave index in its group
     // the wave that runs the unsplit ops: rotated over the groups so that the lead waves of
     // the groups sharing a CU do not all sit on the same SIMD
