@@ -34,7 +34,7 @@ constexpr uint32_t NODE_R0 = 0x00, NODE_R1 = 0x0F, NODE_REP = 0x02, NODE_SPC = 0
 
 // largest per-wave LDS footprint kept on chip; above it stages go to HBM scratch
 constexpr uint32_t LDS_WAVE_LIMIT = 80u * 1024u;   // all-LDS interpreter limit per 8-frame group
-constexpr int LDS_LOW_SLOTS = 128;                  // HBM mode: nodes <= 128 words keep their levels in LDS
+constexpr int LDS_LOW_SLOTS = 256;                  // HBM mode: the levels of nodes <= 128 words stay in LDS (WIN_DWORDS = this / 16)
 
 }  // namespace
 

@@ -46,7 +46,7 @@ enum : int {
     OP_WOPEN = 11, OP_WFLUSH = 12,  // HBM-scratch plans: partial-sum window of a 128-word subtree
     OP_SUB = 13                     // hybrid plans: generated subtree decoder `fb` at node (level, pos)
 };
-constexpr int WIN_DWORDS = 8;       // 128 words of partial sums
+constexpr int WIN_DWORDS = 16;      // 256 words of partial sums (polar_sc_host.cpp LDS_LOW_SLOTS / 16)
 
 struct Op {            // == polar_sc_op (include/polar_sc.h)
     int32_t code, level, n, pos, upos;
@@ -184,8 +184,9 @@ __device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int
             // partial sums of words upos+i .. upos+i+CH-1 (at most two bit dwords)
             uint32_t u0 = 0, u1 = 0;
             if (upos >= 0) {
-                // ops wider than the partial-sum window (2n > 128 words) are never windowed
-                if (GMEM_OF<C>::value && n > 64) {
+                // ops wider than the partial-sum window (2n > 16 * WIN_DWORDS words) are never
+                // windowed (polar_sc_host.cpp window_schedule)
+                if (GMEM_OF<C>::value && n > 8 * WIN_DWORDS) {
                     u0 = c.bld_nowin((upos + i) >> 4);
                     u1 = c.bld_nowin((upos + i + CH - 1) >> 4);
                 } else {
