@@ -4,6 +4,7 @@ TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.
 cpu_baseline leg as the checker / timed CPU baseline. The product package
 (sc_polar_decoder_hls_amd) never imports this module.
 """
+import contextlib
 import ctypes
 import os
 import subprocess
@@ -67,6 +68,8 @@ def lib():
             getattr(L, name).restype = u32
         L.orc_encode.argtypes = [i32, p, p, i32]
         L.orc_encode.restype = None
+        L.orc_set_llr_bits.argtypes = [i32]
+        L.orc_set_llr_bits.restype = i32
         _lib = L
     return _lib
 
@@ -93,17 +96,30 @@ def _cfg(config):
     return c
 
 
-def decode_fsm(mask, llr, return_counts=False, config=None):
+@contextlib.contextmanager
+def _llr_bits(q):
+    """LLR_BITS of the restatement for the calling thread (config.h:2; 6 = as shipped)."""
+    if lib().orc_set_llr_bits(int(q)) != 0:
+        raise ValueError("llr_bits must be 5..8, got %r" % (q,))
+    try:
+        yield
+    finally:
+        lib().orc_set_llr_bits(6)
+
+
+def decode_fsm(mask, llr, return_counts=False, config=None, llr_bits=6):
     """Literal FSM decode. mask: (N,) 0/1; llr: (B, N) int8. Returns xhat (B, N) uint8.
-    config: 7-tuple (see SWEEP_CONFIGS) or None for the shipped config.h."""
+    config: 7-tuple (see SWEEP_CONFIGS) or None for the shipped config.h; llr_bits: LLR_BITS
+    (5..8, the low llr_bits of each int8 are the LLR)."""
     mask = np.ascontiguousarray(mask, dtype=np.uint8)
     llr = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
     B, N = llr.shape
     out = np.zeros((B, N), dtype=np.uint8)
     counts = np.zeros(len(STATES), dtype=np.int64)
     c = _cfg(config)
-    rc = lib().orc_decode_fsm_cfg(N, _ptr(mask), _ptr(llr), _ptr(out), B, _ptr(counts),
-                                  None if c is None else _ptr(c))
+    with _llr_bits(llr_bits):
+        rc = lib().orc_decode_fsm_cfg(N, _ptr(mask), _ptr(llr), _ptr(out), B, _ptr(counts),
+                                      None if c is None else _ptr(c))
     if rc != 0:
         raise RuntimeError("orc_decode_fsm failed: %d" % rc)
     if return_counts:
@@ -111,14 +127,15 @@ def decode_fsm(mask, llr, return_counts=False, config=None):
     return out
 
 
-def decode_rec(mask, llr, config=None):
+def decode_rec(mask, llr, config=None, llr_bits=6):
     """Recursive-restatement decode (same I/O as decode_fsm)."""
     mask = np.ascontiguousarray(mask, dtype=np.uint8)
     llr = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
     B, N = llr.shape
     out = np.zeros((B, N), dtype=np.uint8)
     c = _cfg(config)
-    rc = lib().orc_decode_rec_cfg(N, _ptr(mask), _ptr(llr), _ptr(out), B, None if c is None else _ptr(c))
+    with _llr_bits(llr_bits):
+        rc = lib().orc_decode_rec_cfg(N, _ptr(mask), _ptr(llr), _ptr(out), B, None if c is None else _ptr(c))
     if rc != 0:
         raise RuntimeError("orc_decode_rec failed: %d" % rc)
     return out

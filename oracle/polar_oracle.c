@@ -37,7 +37,19 @@
 #include <string.h>
 
 #define PAR 16
-#define LLR_BITS 6
+
+/* LLR_BITS (config.h:2): 6 in the shipped config. The reference's pruning sweep runs at
+ * QUANT = 8 (script/script_tests.sh:9,25); orc_set_llr_bits() selects 5..8 for the calling
+ * thread, as the GPU plans take polar_sc_config.llr_bits. */
+static _Thread_local int g_llr_bits = 6;
+#define LLR_BITS g_llr_bits
+
+int orc_set_llr_bits(int q)
+{
+    if (q < 5 || q > 8) return -22;
+    g_llr_bits = q;
+    return 0;
+}
 
 /* node codes: shared/src/library.h:34-40 */
 #define NODE_R0   0x00
@@ -192,8 +204,8 @@ uint32_t orc_leaf16(const uint32_t *llr, uint32_t fb)
     return spec_pn_ext(16, LLR_BITS, llr, fb & 0xFFFFu);
 }
 
-/* ADD_TREE_16_SM<6> + ADDER_TREE_16<6> (functions.h:3036-3083, 3190-3205).
- * llr: 16 six-bit SM. old_sum / return: 11-bit SM (sign bit 10). */
+/* ADD_TREE_16_SM<Q> + ADDER_TREE_16<Q> (functions.h:3036-3083, 3190-3205), Q = LLR_BITS.
+ * llr: 16 Q-bit SM. old_sum / return: (Q+5)-bit SM (sign bit Q+4: 11 bits at Q = 6). */
 uint32_t orc_rep_add_tree16(const uint32_t *llr, uint32_t old_sum)
 {
     uint32_t v[16];
@@ -205,10 +217,12 @@ uint32_t orc_rep_add_tree16(const uint32_t *llr, uint32_t old_sum)
         n = h;
         Q += 1;
     }
-    /* add_tree is (Q+4)=10 bits: sign bit 9, magnitude bits 8..0; extend to 11 bits */
-    uint32_t add_tree = v[0] & msk(10);
-    uint32_t ext = (((add_tree >> 9) & 1u) << 10) | (add_tree & msk(9));
-    return orc_full_adder_sat_sm(11, ext, old_sum & msk(11));
+    /* add_tree is Q+4 bits (sign bit Q+3), extended to the Q+5 bits of the accumulator
+     * (functions.h:3200-3202) */
+    const int W = LLR_BITS + 4;
+    uint32_t add_tree = v[0] & msk(W);
+    uint32_t ext = (((add_tree >> (W - 1)) & 1u) << W) | (add_tree & msk(W - 1));
+    return orc_full_adder_sat_sm(W + 1, ext, old_sum & msk(W + 1));
 }
 
 /* Min_Mask_16_SM<5> via Min_Mask_TREE_16<6> (functions.h:3652-3747, 3900-3913).
@@ -589,7 +603,7 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             N_REG = CNT(N_REG >> 1);
             stk_push(&stack, 0);
             stk_push(&m->nts, 0x00);
-            uint32_t sum = 0;   /* sc_bigint<LLR_BITS + LOG2_PAR + 1> = 11-bit SM pattern */
+            uint32_t sum = 0;   /* sc_bigint<LLR_BITS + LOG2_PAR + 1>: (Q+5)-bit SM pattern */
             for (uint32_t i = 0; i < NB_ITER; i++) {
                 word_t res;
                 CHK(adr_a); CHK(adr_b); CHK(adr_s);
@@ -598,7 +612,7 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
                 m->bit_mem_1[adr_s] = 0; m->bit_mem_2[adr_s] = 0;
                 adr_a = CNT(adr_a + 1); adr_b = CNT(adr_b + 1); adr_s = CNT(adr_s + 1);
             }
-            if ((sum >> 10) & 1u) {
+            if ((sum >> (LLR_BITS + 4)) & 1u) {   /* VECTOR_SIGN<1, LLR_BITS + LOG2_PAR + 1> */
                 adr_s = CNT(adr_s - NB_ITER);
                 for (uint32_t i = 0; i < NB_ITER; i++) {
                     CHK(adr_s);
@@ -800,7 +814,7 @@ static void rec_node(rec_t *r, int g0, int cnt, const word_t *lam, int is_root)
     } else if (tl == NODE_REP) {
         uint32_t acc = 0;
         for (int i = 0; i < h; i++) { word_t t; word_F(t, lam[i], lam[h + i]); acc = orc_rep_add_tree16(t, acc); }
-        uint16_t d = ((acc >> 10) & 1u) ? 0xFFFF : 0;
+        uint16_t d = ((acc >> (LLR_BITS + 4)) & 1u) ? 0xFFFF : 0;
         for (int i = 0; i < h; i++) r->x[g0 + i] = d;
     } else {
         for (int i = 0; i < h; i++) word_F(child[i], lam[i], lam[h + i]);
@@ -821,7 +835,7 @@ static void rec_node(rec_t *r, int g0, int cnt, const word_t *lam, int is_root)
             for (int l = 0; l < PAR; l++) {
                 parity ^= (s >> l) & 1u;
                 uint32_t br = ((l & 1) << 3) | ((l & 2) << 1) | ((l & 4) >> 1) | ((l & 8) >> 3);
-                uint32_t key = ((child[i][l] & 0x1Fu) << 24) | ((uint32_t)i << 4) | br;
+                uint32_t key = ((child[i][l] & msk(LLR_BITS - 1)) << 24) | ((uint32_t)i << 4) | br;
                 if (key < best) { best = key; bg = i; bl = l; }
             }
         }

@@ -17,6 +17,19 @@ typedef short i16x2 __attribute__((ext_vector_type(2)));
 constexpr u32 SGN = 0x80008000u;   // sign flags of both halves
 constexpr u32 MAG = 0x7FFF7FFFu;   // magnitudes of both halves
 
+// LLR_BITS (config.h:2). The hipcc-built schedule interpreter is the shipped 6; generated
+// (hipRTC) kernels of plans with another llr_bits define POLAR_Q first. 5..8: the channel
+// is an int8 stream, and HBM slots keep SM8.
+#ifndef POLAR_Q
+#define POLAR_Q 6
+#endif
+static_assert(POLAR_Q >= 5 && POLAR_Q <= 8, "LLR_BITS 5..8");
+constexpr int QB = POLAR_Q;
+constexpr u32 QMAG = (1u << (QB - 1)) - 1u;     // channel / F magnitude bound (31 at 6 bits)
+constexpr u32 GSAT = (1u << (QB - 2)) - 1u;     // G clamp, qsat_sm<Q-1> (15)
+constexpr u32 REPSAT = (1u << (QB + 3)) - 1u;   // REP accumulator clamp, qfull_adder_sat_sm<Q+5> (511)
+constexpr u32 GSAT2 = GSAT * 0x00010001u;
+
 // ---------------------------------------------------------------------------------------
 // packed 16-bit helpers (v_pk_* on gfx950)
 // ---------------------------------------------------------------------------------------
@@ -304,24 +317,27 @@ __device__ __forceinline__ u32 leaf_spc(u32 L, const Lanes &ln)
 // set iff t >= 33 (t + 0x7FDF reaches bit 15).
 __device__ __forceinline__ u32 conv_pair(u32 raw)
 {
-    u32 t = raw & 0x003F003Fu;
-    u32 m = pk_min(t, pk_sub(0x00400040u, t)) & 0x001F001Fu;
-    return m | (pk_add(t, 0x7FDF7FDFu) & SGN);
+    constexpr u32 QM = (1u << QB) - 1u, QP = 1u << QB;
+    constexpr u32 SB = 0x8000u - (QP / 2u + 1u);   // t + SB reaches bit 15 iff t > 2^(Q-1)
+    u32 t = raw & (QM * 0x00010001u);
+    u32 m = pk_min(t, pk_sub(QP * 0x00010001u, t)) & (QMAG * 0x00010001u);
+    return m | (pk_add(t, SB * 0x00010001u) & SGN);
 }
 
 // Channel byte -> SM8 (bit 7 sign, bits 0..4 magnitude): the per-mask kernels keep a
 // 256-entry copy of this map in LDS and convert a word with two lookups + 2 VALU.
 __device__ __forceinline__ u32 sm8_of_byte(u32 b)
 {
-    const u32 t = b & 63u;
-    const u32 m = (t < 64u - t ? t : 64u - t) & 31u;
-    return (t >= 33u ? 0x80u : 0u) | m;
+    constexpr u32 QP = 1u << QB;
+    const u32 t = b & (QP - 1u);
+    const u32 m = (t < QP - t ? t : QP - t) & QMAG;
+    return (t >= QP / 2u + 1u ? 0x80u : 0u) | m;
 }
 // two SM8 bytes (low byte of lo, low byte of hi) -> SM16 pair: duplicate each byte into both
 // bytes of its half, keep bit 15 and bits 0..4
 __device__ __forceinline__ u32 sm8_pair(u32 lo, u32 hi)
 {
-    return __builtin_amdgcn_perm(hi, lo, 0x04040000u) & 0x801F801Fu;
+    return __builtin_amdgcn_perm(hi, lo, 0x04040000u) & ((0x8000u | QMAG) * 0x00010001u);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -371,7 +387,7 @@ __device__ __forceinline__ u32 leaf_ms(u32 M, u32 S, const Lanes &ln)
 // bits 8..15); inverse of sm8_pair
 __device__ __forceinline__ u32 sm16_to_sm8x2(u32 v)
 {
-    const u32 t = (v & 0x001F001Fu) | ((v >> 8) & 0x00800080u);   // SM8 in bytes 0 and 2
+    const u32 t = (v & (QMAG * 0x00010001u)) | ((v >> 8) & 0x00800080u);   // SM8 in bytes 0 and 2
     return __builtin_amdgcn_perm(t, t, 0x0C0C0200u);              // bytes [0, 2] -> [0, 1]
 }
 
@@ -409,7 +425,7 @@ __device__ __forceinline__ u32 G_root(u32 a, u32 b, u32 u, u32 &S)
     const u32 d = pk_sub(ma, mb);
     const u32 x = a ^ u ^ b;
     S = plane_put<I>(S, b ^ (x & ~d));
-    return pk_min(bsel(opaque(pk_sra(x, 15)), pk_abs_i16(d), pk_add(ma, mb)), 0x000F000Fu);
+    return pk_min(bsel(opaque(pk_sra(x, 15)), pk_abs_i16(d), pk_add(ma, mb)), GSAT2);
 }
 // G on split words: X = plane of sign(a') ^ sign(b); returns the clamped magnitude and puts
 // |a| < |b| into LT. The output sign plane is then sign(b) ^ (X & ~LT) per 16 words.
@@ -419,7 +435,7 @@ __device__ __forceinline__ u32 G_split(u32 ma, u32 mb, u32 X, u32 &LT)
     const u32 xm = opaque(plane_mask<I>(X));
     const u32 d = pk_sub(ma, mb);
     LT = plane_put<I>(LT, d);
-    return pk_min(bsel(xm, pk_abs_i16(d), pk_add(ma, mb)), 0x000F000Fu);
+    return pk_min(bsel(xm, pk_abs_i16(d), pk_add(ma, mb)), GSAT2);
 }
 // REP word from split parent words: F value + 512 per half, and its SM16 form
 template <int I>
@@ -455,8 +471,8 @@ __device__ __forceinline__ u32 rep_acc(u32 acc, u32 total_biased)
 {
     u32 t = pk_sub(pk_add(acc, total_biased), 0x20002000u);
     i16x2 v = __builtin_bit_cast(i16x2, t);
-    v = __builtin_elementwise_min(v, (i16x2){511, 511});
-    v = __builtin_elementwise_max(v, (i16x2){-511, -511});
+    v = __builtin_elementwise_min(v, (i16x2){(short)REPSAT, (short)REPSAT});
+    v = __builtin_elementwise_max(v, (i16x2){(short)-(int)REPSAT, (short)-(int)REPSAT});
     return __builtin_bit_cast(u32, v);
 }
 // true if some frame of the wave ended with a zero accumulator

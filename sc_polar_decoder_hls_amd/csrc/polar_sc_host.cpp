@@ -220,16 +220,17 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
     emit(out, left_zero ? POLAR_OP_H0 : POLAR_OP_H, level, (int)h, (int)g0, -1, 0);
 }
 
-// The reference's swept configurations (script/script_tests.sh:103-122) at its shipped
-// arithmetic: PRUNING_LEVEL 0/1/2 with any ELAG_R1/REP/SPC/REP2/SPC2/H0 switches.
-// ELAG_RARE = 1 does not compile in the reference (my_module.h:255 vs :1511); LLR_BITS,
-// PAR, CA2 and EXTENDED = 0 change the arithmetic and are not built yet.
+// The reference's swept configurations (script/script_tests.sh:103-122): PRUNING_LEVEL 0/1/2
+// with any ELAG_R1/REP/SPC/REP2/SPC2/H0 switches, at LLR_BITS 5..8 (the sweep itself runs at
+// QUANT = 8, script_tests.sh:9,25; the channel stays one int8 per LLR). ELAG_RARE = 1 does
+// not compile in the reference (my_module.h:255 vs :1511); PAR, CA2 and EXTENDED = 0 change
+// the datapath and are not built.
 bool config_supported(const polar_sc_config &c)
 {
     polar_sc_config d;
     polar_sc_default_config(&d);
     auto sw = [](int32_t v) { return v == 0 || v == 1; };
-    return c.llr_bits == d.llr_bits && c.par == d.par && c.sigmag == d.sigmag && c.extended == d.extended &&
+    return c.llr_bits >= 5 && c.llr_bits <= 8 && c.par == d.par && c.sigmag == d.sigmag && c.extended == d.extended &&
            c.pruning_level >= 0 && c.pruning_level <= 2 && sw(c.elag_r1) && sw(c.elag_rep) && sw(c.elag_spc) &&
            sw(c.elag_rep2) && sw(c.elag_spc2) && c.elag_rare == 0 && sw(c.elag_h0) && sw(c.strict_llr);
 }
@@ -517,6 +518,12 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         s.n_sub_calls = sc.calls;
     } else {
         dev_sched = p->ops;
+        if (!p->jit && c.llr_bits != 6) {
+            // the hipcc-built interpreter is the shipped LLR_BITS = 6; other widths run the
+            // same interpreter compiled by hipRTC with POLAR_Q (a hybrid kernel without subtrees)
+            p->hybrid = 1;
+            p->hybrid_waves = polar_host::HYBRID_MAX_WAVES;
+        }
     }
     if (p->gmem) window_schedule(*p, dev_sched);
     else if (p->hybrid) p->dev_ops = dev_sched;
@@ -585,9 +592,10 @@ int polar_sc_decode_host(const polar_sc_plan *p, const int8_t *llr, uint64_t *ha
     if (!p || (batch > 0 && (!llr || !hard_bits))) return -EINVAL;
     if (batch == 0) return 0;
     if (p->cfg.strict_llr) {
+        const int lim = (1 << (p->cfg.llr_bits - 1)) - 1;   // quantizer range +-(2^(Q-1) - 1)
         const size_t total = batch * (size_t)p->N;
         for (size_t i = 0; i < total; i++)
-            if (llr[i] > 31 || llr[i] < -31) return -EINVAL;
+            if (llr[i] > lim || llr[i] < -lim) return -EINVAL;
     }
     // chunks of at most ~256 MB of LLRs through device buffers cached in the plan (one host
     // decode per plan at a time: the buffers are shared)

@@ -198,7 +198,7 @@ __device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int
             for (int j = 0; j < CH; j++) {
                 const int q = upos + i + j;
                 const uint32_t u = (upos >= 0) ? ubit(((q >> 4) == ((upos + i) >> 4)) ? u0 : u1, q) : 0u;
-                r[j] = G_sm<15>(a[j], b[j], u);
+                r[j] = G_sm<GSAT>(a[j], b[j], u);
             }
         } else {
 #pragma unroll
@@ -212,7 +212,7 @@ __device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int
         uint32_t r;
         if constexpr (ISG) {
             const uint32_t u = (upos >= 0) ? ubit(c.bld((upos + i) >> 4), upos + i) : 0u;
-            r = G_sm<15>(a, b, u);
+            r = G_sm<GSAT>(a, b, u);
         } else {
             r = F_sm(a, b);
         }
@@ -248,7 +248,7 @@ __device__ __forceinline__ void op_leaf(const C &c, int k, int pos, int upos, ui
     uint32_t L;
     if constexpr (ISG) {
         uint32_t u = (upos >= 0) ? ubit(c.bld(upos >> 4), upos) : 0u;
-        L = G_sm<15>(a, b, u);
+        L = G_sm<GSAT>(a, b, u);
     } else {
         L = F_sm(a, b);
     }
@@ -298,7 +298,7 @@ __device__ __forceinline__ void rep_body(const C &c, int s0, int n, int pos)
         for (i = 0; i < n; i++) {
             uint32_t lam = F_sm(c.template ldx<L>(s0 + i), c.template ldx<L>(s0 + n + i));
             uint32_t t = row_add_tree(lam, c.ln);
-            acc = G_sm<511>(t, acc, 0u);
+            acc = G_sm<REPSAT>(t, acc, 0u);
         }
     }
     // two's complement or SM16: the decision is bit 15 / 31 either way
@@ -334,15 +334,15 @@ __device__ __forceinline__ void r1spc_body(const C &c, int s0, int n, int upos, 
             if (((upos + i) & 15) == 0 || i == i0) ud = c.bld((upos + i) >> 4);
             u = ubit(ud, upos + i);
         }
-        uint32_t lam = G_sm<15>(a, b, u);
+        uint32_t lam = G_sm<GSAT>(a, b, u);
         uint32_t h = lam & SGN;
         int q = (pos + i) & 15;
         acc |= h >> (15 - q);
         if (n >= 16 && q == 15) { c.bst((pos + i) >> 4, acc); acc = 0; }
         if constexpr (SPC) {
             par ^= h;
-            uint32_t klo = ((lam & 0x1Fu) << 24) | ((uint32_t)i << 4);
-            uint32_t khi = (((lam >> 16) & 0x1Fu) << 24) | ((uint32_t)i << 4);
+            uint32_t klo = ((lam & QMAG) << 24) | ((uint32_t)i << 4);
+            uint32_t khi = (((lam >> 16) & QMAG) << 24) | ((uint32_t)i << 4);
             key_lo = __builtin_elementwise_min(key_lo, klo);
             key_hi = __builtin_elementwise_min(key_hi, khi);
         }

@@ -213,7 +213,7 @@ struct Gen {
                 } else {
                     o << "    u32 c_; ";
                     ucache(op.upos, 0);
-                    o << "    const u32 L_ = G_sm<15>(CH(0), CH(1), " << uflag(0) << ");\n"
+                    o << "    const u32 L_ = G_sm<GSAT>(CH(0), CH(1), " << uflag(0) << ");\n"
                       << "    const u32 M_ = L_ & MAG, S_ = pk_sra(L_, 15);\n";
                 }
             } else if (f) {
@@ -224,7 +224,7 @@ struct Gen {
                   << "));\n"
                   << "    const u32 d_ = pk_sub(" << M(sd, 0) << ", " << M(sd, 1) << ");\n"
                   << "    const u32 M_ = pk_min(bsel(xm_, pk_abs_i16(d_), pk_add(" << M(sd, 0) << ", " << M(sd, 1)
-                  << ")), 0x000F000Fu);\n"
+                  << ")), GSAT2);\n"
                   << "    const u32 S_ = plane_mask<0>(" << P(sd, 1) << ") ^ (xm_ & ~pk_sra(d_, 15));\n";
             }
             o << "    const u32 x_ = leaf_ms<0x" << std::hex << op.fb << std::dec << "u, 0, 16>(M_, S_, ln);\n";
@@ -245,7 +245,7 @@ struct Gen {
             }
             o << "    if (rep_any_zero(acc_)) {\n      acc_ = 0u;\n";
             for (int i = 0; i < n; i++)
-                o << "      acc_ = G_sm<511>(row_add_tree(F_split_sm<" << i % 16 << ">(" << M(sd, i) << ", " << M(sd, n + i)
+                o << "      acc_ = G_sm<REPSAT>(row_add_tree(F_split_sm<" << i % 16 << ">(" << M(sd, i) << ", " << M(sd, n + i)
                   << ", FS_[" << i / 16 << "]), ln), acc_, 0u);\n";
             // two's complement or SM16: the hard decision is bit 15 / 31 either way
             o << "    }\n    full_ = pk_sra(acc_, 15);\n";
@@ -375,7 +375,8 @@ struct Gen {
         // once for the root G. Frame stride N + 16 bytes keeps the four rows of a read in
         // different banks.
         const int FS = N + 16, chunks = N / 2;   // 16-byte chunks per wave
-        o << "#define POLAR_LANE_REMAP 1\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
+        o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
+          << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
           << "#define CH(w) sm8_pair(tab_[chl[16 * (w)]], tab_[chh[16 * (w)]])\n"
           << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
@@ -432,7 +433,8 @@ std::string hybrid_source(const polar_sc_plan &p)
 {
     std::ostringstream o;
     const bool gm = p.gmem != 0;
-    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_SC_SUBS 1\n#include \"polar_sc_interp.h\"\n"
+    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_SC_SUBS 1\n#define POLAR_Q " << p.cfg.llr_bits
+      << "\n#include \"polar_sc_interp.h\"\n"
       << "namespace polar {\n#define CH(w) cin_[(w) * 64]\n";
     int lg = 0;
     while ((1 << lg) < p.sub_words) lg++;

@@ -154,7 +154,7 @@ def test_sweep_configs_change_results(pkg, oracle_mod):
 
 def test_unsupported_configs(pkg):
     mask = util.mask("FB_N128_K64")
-    for field, val in (("elag_rare", 1), ("llr_bits", 8), ("par", 64), ("sigmag", 0), ("pruning_level", 3)):
+    for field, val in (("elag_rare", 1), ("llr_bits", 9), ("llr_bits", 4), ("par", 64), ("sigmag", 0), ("pruning_level", 3)):
         c = pkg.default_config()
         setattr(c, field, val)
         with pytest.raises(pkg.PolarError):
