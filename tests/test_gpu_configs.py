@@ -54,3 +54,27 @@ def test_sweep_configs_planted_groups(pkg, cuda, oracle_mod):
         for c7 in oracle_mod.SWEEP_CONFIGS + EXTRA:
             got, kernel = _run(pkg, cuda, mask, llr, c7)
             _assert_same(got, oracle_mod.decode_fsm(mask, llr, config=c7), "N=%d %s kernel %d" % (N, c7, kernel))
+
+
+@pytest.mark.parametrize("q", [5, 7, 8])
+def test_llr_bits_configs(pkg, cuda, oracle_mod, q):
+    """LLR_BITS other than the shipped 6 (config.h:2; the reference's pruning sweep runs at
+    QUANT = 8, script/script_tests.sh:9,25): the per-mask kernel, the hybrid kernel and the
+    hipRTC-compiled interpreter (PRUNING_LEVEL 1 leaf decoders) against the oracle at the same
+    LLR_BITS, on AWGN frames at that quantisation and on the whole int8 range."""
+    rng = np.random.default_rng(50 + q)
+    amp = (1 << (q - 1)) - 1
+    for name in ("FB_N128_K64", "FB_N1024_K512", "frozen_n_4096_k_2048"):
+        mask = util.mask(name)
+        awgn, _ = util.synth_frames(mask, 12, ebn0_db=1.5, seed=q)
+        awgn = np.clip(awgn.astype(np.int32) * (1 << q) // 64, -amp, amp)
+        llr = np.concatenate([awgn, rng.integers(-128, 128, size=(7, mask.size))]).astype(np.int8)
+        for c7 in (oracle_mod.DEFAULT_CONFIG, (1, 1, 1, 1, 1, 1, 0)):
+            c = _cfg(pkg, c7)
+            c.llr_bits = q
+            dec = pkg.Decoder(mask, config=c)
+            out = dec.decode(cuda.from_numpy(llr).cuda())
+            cuda.cuda.synchronize()
+            got = pkg.unpack_bits(out.cpu().numpy(), mask.size)
+            _assert_same(got, oracle_mod.decode_fsm(mask, llr, config=c7, llr_bits=q),
+                         "%s q=%d %s kernel %d" % (name, q, c7, dec.stats["kernel"]))

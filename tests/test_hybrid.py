@@ -69,6 +69,20 @@ def test_hybrid_source_compiles(pkg, sub_words):
     dec.compile()   # hipRTC for gfx950 on the host
 
 
+@pytest.mark.parametrize("q", [5, 8])
+def test_llr_bits_kernels_compile(pkg, q):
+    """LLR_BITS 5..8 plans are specialised through POLAR_Q in the hipRTC kernels: the per-mask
+    kernel (N <= 1024), the hybrid kernel (N > 1024) and, for plans that would use the hipcc
+    interpreter (PRUNING_LEVEL 1 leaf decoders), the interpreter compiled by hipRTC."""
+    for name, pr, kernel in (("FB_N1024_K512", 2, 1), ("frozen_n_4096_k_2048", 2, 2), ("FB_N1024_K512", 1, 2)):
+        c = pkg.default_config()
+        c.llr_bits, c.pruning_level = q, pr
+        dec = pkg.Decoder(util.mask(name), config=c)
+        assert dec.stats["kernel"] == kernel, (name, pr)
+        assert "#define POLAR_Q %d" % q in dec.kernel_source()
+        dec.compile()
+
+
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sub_words", [2, 4, 8, 16, 32, 64])

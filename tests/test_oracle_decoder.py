@@ -99,3 +99,26 @@ def test_restatement_reproduces_committed_vectors(oracle_mod, case):
     """The oracle still decodes the committed regression vectors to the committed x^."""
     name, llr, x = util.decode_vectors()[case]
     np.testing.assert_array_equal(oracle_mod.decode_fsm(util.mask(name), llr), x, err_msg=case)
+
+
+@pytest.mark.parametrize("q", [5, 7, 8])
+def test_fsm_equals_recursive_other_llr_bits(oracle_mod, q):
+    """LLR_BITS 5..8 (config.h:2; the reference's pruning sweep runs at QUANT = 8,
+    script/script_tests.sh:9,25): both restatements agree on the whole int8 range (the low
+    q bits are the LLR), noiseless frames decode, and q = 6 through the switch is the default."""
+    rng = np.random.default_rng(70 + q)
+    for trial in range(60):
+        N = int(2 ** rng.integers(5, 11))
+        mask = _random_mask(rng, N, trial % 4)
+        llr = rng.integers(-128, 128, size=(5, N)).astype(np.int8)
+        np.testing.assert_array_equal(oracle_mod.decode_fsm(mask, llr, llr_bits=q),
+                                      oracle_mod.decode_rec(mask, llr, llr_bits=q), err_msg="trial %d" % trial)
+    mask = util.mask("FB_N1024_K512")
+    x = np.array(util.kat()["cw1024x512"], dtype=np.uint8)
+    amp = (1 << (q - 1)) - 1
+    np.testing.assert_array_equal(oracle_mod.decode_fsm(mask, np.where(x == 1, -amp, amp).astype(np.int8),
+                                                        llr_bits=q), x)
+    llr, _ = util.synth_frames(mask, 6, ebn0_db=1.0, seed=5)
+    np.testing.assert_array_equal(oracle_mod.decode_fsm(mask, llr, llr_bits=6), oracle_mod.decode_fsm(mask, llr))
+    with pytest.raises(ValueError):
+        oracle_mod.decode_fsm(mask, llr, llr_bits=9)
