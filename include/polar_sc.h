@@ -35,9 +35,10 @@ extern "C" {
  * src/module/config.h:2-30 (+ PAR from polar_parameters.h:8). The default
  * (polar_sc_default_config) is the configuration the reference ships. Also accepted: the
  * pruning sweep of script/script_tests.sh:103-122, i.e. pruning_level 0/1/2 with any
- * combination of elag_r1 / elag_rep / elag_spc / elag_rep2 / elag_spc2 / elag_h0.
- * elag_rare = 1 (does not compile in the reference, my_module.h:255 vs :1511) and any other
- * llr_bits / par / sigmag / extended are rejected with -ENOTSUP in this version.
+ * combination of elag_r1 / elag_rep / elag_spc / elag_rep2 / elag_spc2 / elag_h0, at
+ * llr_bits 5..8 (the sweep itself runs at QUANT = 8, script_tests.sh:9,25; the LLR is the low
+ * llr_bits of each int8). elag_rare = 1 (does not compile in the reference, my_module.h:255
+ * vs :1511) and any other par / sigmag / extended are rejected with -ENOTSUP.
  */
 typedef struct polar_sc_config {
     int32_t llr_bits;       /* LLR_BITS            (config.h:2)      default 6  */
@@ -52,10 +53,10 @@ typedef struct polar_sc_config {
     int32_t elag_spc2;      /* ELAG_SPC2           (config.h:23)     default 0  */
     int32_t elag_rare;      /* ELAG_RARE           (config.h:26)     default 0  */
     int32_t elag_h0;        /* ELAG_H0             (config.h:28)     default 1  */
-    int32_t strict_llr;     /* 0: LLRs are taken modulo 2^6 like the reference's
-                               sc_bigint<6> LLR (config.h:6); 1: polar_sc_decode_host
-                               rejects |llr| > 31 with -EINVAL (the device entry point
-                               never validates).                           default 0 */
+    int32_t strict_llr;     /* 0: LLRs are taken modulo 2^llr_bits like the reference's
+                               sc_bigint<LLR_BITS> LLR (config.h:6); 1: polar_sc_decode_host
+                               rejects |llr| > 2^(llr_bits-1) - 1 with -EINVAL (the device
+                               entry point never validates).               default 0 */
 } polar_sc_config;
 
 /* Immutable decode plan: N, config, frozen mask, compiled decode schedule and its device

@@ -206,7 +206,7 @@ __device__ __forceinline__ u32 leaf_rec(u32 L, u32 fb, u32 fbm, const Lanes &ln)
 
 __device__ __forceinline__ u32 leaf16(u32 L, u32 fb, const Lanes &ln)
 {
-    u32 fbm = ((fb >> ln.pl) & 1u) ? SGN : 0u;
+    u32 fbm = ((fb >> ln.pos) & 1u) ? SGN : 0u;   // the frozen bit of this lane's word position
     return leaf_rec<0, 16>(L, fb, fbm, ln);
 }
 

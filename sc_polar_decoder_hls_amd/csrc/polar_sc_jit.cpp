@@ -35,6 +35,9 @@ struct Gen {
     const std::vector<polar_sc_op> &ops;   // schedule of the code (or subtree) of 16 * 2^LG LLRs
     std::ostringstream o;
     int LG;
+    // per-mask kernels: the channel words are split once (root_presplit) into m<LG> / s<LG>,
+    // so the root ops run on split words like every other level
+    bool presplit = false;
     Gen(const std::vector<polar_sc_op> &ops_, int lg) : ops(ops_), LG(lg) {}
 
     // Partial sums: u32 bw[max(1, G / 16)], dword j = groups 16 j .. 16 j + 15, low frame in
@@ -109,7 +112,7 @@ struct Gen {
     // registers held across the whole left subtree.
     void clobber_parent(int sd, int n)
     {
-        if (sd == LG) return;   // root: channel words are re-read from LDS
+        if (sd == LG && !presplit) return;   // root: channel words are re-read from LDS
         for (int i = 0; i < 2 * n; i++) o << "  asm volatile(\"\" : \"+v\"(" << M(sd, i) << "));\n";
         for (int k = 0; k < planes(2 * n); k++) o << "  asm volatile(\"\" : \"+v\"(s" << sd << "[" << k << "]));\n";
     }
@@ -150,10 +153,27 @@ struct Gen {
         }
     }
 
+    // Per-mask kernels: wrapper_in + qconv_format (wrapper_in.h:26-44, scalar.h:229-239) once
+    // per frame. Every channel word becomes a magnitude pair m<LG>[w] and a bit of the sign
+    // plane s<LG>[w / 16] (two LDS tables give |LLR| and the sign of a channel byte), so the
+    // root F / G are the split-word ops of every other level (F: 1 VALU per word instead of
+    // 10, G: 10 instead of 18) for a conversion of about 3 VALU per word.
+    void root_presplit(int words)
+    {
+        for (int k = 0; k < planes(words); k++) o << "  s" << LG << "[" << k << "] = 0u;\n";
+        for (int i = 0; i < words; i++) {
+            o << "  { const u32 bl_ = chl[" << 16 * i << "], bh_ = chh[" << 16 * i << "];\n"
+              << "    " << M(LG, i) << " = (u32)tabm_[bl_] | ((u32)tabm_[bh_] << 16);\n"
+              << "    s" << LG << "[" << i / 16 << "] |= ((u32)tabs_[bl_] | ((u32)tabs_[bh_] << 16)) << " << i % 16
+              << "; }\n";
+            chunk_fence(i, words);
+        }
+    }
+
     void op(const polar_sc_op &op)
     {
         const int sd = LG - op.level, cd = sd - 1, n = op.n, np = planes(n);
-        const bool root = sd == LG;
+        const bool root = sd == LG && !presplit;
         fence();
         if (root && (op.code == POLAR_OP_REP || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC)) root_split(2 * n);
         switch (op.code) {
@@ -371,18 +391,18 @@ struct Gen {
         const int N = (int)p.N, G = (int)p.G;
         // Channel staging: each wave copies its 8 frames (8 x N bytes, contiguous rows of the
         // [batch][N] input) into LDS with 16-byte loads, then reads the bytes of its lane
-        // (position 16 w + pl of frames row / row + 4) from there, once for the root F and
-        // once for the root G. Frame stride N + 16 bytes keeps the four rows of a read in
+        // (position 16 w + pl of frames row / row + 4) from there once, into the split root
+        // words (root_presplit). Frame stride N + 16 bytes keeps the four rows of a read in
         // different banks.
         const int FS = N + 16, chunks = N / 2;   // 16-byte chunks per wave
         o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
           << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
-          << "#define CH(w) sm8_pair(tab_[chl[16 * (w)]], tab_[chh[16 * (w)]])\n"
           << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
           << "  __shared__ uint4 stage_[4 * 8 * " << FS / 16 << "];\n"
-          << "  __shared__ unsigned char tab_[256];   // channel byte -> SM8\n"
-          << "  tab_[threadIdx.x] = (unsigned char)sm8_of_byte(threadIdx.x);\n"
+          << "  __shared__ unsigned char tabm_[256], tabs_[256];   // channel byte -> |LLR|, sign (qconv_format)\n"
+          << "  { const u32 v_ = sm8_of_byte(threadIdx.x); tabm_[threadIdx.x] = (unsigned char)(v_ & QMAG);\n"
+          << "    tabs_[threadIdx.x] = (unsigned char)(v_ >> 7); }\n"
           << "  __syncthreads();\n"
           << "  const int lane = threadIdx.x & 63, row = lane >> 4, pl = lane & 15, wib = threadIdx.x >> 6;\n"
           << "  const long wave = (long)blockIdx.x * 4 + wib;\n"
@@ -409,7 +429,9 @@ struct Gen {
           << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
           << " + ln.pos;\n"
           << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
-        stage_arrays(false);
+        stage_arrays(true);
+        presplit = true;
+        root_presplit(G);
         all_ops();
         // END (my_module.h:1848-1869) + wrapper_out: x^ words in natural order
         o << "  const bool st_lo = f_lo < batch, st_hi = f_hi < batch;\n"
