@@ -31,7 +31,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # PMC summary (tools/profile_gpu.sh + tools/pmc_summary.py) of the current C2 kernel: the
 # HBM bytes it reports (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
 # roofline.traffic when the benchmarked configuration is the profiled one.
-TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r01_v7_pmc.json")
+TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r01_v9_pmc.json")
 # VALU issue cost on gfx950 measured by tools/valu_microbench.hip (profiles/
 # r01_valu_microbench.log): 4.2-4.7 cycles per wave64 instruction for the packed-16 / logic /
 # DPP classes the decoder issues (8 waves per SIMD, independent chains)
