@@ -28,16 +28,22 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# PMC summary (tools/profile_gpu.sh + tools/pmc_summary.py) of the current C2 kernel: the
-# HBM bytes it reports (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
-# roofline.traffic when the benchmarked configuration is the profiled one.
-TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r01_v9_pmc.json")
+# PMC summaries (tools/profile_gpu.sh + tools/pmc_summary.py) of the current kernels: the HBM
+# bytes they report (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
+# roofline.traffic when the benchmarked (mask, frames per GPU) is the profiled one.
+TRAFFIC_PROFILES = {
+    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r01_v9_pmc.json"),
+}
+# Rotated input: the timed loop cycles through distinct resident batches of at least this
+# many bytes in total, so the LLR reads come from HBM and not from the 256 MB Infinity Cache
+# (MI355X_MICROARCH.md) that would hold one C2 batch (67 MB).
+ROTATE_BYTES = 300 << 20
+EBN0_SWEEP = (1.0, 2.5, 4.0)   # throughput depends weakly on the SNR
 # VALU issue cost on gfx950 measured by tools/valu_microbench.hip (profiles/
 # r01_valu_microbench.log): 4.2-4.7 cycles per wave64 instruction for the packed-16 / logic /
 # DPP classes the decoder issues (8 waves per SIMD, independent chains)
 VALU_CYCLES_PER_INST = 4.4
 NOMINAL_CLOCK_GHZ = 2.4
-TRAFFIC_PROFILE_CONFIG = ("FB_N1024_K512", 65536)
 
 CONFIGS = {
     # name: (mask fixture, per-GPU frames at N=1 semantics, description)
@@ -81,10 +87,22 @@ def gen_frames_torch(torch, mask, batch, ebn0_db, seed, device):
     return llr, x
 
 
-def cpu_baseline(mask, seconds, ebn0_db, threads=None):
-    """Time the CPU oracle (literal FSM restatement) on a bounded sample of the workload:
-    first one thread, then `threads` threads over disjoint frame chunks (the ctypes call
-    releases the GIL). Returns the multi-thread figure with the single-thread one beside it."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(mask, seconds, ebn0_db, threads=None, runs=5):
+    """Time the CPU oracle (literal FSM restatement) on a bounded sample of the workload
+    (runs of >= 1 s, median of 5): one thread, then `threads` threads over
+    disjoint frame chunks (the ctypes call releases the GIL). Returns the multi-thread median
+    with the single-thread one beside it."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle
     import util
@@ -96,6 +114,7 @@ def cpu_baseline(mask, seconds, ebn0_db, threads=None):
     sample = max(8, min(4096, int(2 ** 22 // N)))
     llr, _ = util.synth_frames(mask, sample, ebn0_db=ebn0_db, seed=0xF0)
     oracle.decode_fsm(mask, llr[:2])   # warm
+    per_run = max(1.0, seconds / (2 * runs))
 
     def timed(fn, budget):
         frames, t0 = 0, time.perf_counter()
@@ -103,20 +122,71 @@ def cpu_baseline(mask, seconds, ebn0_db, threads=None):
             frames += fn()
             el = time.perf_counter() - t0
             if el >= budget:
-                return frames / el, el
+                return frames / el
 
-    fps1, el1 = timed(lambda: (oracle.decode_fsm(mask, llr), sample)[1], seconds / 2)
+    fps1 = [timed(lambda: (oracle.decode_fsm(mask, llr), sample)[1], per_run) for _ in range(runs)]
     chunks = np.array_split(llr, threads)
     with ThreadPoolExecutor(threads) as ex:
         def all_threads():
             list(ex.map(lambda c: oracle.decode_fsm(mask, c), chunks))
             return sample
-        fpsn, eln = timed(all_threads, seconds / 2)
-    return {"value": fpsn * K, "unit": "info_bits/s", "frames_per_sec": fpsn, "cores": threads,
-            "kind": "port", "value_1thread": fps1 * K,
+        fpsn = [timed(all_threads, per_run) for _ in range(runs)]
+    med1, medn = float(np.median(fps1)), float(np.median(fpsn))
+    return {"value": medn * K, "unit": "info_bits/s", "frames_per_sec": medn, "cores": threads,
+            "kind": "port", "value_1thread": med1 * K, "runs": runs, "run_seconds": per_run,
+            "values_nthreads": [v * K for v in fpsn], "values_1thread": [v * K for v in fps1],
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(),
             "sample": "%d frames (N=%d K=%d, Eb/N0=%.1f dB) decoded repeatedly by oracle/polar_oracle.c "
-                      "orc_decode_fsm (literal my_module FSM): %.1f s on 1 thread, then %.1f s on %d threads "
-                      "(frame chunks)" % (sample, N, K, ebn0_db, el1, eln, threads)}
+                      "orc_decode_fsm (literal my_module FSM): median of %d runs of %.1f s on 1 thread, then on "
+                      "%d threads (frame chunks)" % (sample, N, K, ebn0_db, runs, per_run, threads)}
+
+
+def make_batches(pkg, torch, args, mask, per_gpu, frame0, stride, dev, ebn0, nb):
+    """nb distinct resident batches of per_gpu frames (batch b: frames frame0 + b * stride ...
+    of the testbench's frame stream, stride = frames of all ranks; or torch AWGN):
+    [(llr, xref or None, x or None)]"""
+    N, K = mask.size, int(mask.sum())
+    out = []
+    for b in range(nb):
+        if args.data == "csim":
+            kat_key = {8: "cw8x4", 512: "cw512x256", 1024: "cw1024x512"}.get(N)
+            import util
+            cws = np.array(util.kat()[kat_key], dtype=np.uint8) if kat_key else None
+            llr, xref = pkg.csim_frames(N, per_gpu, pkg.csim_sigma(ebn0, K / N), seed=0xF0,
+                                        frame0=frame0 + b * stride, codewords=cws, device=dev)
+            out.append((llr, xref, None))
+        else:
+            from sc_polar_decoder_hls_amd import sharding
+            rank = int(os.environ.get("RANK", "0"))
+            llr, x = gen_frames_torch(torch, mask, per_gpu, ebn0, sharding.frame_seed(0xF0 + 104729 * b, rank), dev)
+            out.append((llr, None, x))
+    return out
+
+
+def timed_decodes(torch, sharding, dist, coll_dev, dec, batches, outs, steps, warmup, stream):
+    """Warm-up, then `steps` back-to-back decode launches on one stream cycling through the
+    resident batches, bracketed by a barrier + synchronize and by one HIP event pair on the
+    launch stream (per-step event records would add ~5 us of stream markers to every step).
+    Returns (wall seconds, mean ms per launch from the events), both max over ranks."""
+    nb = len(batches)
+    for i in range(warmup):
+        dec.decode(batches[i % nb][0], outs[i % nb], stream)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(steps):
+        dec.decode(batches[i % nb][0], outs[i % nb], stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / steps
+    return sharding.max_over_ranks([elapsed, kern_ms], dist, coll_dev)
 
 
 def time_scatter_gather(torch, pkg, sharding, dist, dec, mask, total, rank, dev, cdev, args):
@@ -171,6 +241,11 @@ def main():
     ap.add_argument("--host-io", action="store_true",
                     help="also time polar_sc_decode_host (PCIe-inclusive, host buffers) on the batch")
     ap.add_argument("--check", type=int, default=64, help="frames checked vs the oracle (rank 0)")
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="distinct resident input batches cycled through by the timed loop (0: enough for "
+                         "%d MB, so the inputs do not sit in the Infinity Cache)" % (ROTATE_BYTES >> 20))
+    ap.add_argument("--no-ebn0-sweep", dest="ebn0_sweep", action="store_false",
+                    help="skip the Eb/N0 {1, 2.5, 4} dB sweep of the timed loop")
     ap.add_argument("--io", choices=["resident", "scatter"], default="resident",
                     help="scatter: also time the C4 flow -- rank 0 holds the whole batch in HBM, "
                          "RCCL scatters the LLR shards, every rank decodes, RCCL gathers x^ to rank 0 "
@@ -217,51 +292,22 @@ def main():
 
     dec = pkg.Decoder(mask)
     dec.prepare(per_gpu)
-    xref = None
-    if args.data == "csim":
-        kat_key = {8: "cw8x4", 512: "cw512x256", 1024: "cw1024x512"}.get(N)
-        cws = np.array(util.kat()[kat_key], dtype=np.uint8) if kat_key else None
-        sigma = pkg.csim_sigma(args.ebn0, K / N)
-        # frames of this rank: the next per_gpu frames of the testbench's single stream
-        counts = [per_gpu]
-        if dist is not None:
-            t = torch.zeros(world, dtype=torch.float64, device=coll_dev)
-            t[rank] = per_gpu
-            dist.all_reduce(t)
-            counts = [int(v) for v in t.tolist()]
-        frame0 = int(sum(counts[:rank]))
-        llr, xref = pkg.csim_frames(N, per_gpu, sigma, seed=0xF0, frame0=frame0, codewords=cws, device=dev)
-        x = None
-    else:
-        llr, x = gen_frames_torch(torch, mask, per_gpu, args.ebn0, sharding.frame_seed(0xF0, rank), dev)
-    out = torch.empty((per_gpu, dec.words), dtype=torch.int64, device=dev)
+    # frames of this rank: the next per_gpu frames of the testbench's single stream
+    counts = [per_gpu]
+    if dist is not None:
+        t = torch.zeros(world, dtype=torch.float64, device=coll_dev)
+        t[rank] = per_gpu
+        dist.all_reduce(t)
+        counts = [int(v) for v in t.tolist()]
+    frame0 = int(sum(counts[:rank]))
+    nb = args.rotate if args.rotate > 0 else max(1, min(8, -(-ROTATE_BYTES // (per_gpu * N))))
+    batches = make_batches(pkg, torch, args, mask, per_gpu, frame0, sum(counts), dev, args.ebn0, nb)
+    outs = [torch.empty((per_gpu, dec.words), dtype=torch.int64, device=dev) for _ in range(nb)]
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        dec.decode(llr, out, stream)
-    torch.cuda.synchronize()
-
-    # timed region: back-to-back decode launches on one stream, bracketed by a barrier +
-    # synchronize and by one HIP event pair on the launch stream (per-step event records
-    # would add ~5 us of stream markers to every step). kern_ms = event time / steps is
-    # the average launch duration over the timed region (kernel + inter-launch gap).
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        dec.decode(llr, out, stream)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    elapsed, kern_ms = sharding.max_over_ranks([elapsed, kern_ms], dist, coll_dev)
+    elapsed, kern_ms = timed_decodes(torch, sharding, dist, coll_dev, dec, batches, outs, args.steps, args.warmup,
+                                     stream)
     if dist is not None:   # frames decoded by all ranks (shards may differ by a few frames)
         cnt = torch.tensor([per_gpu], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(cnt)
@@ -272,6 +318,28 @@ def main():
     total_frames = frames_all * args.steps
     fps = total_frames / elapsed
     value = fps * K
+    # the last launch of the timed loop decoded batch (steps - 1) % nb into its output
+    last = (args.steps - 1) % nb
+    llr, xref, x = batches[last]
+    out = outs[last]
+
+    # Eb/N0 sweep: the same timed loop on frames at each SNR
+    sweep = None
+    if args.ebn0_sweep:
+        sweep = []
+        for e in EBN0_SWEEP:
+            bs = make_batches(pkg, torch, args, mask, per_gpu, frame0, sum(counts), dev, e, nb)
+            el, km = timed_decodes(torch, sharding, dist, coll_dev, dec, bs, outs, max(1, args.steps // 2),
+                                   max(1, args.warmup // 4), stream)
+            ent = {"ebn0_db": e, "value": frames_all * max(1, args.steps // 2) / el * K,
+                   "ms_per_step": el / max(1, args.steps // 2) * 1e3, "kernel_ms": km}
+            if bs[0][1] is not None:
+                cnt = pkg.count_errors(outs[(max(1, args.steps // 2) - 1) % nb], bs[(max(1, args.steps // 2) - 1) % nb][1], N)
+                torch.cuda.synchronize()
+                ent["frame_error_rate"] = float(cnt[1].item()) / per_gpu
+            sweep.append(ent)
+            del bs
+        torch.cuda.synchronize()
 
     scatter_res = None
     if args.io == "scatter" and dist is not None:
@@ -305,12 +373,13 @@ def main():
         bytes_per_launch = 1.125 * N * per_gpu
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src, valu = None, None, None
-        if (name, per_gpu) == TRAFFIC_PROFILE_CONFIG and os.path.exists(TRAFFIC_PROFILE):
-            with open(TRAFFIC_PROFILE) as f:
+        prof_path = TRAFFIC_PROFILES.get((name, per_gpu))
+        if prof_path and os.path.exists(prof_path):
+            with open(prof_path) as f:
                 prof = json.load(f)
             if "hbm_read_bytes_corrected" in prof and "hbm_write_bytes" in prof:
                 traffic = prof["hbm_read_bytes_corrected"] + prof["hbm_write_bytes"]
-                traffic_src = os.path.relpath(TRAFFIC_PROFILE, ROOT)
+                traffic_src = os.path.relpath(prof_path, ROOT)
             if "valu_insts_per_wave" in prof:
                 # supplementary: the bound that actually limits this kernel
                 simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
@@ -322,7 +391,7 @@ def main():
                         "peak_basis": "%d SIMDs x %.1f GHz / %.1f cycles per wave64 VALU instruction "
                                       "(profiles/r01_valu_microbench.log)" % (simds, NOMINAL_CLOCK_GHZ,
                                                                              VALU_CYCLES_PER_INST),
-                        "source": os.path.relpath(TRAFFIC_PROFILE, ROOT)}
+                        "source": os.path.relpath(prof_path, ROOT)}
         res = {
             "metric": "decoded info bits/sec + frames/sec, N=1024 K=512 batch, 1/2/4/8 MI355X",
             "value": value,
@@ -341,7 +410,8 @@ def main():
                       "synthetic AWGN frames generated on-device (random info bits, BPSK, Eb/N0=%.1f dB, "
                       "4x quantizer, +-31)") % args.ebn0),
             "config": {"workload": desc, "N": N, "K": K, "frames_per_gpu": per_gpu,
-                       "mask": name, "parallelism": "frames sharded, dp%d" % world},
+                       "mask": name, "parallelism": "frames sharded, dp%d" % world,
+                       "rotated_batches": nb, "rotated_bytes": nb * per_gpu * N},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                          "traffic_source": traffic_src,
@@ -349,6 +419,7 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "valu_roofline": valu,
             "scatter_gather": scatter_res,
+            "ebn0_sweep": sweep,
             "frame_error_rate": fer,
             "bit_error_rate": ber,
             "parity_check": check,

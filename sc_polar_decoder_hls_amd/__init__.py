@@ -314,50 +314,65 @@ class Decoder:
         _check("polar_sc_plan_prepare", lib().polar_sc_plan_prepare(self._plan, int(max_batch)))
 
     # -- e -> s ports -----------------------------------------------------------------------
-    def decode(self, llr, out=None, stream=None):
-        """Decode frames resident on the GPU.
-
-        llr: torch.int8 CUDA tensor [B, N] (contiguous). Returns (or fills `out`) a torch.int64
-        CUDA tensor [B, ceil(N/64)] whose bits are x^ (bit i of word j = x^[64j+i]).
-        Asynchronous on `stream` (default: torch's current stream).
-        """
+    def _check_llr(self, llr):
         torch = _torch()
         if not (isinstance(llr, torch.Tensor) and llr.is_cuda and llr.dtype == torch.int8):
             raise TypeError("llr must be a CUDA int8 tensor")
         if llr.dim() != 2 or llr.shape[1] != self.N or not llr.is_contiguous():
             raise ValueError("llr must be contiguous [B, %d]" % self.N)
+        return torch
+
+    @staticmethod
+    def _check_out(out, llr, shape, dtype):
+        torch = _torch()
+        if not isinstance(out, torch.Tensor) or tuple(out.shape) != tuple(shape) or out.dtype != dtype \
+                or not out.is_contiguous():
+            raise ValueError("out must be a contiguous %s tensor %s" % (dtype, list(shape)))
+        if out.device != llr.device:
+            raise ValueError("out must be on the device of llr (%s), not %s" % (llr.device, out.device))
+
+    def decode(self, llr, out=None, stream=None):
+        """Decode frames resident on the GPU.
+
+        llr: torch.int8 CUDA tensor [B, N] (contiguous). Returns (or fills `out`) a torch.int64
+        CUDA tensor [B, ceil(N/64)] whose bits are x^ (bit i of word j = x^[64j+i]).
+        Asynchronous on `stream` (default: torch's current stream of llr's device).
+        """
+        torch = self._check_llr(llr)
         B = llr.shape[0]
         if out is None:
             out = torch.empty((B, self.words), dtype=torch.int64, device=llr.device)
-        elif out.shape != (B, self.words) or out.dtype != torch.int64 or not out.is_contiguous():
-            raise ValueError("out must be contiguous int64 [B, %d]" % self.words)
-        s = stream if stream is not None else torch.cuda.current_stream(llr.device)
-        _check("polar_sc_decode", lib().polar_sc_decode(
-            self._plan, ctypes.c_void_p(llr.data_ptr()), ctypes.c_void_p(out.data_ptr()), B,
-            ctypes.c_void_p(s.cuda_stream)))
+        else:
+            self._check_out(out, llr, (B, self.words), torch.int64)
+        # the C side picks the code objects / scratch of the current HIP device
+        with torch.cuda.device(llr.device):
+            s = stream if stream is not None else torch.cuda.current_stream(llr.device)
+            _check("polar_sc_decode", lib().polar_sc_decode(
+                self._plan, ctypes.c_void_p(llr.data_ptr()), ctypes.c_void_p(out.data_ptr()), B,
+                ctypes.c_void_p(s.cuda_stream)))
         return out
 
     def trace(self, llr, out=None):
         """Per-op monitor: decode `llr` (as decode(), synchronously) with the instrumented
         kernel and return (records, info). records: one dict per device op (op, level, n, pos,
         nodeN = LLRs of the source node, cycles); info: clock_ghz, total_cycles, us."""
-        torch = _torch()
-        if not (isinstance(llr, torch.Tensor) and llr.is_cuda and llr.dtype == torch.int8 and llr.is_contiguous()
-                and llr.dim() == 2 and llr.shape[1] == self.N):
-            raise TypeError("llr must be a contiguous CUDA int8 tensor [B, %d]" % self.N)
+        torch = self._check_llr(llr)
         B = llr.shape[0]
         if out is None:
             out = torch.empty((B, self.words), dtype=torch.int64, device=llr.device)
-        torch.cuda.synchronize(llr.device)
-        n = ctypes.c_uint32(0)
-        _check("polar_sc_trace", lib().polar_sc_trace(self._plan, ctypes.c_void_p(llr.data_ptr()),
-                                                      ctypes.c_void_p(out.data_ptr()), B, None, 0,
-                                                      ctypes.byref(n), None, None))
-        recs = (polar_sc_trace_rec * n.value)()
-        ghz, tot = ctypes.c_double(0), ctypes.c_uint64(0)
-        _check("polar_sc_trace", lib().polar_sc_trace(self._plan, ctypes.c_void_p(llr.data_ptr()),
-                                                      ctypes.c_void_p(out.data_ptr()), B, recs, n.value,
-                                                      ctypes.byref(n), ctypes.byref(ghz), ctypes.byref(tot)))
+        else:
+            self._check_out(out, llr, (B, self.words), torch.int64)
+        with torch.cuda.device(llr.device):
+            torch.cuda.synchronize(llr.device)
+            n = ctypes.c_uint32(0)
+            _check("polar_sc_trace", lib().polar_sc_trace(self._plan, ctypes.c_void_p(llr.data_ptr()),
+                                                          ctypes.c_void_p(out.data_ptr()), B, None, 0,
+                                                          ctypes.byref(n), None, None))
+            recs = (polar_sc_trace_rec * n.value)()
+            ghz, tot = ctypes.c_double(0), ctypes.c_uint64(0)
+            _check("polar_sc_trace", lib().polar_sc_trace(self._plan, ctypes.c_void_p(llr.data_ptr()),
+                                                          ctypes.c_void_p(out.data_ptr()), B, recs, n.value,
+                                                          ctypes.byref(n), ctypes.byref(ghz), ctypes.byref(tot)))
         rows = [dict(op=TRACE_OPS.get(r.code, r.code), level=r.level, n=r.n, pos=r.pos, nodeN=self.N >> r.level,
                      cycles=int(r.cycles)) for r in recs]
         info = dict(clock_ghz=ghz.value, total_cycles=int(tot.value),
@@ -366,14 +381,17 @@ class Decoder:
 
     def decode_u16(self, llr, out=None, stream=None):
         """As decode(), output int16 [B, N/16]: the TYPE_BITS tokens of my_module's `s` port."""
-        torch = _torch()
+        torch = self._check_llr(llr)
         B = llr.shape[0]
         if out is None:
             out = torch.empty((B, self.N // 16), dtype=torch.int16, device=llr.device)
-        s = stream if stream is not None else torch.cuda.current_stream(llr.device)
-        _check("polar_sc_decode_u16", lib().polar_sc_decode_u16(
-            self._plan, ctypes.c_void_p(llr.data_ptr()), ctypes.c_void_p(out.data_ptr()), B,
-            ctypes.c_void_p(s.cuda_stream)))
+        else:
+            self._check_out(out, llr, (B, self.N // 16), torch.int16)
+        with torch.cuda.device(llr.device):
+            s = stream if stream is not None else torch.cuda.current_stream(llr.device)
+            _check("polar_sc_decode_u16", lib().polar_sc_decode_u16(
+                self._plan, ctypes.c_void_p(llr.data_ptr()), ctypes.c_void_p(out.data_ptr()), B,
+                ctypes.c_void_p(s.cuda_stream)))
         return out
 
     def decode_host(self, llr):

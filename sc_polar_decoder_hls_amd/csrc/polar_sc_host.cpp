@@ -240,11 +240,14 @@ int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
 // device state for the current device: schedule upload (+ scratch for `batch` frames)
 // interp: also upload the interpreter schedule of a per-mask plan (the per-op monitor runs
 // the schedule interpreter for those)
-int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool interp = false)
+// held: if non-null, receives the plan lock (still held on success) so that the caller can
+// launch with the scratch pointer it was given before another thread may reallocate it
+int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool interp = false,
+                  std::unique_lock<std::mutex> *held = nullptr)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -EIO;
-    std::lock_guard<std::mutex> lk(p->mu);
+    std::unique_lock<std::mutex> lk(p->mu);
     DevState &st = p->dev[dev];
     if (st.simds == 0) {
         int cus = 0;
@@ -257,6 +260,10 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool int
         if (p->jit && !interp) {
             *out = &st;
             return 0;
+        }
+        if (p->jit && p->cfg.llr_bits != 6) {   // traced per-mask plan: hipRTC interpreter at POLAR_Q
+            rc = polar_host::jit_load_interp(*p, st);
+            if (rc) return rc;
         }
     }
     if (!st.ops) {
@@ -282,6 +289,7 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool int
         }
     }
     *out = &st;
+    if (held) *held = std::move(lk);
     return 0;
 }
 
@@ -310,7 +318,11 @@ int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size
     if (batch == 0) return 0;
     if (batch > (size_t)0x7FFFFFF8) return -EINVAL;
     DevState *st = nullptr;
-    int rc = ensure_device(p, batch, &st);
+    // HBM-scratch plans launch under the plan lock: a concurrent decode of a larger batch on
+    // another thread reallocates the scratch only after this launch has been queued (and
+    // synchronises the device before freeing it)
+    std::unique_lock<std::mutex> held;
+    int rc = ensure_device(p, batch, &st, false, p->gmem ? &held : nullptr);
     if (rc) return rc;
     if (p->jit) return polar_host::jit_launch(*p, *st, llr, out, (long)batch, out_stride, stream);
     const int wpg = waves_per_group(p, batch, st->simds);
@@ -334,18 +346,24 @@ int trace_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size_
     *count = (uint32_t)dops.size();
     if (!recs) return 0;
     DevState *st = nullptr;
-    int rc = ensure_device(p, batch, &st, true);
+    std::unique_lock<std::mutex> held;
+    int rc = ensure_device(p, batch, &st, true, &held);
     if (rc) return rc;
     const size_t slots = dops.size() + 3;
     unsigned long long *dtrace = nullptr;
     if (hipMalloc(&dtrace, slots * sizeof(unsigned long long)) != hipSuccess) return -ENOMEM;
     std::vector<unsigned long long> h(slots, 0);
     rc = hipMemset(dtrace, 0, slots * sizeof(unsigned long long)) == hipSuccess ? 0 : -EIO;
-    const int wpg = waves_per_group(p, batch, st->simds);
+    int wpg = waves_per_group(p, batch, st->simds);
     if (!rc) {
-        if (p->hybrid)
+        if (p->hybrid) {
             rc = polar_host::jit_launch_hybrid(*p, *st, llr, out, (long)batch, out_stride, wpg, nullptr, dtrace);
-        else
+        } else if (p->jit && p->cfg.llr_bits != 6) {
+            // per-mask plan at another LLR_BITS: the hipRTC interpreter of its POLAR_Q
+            if (wpg > polar_host::HYBRID_MAX_WAVES) wpg = polar_host::HYBRID_MAX_WAVES;
+            rc = polar_host::launch_interp_fn(st->ifn_trace, *p, *st, llr, out, (long)batch, out_stride, wpg, nullptr,
+                                              dtrace);
+        } else
             rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, (uint32_t *)st->scratch, (int)p->N,
                                         (long)batch, out_stride, wpg, 1, p->hbm_group_dwords, p->lds_group_dwords,
                                         p->lds0, nullptr, dtrace) ? -EIO : 0;
@@ -396,7 +414,7 @@ const char *polar_sc_strerror(int err)
     case 0: return "success";
     case -EINVAL: return "invalid argument";
     case -ENOMEM: return "out of memory";
-    case -ENOTSUP: return "configuration not supported (only the reference config.h)";
+    case -ENOTSUP: return "configuration not supported (see polar_sc_config in include/polar_sc.h for the accepted ranges)";
     case -ENOENT: return "file not found";
     case -EIO: return "HIP runtime error";
     default: return "unknown error";
@@ -548,6 +566,7 @@ int polar_sc_plan_destroy(polar_sc_plan *p)
         if (have_dev) (void)hipSetDevice(kv.first);
         if (kv.second.ops) (void)hipFree(kv.second.ops);
         if (kv.second.module) (void)hipModuleUnload(kv.second.module);
+        if (kv.second.imodule) (void)hipModuleUnload(kv.second.imodule);
         if (kv.second.scratch) (void)hipFree(kv.second.scratch);
     }
     if (have_dev && !p->dev.empty()) (void)hipSetDevice(cur);

@@ -450,35 +450,40 @@ struct Gen {
 }  // namespace
 
 // Hybrid plan: the schedule interpreter (polar_sc_interp.h, with OP_SUB) plus one generated
-// subtree decoder per distinct mixed subtree of p.sub_words words.
-std::string hybrid_source(const polar_sc_plan &p)
+// subtree decoder per distinct mixed subtree of p.sub_words words. with_subs = false: the
+// plain interpreter alone, specialised on the plan's POLAR_Q (the per-op monitor of per-mask
+// plans whose LLR_BITS is not the hipcc-built 6).
+std::string hybrid_source(const polar_sc_plan &p, bool with_subs = true)
 {
     std::ostringstream o;
     const bool gm = p.gmem != 0;
-    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_SC_SUBS 1\n#define POLAR_Q " << p.cfg.llr_bits
-      << "\n#include \"polar_sc_interp.h\"\n"
-      << "namespace polar {\n#define CH(w) cin_[(w) * 64]\n";
-    int lg = 0;
-    while ((1 << lg) < p.sub_words) lg++;
-    for (size_t id = 0; id < p.subs.size(); id++) {
-        Gen g(p.subs[id], lg);
-        g.sub_function((int)id, gm);
-        o << g.o.str();
+    const int waves = with_subs ? p.hybrid_waves : HYBRID_MAX_WAVES;
+    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_SC_SUBS " << (with_subs ? 1 : 0) << "\n#define POLAR_Q "
+      << p.cfg.llr_bits << "\n#include \"polar_sc_interp.h\"\n";
+    if (with_subs) {
+        o << "namespace polar {\n#define CH(w) cin_[(w) * 64]\n";
+        int lg = 0;
+        while ((1 << lg) < p.sub_words) lg++;
+        for (size_t id = 0; id < p.subs.size(); id++) {
+            Gen g(p.subs[id], lg);
+            g.sub_function((int)id, gm);
+            o << g.o.str();
+        }
+        const char *ctx = gm ? "Ctx<true>" : "Ctx<false>";
+        o << "#undef CH\ntemplate <>\n__device__ void polar_sub_call<" << (gm ? "true" : "false") << ">(const " << ctx
+          << " &c, int id, int ldo, int pos)\n{\n  switch (id) {\n";
+        for (size_t id = 0; id < p.subs.size(); id++)
+            o << "  case " << id << ": polar_sub_" << id << "(c, ldo, pos); return;\n";
+        o << "  default: return;\n  }\n}\n}  // namespace polar\n";
     }
-    const char *ctx = gm ? "Ctx<true>" : "Ctx<false>";
-    o << "#undef CH\ntemplate <>\n__device__ void polar_sub_call<" << (gm ? "true" : "false") << ">(const " << ctx
-      << " &c, int id, int ldo, int pos)\n{\n  switch (id) {\n";
-    for (size_t id = 0; id < p.subs.size(); id++)
-        o << "  case " << id << ": polar_sub_" << id << "(c, ldo, pos); return;\n";
-    o << "  default: return;\n  }\n}\n}  // namespace polar\n"
-      << "extern \"C\" __global__ void __launch_bounds__(" << p.hybrid_waves * 64 << ") polar_sc_hybrid_kernel(\n"
+    o << "extern \"C\" __global__ void __launch_bounds__(" << waves * 64 << ") polar_sc_hybrid_kernel(\n"
       << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
       << "    unsigned int *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb, int group_dwords,\n"
       << "    int lds_dwords, int lds0)\n{\n"
       << "  polar::decode_body<" << (gm ? "true" : "false")
       << ">(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords, lds0);\n}\n"
       // the per-op monitor variant (polar_sc_trace)
-      << "extern \"C\" __global__ void __launch_bounds__(" << p.hybrid_waves * 64 << ") polar_sc_hybrid_trace_kernel(\n"
+      << "extern \"C\" __global__ void __launch_bounds__(" << waves * 64 << ") polar_sc_hybrid_trace_kernel(\n"
       << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
       << "    unsigned int *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb, int group_dwords,\n"
       << "    int lds_dwords, int lds0, unsigned long long *__restrict__ trace)\n{\n"
@@ -493,10 +498,9 @@ std::string jit_source(const polar_sc_plan &p)
     return Gen(p.ops, p.lg).run_mask(p);
 }
 
-int jit_compile(const polar_sc_plan &p)
+namespace {
+int rtc_compile(const std::string &src, std::vector<char> &code, std::string &log)
 {
-    if (!p.jit_code.empty()) return 0;
-    const std::string src = jit_source(p);
     hiprtcProgram prog;
     const char *hdrs[] = {kPolarDeviceSrc, kPolarInterpSrc};
     const char *names[] = {"polar_sc_device.h", "polar_sc_interp.h"};
@@ -506,8 +510,8 @@ int jit_compile(const polar_sc_plan &p)
     size_t log_size = 0;
     hiprtcGetProgramLogSize(prog, &log_size);
     if (log_size > 1) {
-        p.jit_log.resize(log_size);
-        hiprtcGetProgramLog(prog, &p.jit_log[0]);
+        log.resize(log_size);
+        hiprtcGetProgramLog(prog, &log[0]);
     }
     if (rc != HIPRTC_SUCCESS) {
         hiprtcDestroyProgram(&prog);
@@ -515,9 +519,30 @@ int jit_compile(const polar_sc_plan &p)
     }
     size_t code_size = 0;
     hiprtcGetCodeSize(prog, &code_size);
-    p.jit_code.resize(code_size);
-    hiprtcGetCode(prog, p.jit_code.data());
+    code.resize(code_size);
+    hiprtcGetCode(prog, code.data());
     hiprtcDestroyProgram(&prog);
+    return 0;
+}
+}  // namespace
+
+int jit_compile(const polar_sc_plan &p)
+{
+    if (!p.jit_code.empty()) return 0;
+    return rtc_compile(jit_source(p), p.jit_code, p.jit_log);
+}
+
+// Per-mask plans whose LLR_BITS is not the hipcc-built 6: the per-op monitor runs the schedule
+// interpreter compiled by hipRTC with the plan's POLAR_Q (DevState::ifn_trace).
+int jit_load_interp(const polar_sc_plan &p, DevState &st)
+{
+    if (st.ifn_trace) return 0;
+    if (p.interp_code.empty()) {
+        int rc = rtc_compile(hybrid_source(p, false), p.interp_code, p.jit_log);
+        if (rc) return rc;
+    }
+    if (hipModuleLoadData(&st.imodule, p.interp_code.data()) != hipSuccess) return -EIO;
+    if (hipModuleGetFunction(&st.ifn_trace, st.imodule, "polar_sc_hybrid_trace_kernel") != hipSuccess) return -EIO;
     return 0;
 }
 
@@ -548,8 +573,8 @@ int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, ui
 }
 
 // hybrid kernel: the interpreter's launch shape (polar_sc_kernels.hip, polar_sc_launch_decode)
-int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
-                      int out_stride, int wpg, void *stream, unsigned long long *trace)
+int launch_interp_fn(hipFunction_t fn, const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out,
+                     long batch, int out_stride, int wpg, void *stream, unsigned long long *trace)
 {
     const long groups = (batch + 7) / 8;
     const unsigned lds = (unsigned)p.lds_group_dwords * 4u;
@@ -559,9 +584,15 @@ int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *
     void *args[] = {(void *)&llr, (void *)&out, (void *)&ops, (void *)&scratch, (void *)&N, (void *)&b,
                     (void *)&out_stride, (void *)&wpg, (void *)&gpb, (void *)&gd, (void *)&ld, (void *)&l0,
                     (void *)&trace};
-    hipError_t e = hipModuleLaunchKernel(trace ? st.fn_trace : st.fn, (unsigned)groups, 1, 1, (unsigned)(64 * wpg), 1,
-                                         1, lds, (hipStream_t)stream, args, nullptr);
+    hipError_t e = hipModuleLaunchKernel(fn, (unsigned)groups, 1, 1, (unsigned)(64 * wpg), 1, 1, lds,
+                                         (hipStream_t)stream, args, nullptr);
     return e == hipSuccess ? 0 : -EIO;
+}
+
+int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
+                      int out_stride, int wpg, void *stream, unsigned long long *trace)
+{
+    return launch_interp_fn(trace ? st.fn_trace : st.fn, p, st, llr, out, batch, out_stride, wpg, stream, trace);
 }
 
 }  // namespace polar_host

@@ -21,6 +21,8 @@ struct DevState {
     hipModule_t module = nullptr; // per-mask kernel
     hipFunction_t fn = nullptr;
     hipFunction_t fn_trace = nullptr;   // hybrid plans: the per-op monitor variant
+    hipModule_t imodule = nullptr;      // per-mask plans with llr_bits != 6: hipRTC interpreter
+    hipFunction_t ifn_trace = nullptr;  //   (per-op monitor only)
     int simds = 0;                // SIMDs of the device (4 per CU), for launch sizing
 };
 
@@ -73,6 +75,7 @@ struct polar_sc_plan {
     mutable std::mutex host_mu;                             // polar_sc_decode_host staging
     mutable std::map<int, polar_host::HostBufs> host_bufs;
     mutable std::vector<char> jit_code;   // compiled code object (lazily built)
+    mutable std::vector<char> interp_code;   // per-mask plans, llr_bits != 6: traced interpreter
     mutable std::string jit_log;
 };
 
@@ -86,5 +89,8 @@ int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, ui
                long batch, int out_stride, void *stream);
 int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
                       int out_stride, int wpg, void *stream, unsigned long long *trace = nullptr);
+int jit_load_interp(const polar_sc_plan &p, DevState &st);
+int launch_interp_fn(hipFunction_t fn, const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out,
+                     long batch, int out_stride, int wpg, void *stream, unsigned long long *trace);
 bool jit_supported(uint32_t N);
 }  // namespace polar_host

@@ -145,3 +145,27 @@ def test_c_cli_stats_generated_mask_format(pkg, tmp_path):
     st = pkg.Decoder(mask).stats
     assert ("N=1024 K=512 groups=64 R0=%d R1=%d REP=%d SPC=%d RN=%d" %
             (st["n_r0"], st["n_r1"], st["n_rep"], st["n_spc"], st["n_rn"])) in r.stdout
+
+
+def test_decode_entry_points_reject_bad_tensors(pkg):
+    """decode / decode_u16 / trace validate device, dtype, shape and contiguity before any
+    pointer reaches the C ABI (a CPU tensor or a short row would fault the GPU)."""
+    import torch
+    import util
+    dec = pkg.Decoder(util.mask("FB_N128_K64"))
+    cpu = torch.zeros((4, 128), dtype=torch.int8)
+    for fn in (dec.decode, dec.decode_u16, dec.trace):
+        with pytest.raises(TypeError):
+            fn(cpu)                                   # host tensor
+        with pytest.raises(TypeError):
+            fn(np.zeros((4, 128), np.int8))           # not a tensor at all
+    with pytest.raises(TypeError):
+        dec.decode(torch.zeros((4, 128), dtype=torch.int16))
+    assert dec._check_out is not None
+    # out-tensor checks (device-independent part)
+    with pytest.raises(ValueError):
+        pkg.Decoder._check_out(torch.zeros((4, 3), dtype=torch.int64), cpu, (4, 2), torch.int64)
+    with pytest.raises(ValueError):
+        pkg.Decoder._check_out(torch.zeros((4, 8), dtype=torch.int64), cpu, (4, 8), torch.int16)
+    with pytest.raises(ValueError):
+        pkg.Decoder._check_out(torch.zeros((8, 4), dtype=torch.int16).t(), cpu, (4, 8), torch.int16)

@@ -46,3 +46,22 @@ def test_trace_decode(pkg, cuda, oracle_mod, name, batch):
         assert any(r["op"] == "SUB" for r in rows)
     rep = monitor.report(rows, info)
     assert sum(rep["by_function"].values()) == info["total_cycles"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [5, 7, 8])
+@pytest.mark.parametrize("name", ["FB_N1024_K512", "frozen_n_4096_k_2048"])
+def test_trace_decode_llr_bits(pkg, cuda, oracle_mod, name, q):
+    """The monitor of a plan at another LLR_BITS runs that plan's own arithmetic (per-mask
+    plans: the hipRTC interpreter compiled with POLAR_Q = q): same x^ as the oracle at q."""
+    mask = util.mask(name)
+    rng = np.random.default_rng(q)
+    lim = (1 << (q - 1)) - 1
+    llr = rng.integers(-lim, lim + 1, size=(16, mask.size)).astype(np.int8)
+    cfg = pkg.default_config()
+    cfg.llr_bits = q
+    dec = pkg.Decoder(mask, cfg)
+    rows, info = dec.trace(cuda.from_numpy(llr).cuda())
+    got = pkg.unpack_bits(info["out"].cpu().numpy(), mask.size)
+    np.testing.assert_array_equal(got, oracle_mod.decode_fsm(mask, llr, llr_bits=q))
+    assert sum(r["cycles"] for r in rows if r["op"] != "END") == info["total_cycles"]

@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--ebn0", type=float, default=2.5)
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="distinct input batches cycled through (0: as bench.py, >= 300 MB in total)")
     a = ap.parse_args()
     import torch
     import bench
@@ -25,11 +27,12 @@ def main():
     dev = torch.device("cuda", 0)
     dec = pkg.Decoder(mask)
     dec.prepare(a.batch)
-    llr, _ = bench.gen_frames_torch(torch, mask, a.batch, a.ebn0, 0xF0, dev)
+    nb = a.rotate if a.rotate > 0 else max(1, min(8, -(-bench.ROTATE_BYTES // (a.batch * mask.size))))
+    llrs = [bench.gen_frames_torch(torch, mask, a.batch, a.ebn0, 0xF0 + b, dev)[0] for b in range(nb)]
     out = torch.empty((a.batch, dec.words), dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
-    for _ in range(a.reps):
-        dec.decode(llr, out)
+    for i in range(a.reps):
+        dec.decode(llrs[i % nb], out)
     torch.cuda.synchronize()
     print("decoded %d x %d frames (N=%d)" % (a.reps, a.batch, mask.size))
 
