@@ -69,3 +69,29 @@ def build(force=False, verbose=False):
     subprocess.check_call(cmd)
     os.replace(tmp, LIB)
     return LIB
+
+
+def prewarm(masks, configs=(None,), threads=8, verbose=False):
+    """Compile the hipRTC kernels of the plans of `masks` ({name: info mask}) x `configs`
+    into the on-disk code-object cache next to the library (lib/rtc_cache/), host only, in
+    parallel. A GPU box then loads them instead of compiling (the C5 hybrid kernel takes about
+    two minutes of hipRTC)."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+    import sc_polar_decoder_hls_amd as pkg
+
+    def one(item):
+        name, m, cfg = item
+        t0 = time.time()
+        dec = pkg.Decoder(m, cfg)
+        ok = dec.compile()
+        dec.close()
+        return name, ok, time.time() - t0
+
+    items = [(n, m, c) for n, m in masks.items() for c in configs]
+    # largest first: the long compiles overlap the short ones
+    items.sort(key=lambda it: -it[1].size)
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        for name, ok, dt in ex.map(one, items):
+            if verbose:
+                print("prewarm %-28s %s %.1f s" % (name, "compiled" if ok else "(no hipRTC kernel)", dt))

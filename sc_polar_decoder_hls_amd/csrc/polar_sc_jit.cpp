@@ -15,9 +15,15 @@
 
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <cerrno>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <sstream>
 
 namespace {
@@ -499,14 +505,88 @@ std::string jit_source(const polar_sc_plan &p)
 }
 
 namespace {
+// Code-object cache: hipRTC output keyed by a hash of the generated source, the embedded
+// device headers and the options, kept next to the library (lib/rtc_cache/, or
+// $POLAR_SC_RTC_CACHE). The hybrid kernels of the large-N configurations take minutes to
+// compile (C5: ~120 subtree decoders); __graft_entry__.build() compiles the benchmark plans
+// once on the build host and the cache travels with the in-tree library.
+const char *const kRtcOpts[] = {"--gpu-architecture=gfx950", "-O3", "-std=c++17"};
+
+uint64_t fnv1a(uint64_t h, const char *s, size_t n)
+{
+    for (size_t i = 0; i < n; i++) {
+        h ^= (unsigned char)s[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+std::string cache_dir()
+{
+    if (const char *e = std::getenv("POLAR_SC_RTC_CACHE")) return e;   // "" disables the cache
+    Dl_info info;
+    if (!dladdr((const void *)&cache_dir, &info) || !info.dli_fname) return "";
+    std::string so = info.dli_fname;
+    const size_t slash = so.rfind('/');
+    return (slash == std::string::npos ? std::string(".") : so.substr(0, slash)) + "/rtc_cache";
+}
+
+std::string cache_path(const std::string &src)
+{
+    const std::string dir = cache_dir();
+    if (dir.empty()) return "";
+    uint64_t h = 1469598103934665603ull;
+    h = fnv1a(h, src.data(), src.size());
+    h = fnv1a(h, kPolarDeviceSrc, sizeof kPolarDeviceSrc);
+    h = fnv1a(h, kPolarInterpSrc, sizeof kPolarInterpSrc);
+    for (const char *o : kRtcOpts) h = fnv1a(h, o, std::strlen(o) + 1);
+    int ver_major = 0, ver_minor = 0;
+    hiprtcVersion(&ver_major, &ver_minor);
+    h = fnv1a(h, (const char *)&ver_major, sizeof ver_major);
+    h = fnv1a(h, (const char *)&ver_minor, sizeof ver_minor);
+    char name[40];
+    std::snprintf(name, sizeof name, "/%016llx.co", (unsigned long long)h);
+    return dir + name;
+}
+
+bool cache_load(const std::string &path, std::vector<char> &code)
+{
+    if (path.empty()) return false;
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    std::vector<char> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (buf.size() < 4 || std::memcmp(buf.data(), "\x7f" "ELF", 4) != 0) return false;
+    code.swap(buf);
+    return true;
+}
+
+void cache_store(const std::string &path, const std::vector<char> &code)
+{
+    if (path.empty()) return;
+    const size_t slash = path.rfind('/');
+    (void)mkdir(path.substr(0, slash).c_str(), 0755);
+    const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) return;
+        f.write(code.data(), (std::streamsize)code.size());
+        if (!f) {
+            std::remove(tmp.c_str());
+            return;
+        }
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
+}
+
 int rtc_compile(const std::string &src, std::vector<char> &code, std::string &log)
 {
+    const std::string cpath = cache_path(src);
+    if (cache_load(cpath, code)) return 0;
     hiprtcProgram prog;
     const char *hdrs[] = {kPolarDeviceSrc, kPolarInterpSrc};
     const char *names[] = {"polar_sc_device.h", "polar_sc_interp.h"};
     if (hiprtcCreateProgram(&prog, src.c_str(), "polar_sc_mask.hip", 2, hdrs, names) != HIPRTC_SUCCESS) return -EIO;
-    const char *opts[] = {"--gpu-architecture=gfx950", "-O3", "-std=c++17"};
-    hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    hiprtcResult rc = hiprtcCompileProgram(prog, 3, const_cast<const char **>(kRtcOpts));
     size_t log_size = 0;
     hiprtcGetProgramLogSize(prog, &log_size);
     if (log_size > 1) {
@@ -522,6 +602,7 @@ int rtc_compile(const std::string &src, std::vector<char> &code, std::string &lo
     code.resize(code_size);
     hiprtcGetCode(prog, code.data());
     hiprtcDestroyProgram(&prog);
+    cache_store(cpath, code);
     return 0;
 }
 }  // namespace
