@@ -70,6 +70,15 @@ def lib():
         L.orc_encode.restype = None
         L.orc_set_llr_bits.argtypes = [i32]
         L.orc_set_llr_bits.restype = i32
+        L.orc_set_format.argtypes = [i32, i32, i32, i32]
+        L.orc_set_format.restype = i32
+        L.orc_decode_fsm16.argtypes = [i32, p, p, p, i32, p, p]
+        L.orc_decode_fsm16.restype = i32
+        L.orc_decode_rec16.argtypes = [i32, p, p, p, i32, p]
+        L.orc_decode_rec16.restype = i32
+        for name in ("orc_F_ca2", "orc_G_ca2", "orc_Gext_ca2"):
+            getattr(L, name).argtypes = [i32, u32, u32] + ([u32] if name != "orc_F_ca2" else [])
+            getattr(L, name).restype = u32
         _lib = L
     return _lib
 
@@ -97,29 +106,44 @@ def _cfg(config):
 
 
 @contextlib.contextmanager
-def _llr_bits(q):
-    """LLR_BITS of the restatement for the calling thread (config.h:2; 6 = as shipped)."""
-    if lib().orc_set_llr_bits(int(q)) != 0:
-        raise ValueError("llr_bits must be 5..8, got %r" % (q,))
+def _format(llr_bits=6, par=16, sigmag=1, extended=1):
+    """Datapath of the restatement for the calling thread: LLR_BITS (config.h:2), PAR
+    (polar_parameters.h:8), SIGMAG / CA2 (config.h:11) and EXTENDED (config.h:14); the
+    defaults are the shipped configuration."""
+    if lib().orc_set_format(int(llr_bits), int(par), 0 if sigmag else 1, 1 if extended else 0) != 0:
+        raise ValueError("bad format: llr_bits %r (5..9), par %r (2..64, power of two)" % (llr_bits, par))
     try:
         yield
     finally:
-        lib().orc_set_llr_bits(6)
+        lib().orc_set_format(6, 16, 0, 1)
 
 
-def decode_fsm(mask, llr, return_counts=False, config=None, llr_bits=6):
-    """Literal FSM decode. mask: (N,) 0/1; llr: (B, N) int8. Returns xhat (B, N) uint8.
-    config: 7-tuple (see SWEEP_CONFIGS) or None for the shipped config.h; llr_bits: LLR_BITS
-    (5..8, the low llr_bits of each int8 are the LLR)."""
+def _llr_bits(q):
+    return _format(q)
+
+
+def _llr_array(llr, llr_bits):
+    """int8 frames (llr_bits <= 8) or int16 frames (any llr_bits; the only form for 9)."""
+    a = np.atleast_2d(np.asarray(llr))
+    if a.dtype == np.int16 or llr_bits > 8:
+        return np.ascontiguousarray(a, dtype=np.int16), True
+    return np.ascontiguousarray(a, dtype=np.int8), False
+
+
+def decode_fsm(mask, llr, return_counts=False, config=None, llr_bits=6, par=16, sigmag=1, extended=1):
+    """Literal FSM decode. mask: (N,) 0/1; llr: (B, N) int8 (or int16). Returns xhat (B, N)
+    uint8. config: 7-tuple (see SWEEP_CONFIGS) or None for the shipped config.h; llr_bits:
+    LLR_BITS (5..9, the low llr_bits of each input are the LLR); par / sigmag / extended: the
+    datapath (see _format)."""
     mask = np.ascontiguousarray(mask, dtype=np.uint8)
-    llr = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
+    llr, wide = _llr_array(llr, llr_bits)
     B, N = llr.shape
     out = np.zeros((B, N), dtype=np.uint8)
     counts = np.zeros(len(STATES), dtype=np.int64)
     c = _cfg(config)
-    with _llr_bits(llr_bits):
-        rc = lib().orc_decode_fsm_cfg(N, _ptr(mask), _ptr(llr), _ptr(out), B, _ptr(counts),
-                                      None if c is None else _ptr(c))
+    fn = lib().orc_decode_fsm16 if wide else lib().orc_decode_fsm_cfg
+    with _format(llr_bits, par, sigmag, extended):
+        rc = fn(N, _ptr(mask), _ptr(llr), _ptr(out), B, _ptr(counts), None if c is None else _ptr(c))
     if rc != 0:
         raise RuntimeError("orc_decode_fsm failed: %d" % rc)
     if return_counts:
@@ -127,15 +151,16 @@ def decode_fsm(mask, llr, return_counts=False, config=None, llr_bits=6):
     return out
 
 
-def decode_rec(mask, llr, config=None, llr_bits=6):
+def decode_rec(mask, llr, config=None, llr_bits=6, par=16, sigmag=1, extended=1):
     """Recursive-restatement decode (same I/O as decode_fsm)."""
     mask = np.ascontiguousarray(mask, dtype=np.uint8)
-    llr = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
+    llr, wide = _llr_array(llr, llr_bits)
     B, N = llr.shape
     out = np.zeros((B, N), dtype=np.uint8)
     c = _cfg(config)
-    with _llr_bits(llr_bits):
-        rc = lib().orc_decode_rec_cfg(N, _ptr(mask), _ptr(llr), _ptr(out), B, None if c is None else _ptr(c))
+    fn = lib().orc_decode_rec16 if wide else lib().orc_decode_rec_cfg
+    with _format(llr_bits, par, sigmag, extended):
+        rc = fn(N, _ptr(mask), _ptr(llr), _ptr(out), B, None if c is None else _ptr(c))
     if rc != 0:
         raise RuntimeError("orc_decode_rec failed: %d" % rc)
     return out

@@ -7,9 +7,18 @@
  *   (sc_polar_decoder_hls_amd / libpolar_sc.so) never links, loads or calls it.
  *
  * What it is: a plain-C restatement of the reference decoder of
- * ydelomier/SC_Polar_decoder_HLS (SystemC / Vivado-HLS, config of src/module/config.h:
- * LLR_BITS=6, SIGMAG, EXTENDED=1, PRUNING_LEVEL=2, ELAG_R1=ELAG_REP=ELAG_SPC=1,
- * ELAG_REP2=ELAG_SPC2=ELAG_RARE=0, ELAG_H0=1, PAR=16).
+ * ydelomier/SC_Polar_decoder_HLS (SystemC / Vivado-HLS). The shipped configuration is
+ * src/module/config.h (LLR_BITS=6, SIGMAG, EXTENDED=1, PRUNING_LEVEL=2,
+ * ELAG_R1=ELAG_REP=ELAG_SPC=1, ELAG_REP2=ELAG_SPC2=ELAG_RARE=0, ELAG_H0=1) with PAR=16
+ * (src/module/polar_parameters.h:8). The compile-time switches the reference's scripts sweep
+ * are run-time settings here, per calling thread:
+ *   * orc_set_format(q, par, ca2, ext): LLR_BITS 5..9 (config.h:2; parser.sh:12 and
+ *     parser_comp.sh:12 sweep QUANT 6/7/8/9), PAR 2..64 (polar_parameters.h:8;
+ *     script_RTL_sim.sh / parser.sh sweep 4..64, script_tests.sh:11 16 and 64), the number
+ *     format SIGMAG or CA2 (config.h:11; functions.h:48-118 vs 124-281) and EXTENDED
+ *     (config.h:14; functions.h:785-866 Spec_P*_ext vs Spec_P*);
+ *   * the 7-tuple of orc_decode_*_cfg: PRUNING_LEVEL and the ELAG_* node switches
+ *     (config.h:16-28, script/script_tests.sh:103-122).
  *
  * Two independent restatements live here:
  *   1. orc_decode_fsm  -- a LITERAL cycle-free simulation of my_module::do_prunning and
@@ -27,29 +36,38 @@
  * and it ships no recorded decoder outputs. The only known-answer vectors it holds are
  * the 9 hard-coded codewords of src/testbench/sc_encoder/sc_encoder.h:74-88; those pin
  * the encoding / frozen-bit conventions and noiseless decoding (tests/golden/kat_*.json).
- * The fixed-point corner cases (signed zero, G saturation at 15, REP 511 clamp, SPC tie
- * rule) are PARITY UNPINNED by reference outputs: they follow the literal text of the
- * cited SystemC source, cross-checked by the two restatements above and by the
- * bit-level primitive tests in tests/test_oracle_primitives.py.
+ * The fixed-point corner cases (signed zero, G saturation, REP clamps, SPC tie rule, the
+ * CA2 qabs(-2^(Q-1)) wrap) are PARITY UNPINNED by reference outputs: they follow the
+ * literal text of the cited SystemC source, cross-checked by the two restatements above
+ * and by the bit-level primitive tests in tests/test_oracle_primitives.py.
  */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
-#define PAR 16
+#define PAR_MAX 64
 
-/* LLR_BITS (config.h:2): 6 in the shipped config. The reference's pruning sweep runs at
- * QUANT = 8 (script/script_tests.sh:9,25); orc_set_llr_bits() selects 5..8 for the calling
- * thread, as the GPU plans take polar_sc_config.llr_bits. */
-static _Thread_local int g_llr_bits = 6;
-#define LLR_BITS g_llr_bits
+/* Per-thread configuration of the restated hardware (see header). */
+static _Thread_local int g_q = 6;       /* LLR_BITS */
+static _Thread_local int g_par = 16;    /* PAR */
+static _Thread_local int g_lpar = 4;    /* LOG2_PAR */
+static _Thread_local int g_ca2 = 0;     /* 1: CA2 (two's complement), 0: SIGMAG */
+static _Thread_local int g_ext = 1;     /* EXTENDED */
+#define LLR_BITS g_q
+#define PAR g_par
+#define LOG2_PAR g_lpar
 
-int orc_set_llr_bits(int q)
+static int ilog2(int v) { int l = 0; while ((1 << l) < v) l++; return l; }
+
+int orc_set_format(int q, int par, int ca2, int ext)
 {
-    if (q < 5 || q > 8) return -22;
-    g_llr_bits = q;
+    if (q < 5 || q > 9 || par < 2 || par > PAR_MAX || (par & (par - 1)) || (ca2 & ~1) || (ext & ~1)) return -22;
+    g_q = q; g_par = par; g_lpar = ilog2(par); g_ca2 = ca2; g_ext = ext;
     return 0;
 }
+
+/* LLR_BITS only (the other switches keep their current values) */
+int orc_set_llr_bits(int q) { return orc_set_format(q, g_par, g_ca2, g_ext); }
 
 /* node codes: shared/src/library.h:34-40 */
 #define NODE_R0   0x00
@@ -61,9 +79,13 @@ int orc_set_llr_bits(int q)
 #define NODE_RN   0x08
 
 static inline uint32_t msk(int q) { return (q >= 32) ? 0xFFFFFFFFu : ((1u << q) - 1u); }
+static inline uint64_t msk64(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
+/* sign-extend a Q-bit pattern */
+static inline int32_t sx(int Q, uint32_t v) { v &= msk(Q); return (v >> (Q - 1)) & 1u ? (int32_t)v - (int32_t)(1u << Q) : (int32_t)v; }
+static inline uint32_t sgn(int Q, uint32_t v) { return (v >> (Q - 1)) & 1u; }   /* qsign / qsign_sm */
 
 /* ------------------------------------------------------------------------------------ */
-/* Scalar primitives (shared/src/scalar.h)                                               */
+/* SIGMAG scalar primitives (shared/src/scalar.h:86-239)                                */
 /* ------------------------------------------------------------------------------------ */
 
 /* qconv_format<Q> (scalar.h:229-239): CA2 -> SIGMAG (Q-bit patterns). */
@@ -126,7 +148,7 @@ uint32_t orc_full_adder_sat_sm(int Q, uint32_t a, uint32_t b)
 }
 
 /* ------------------------------------------------------------------------------------ */
-/* Polar operators (shared/src/functions.h:124-281), one lane                             */
+/* Polar operators, one lane: SIGMAG (functions.h:124-281) and CA2 (functions.h:48-118)  */
 /* ------------------------------------------------------------------------------------ */
 
 /* F_function_SM<P,Q> (functions.h:124-145): sign = xor, magnitude = min, no saturation. */
@@ -155,15 +177,60 @@ uint32_t orc_Gext_sm(int Q, uint32_t la, uint32_t lb, uint32_t sa)
     return qfull_add_sub_sm(Q, la, lb, sa);
 }
 
-/* F_simplified_SM (functions.h:241-256) for P=1 */
+/* qabs<Q> (scalar.h:42-49): -v in Q bits, so qabs(-2^(Q-1)) = -2^(Q-1) (the pattern wraps) */
+static uint32_t qabs_ca2(int Q, uint32_t v) { return (uint32_t)(sgn(Q, v) ? -sx(Q, v) : sx(Q, v)) & msk(Q); }
+
+/* qsat<Q>(sc_bigint<Q+1>) (scalar.h:15-20): clamp to [-(2^(Q-1)-1), 2^(Q-1)-1] */
+static int32_t qsat_ca2(int Q, int32_t v)
+{
+    const int32_t hi = (int32_t)msk(Q - 1), lo = -hi;
+    return v > hi ? hi : (v < lo ? lo : v);
+}
+
+/* F_function_C2<P,Q> (functions.h:48-61): min of the qabs values (signed compare, qmin),
+ * negated (in Q bits) when the signs differ (qsign) */
+uint32_t orc_F_ca2(int Q, uint32_t la, uint32_t lb)
+{
+    uint32_t aa = qabs_ca2(Q, la), ab = qabs_ca2(Q, lb);
+    uint32_t mn = sx(Q, aa) < sx(Q, ab) ? aa : ab;
+    uint32_t sig = sgn(Q, la) ^ sgn(Q, lb);
+    return sig ? ((uint32_t)(-sx(Q, mn)) & msk(Q)) : mn;
+}
+
+/* G_function_C2<P,Q> (functions.h:63-75): sa ? lb - la : lb + la exactly (Q+1 bits), then
+ * VECTOR_SAT<P,Q> (qsat<Q>: +-(2^(Q-1)-1), 31 at Q = 6) */
+uint32_t orc_G_ca2(int Q, uint32_t la, uint32_t lb, uint32_t sa)
+{
+    int32_t g = (sa & 1u) ? sx(Q, lb) - sx(Q, la) : sx(Q, lb) + sx(Q, la);
+    return (uint32_t)qsat_ca2(Q, g) & msk(Q);
+}
+
+/* G_extended_C2<P,Q> (functions.h:77-87): the same without saturation, (Q+1)-bit pattern */
+uint32_t orc_Gext_ca2(int Q, uint32_t la, uint32_t lb, uint32_t sa)
+{
+    int32_t g = (sa & 1u) ? sx(Q, lb) - sx(Q, la) : sx(Q, lb) + sx(Q, la);
+    return (uint32_t)g & msk(Q + 1);
+}
+
+/* Function_F / G / G_ext / F_simp / G_simp (functions.h:287-341): the configured format */
+static uint32_t fF(int Q, uint32_t a, uint32_t b) { return g_ca2 ? orc_F_ca2(Q, a, b) : orc_F_sm(Q, a, b); }
+static uint32_t fG(int Q, uint32_t a, uint32_t b, uint32_t s) { return g_ca2 ? orc_G_ca2(Q, a, b, s) : orc_G_sm(Q, a, b, s); }
+static uint32_t fGext(int Q, uint32_t a, uint32_t b, uint32_t s) { return g_ca2 ? orc_Gext_ca2(Q, a, b, s) : orc_Gext_sm(Q, a, b, s); }
+
+/* F_simplified_SM / _C2 (functions.h:241-256, 89-101): sign xor & fb */
 static uint32_t F_simp(int Q, uint32_t la, uint32_t lb, uint32_t fb)
 {
     return (((la ^ lb) >> (Q - 1)) & 1u) & fb;
 }
 
-/* G_simplified_SM (functions.h:258-281) for P=1 */
+/* G_simplified_SM (functions.h:258-281): the qfull_add_sub_sm sign rule & fb;
+ * G_simplified_C2 (functions.h:103-118): sign of the exact (Q+1)-bit g & fb */
 static uint32_t G_simp(int Q, uint32_t la, uint32_t lb, uint32_t sa, uint32_t fb)
 {
+    if (g_ca2) {
+        int32_t g = (sa & 1u) ? sx(Q, lb) - sx(Q, la) : sx(Q, lb) + sx(Q, la);
+        return (g < 0 ? 1u : 0u) & fb;
+    }
     uint32_t sla = (la >> (Q - 1)) & 1u;
     uint32_t sigla = sla ^ sa;
     uint32_t siglb = (lb >> (Q - 1)) & 1u;
@@ -182,94 +249,123 @@ static uint32_t spec_p2(int Q, const uint32_t *llr, uint32_t fb)
     return (sb1 << 1) | (sa1 ^ sb1);
 }
 
-/* Spec_P{4,8,16}_ext<Q> (functions.h:413-438, 467-492, 521-546): exact leaf with
- * widths growing by one bit per G_extended. Returns the n encoded bits x (lane 0 = bit 0). */
-static uint32_t spec_pn_ext(int n, int Q, const uint32_t *llr, uint32_t fb)
+/* Spec_P{n}_ext<Q> (EXTENDED = 1, functions.h:413-438 ...: widths grow by one bit per
+ * G_extended) or Spec_P{n}<Q> (EXTENDED = 0, functions.h:386-411 ...: saturating G, width
+ * Q throughout); Spec_P1 (functions.h:354-364) for n = 1. Returns the n encoded bits x
+ * (lane 0 = bit 0); fb bit k = frozen-table bit of lane k (1 = information). */
+static uint64_t spec_pn(int n, int Q, const uint32_t *llr, uint64_t fb)
 {
-    if (n == 2) return spec_p2(Q, llr, fb);
+    if (n == 1) return sgn(Q, llr[0]) & (uint32_t)fb;
+    if (n == 2) return spec_p2(Q, llr, (uint32_t)fb);
     int h = n / 2;
-    uint32_t la1[8] = {0}, lb1[8] = {0};
-    for (int j = 0; j < h; j++) la1[j] = orc_F_sm(Q, llr[j], llr[h + j]);
-    uint32_t sa1 = spec_pn_ext(h, Q, la1, fb & msk(h));
-    for (int j = 0; j < h; j++) lb1[j] = orc_Gext_sm(Q, llr[j], llr[h + j], (sa1 >> j) & 1u);
-    uint32_t sb1 = spec_pn_ext(h, Q + 1, lb1, (fb >> h) & msk(h));
-    return (sb1 << h) | ((sa1 ^ sb1) & msk(h));
+    uint32_t la1[PAR_MAX / 2] = {0}, lb1[PAR_MAX / 2] = {0};
+    for (int j = 0; j < h; j++) la1[j] = fF(Q, llr[j], llr[h + j]);
+    uint64_t sa1 = spec_pn(h, Q, la1, fb & msk64(h));
+    for (int j = 0; j < h; j++) {
+        uint32_t s = (uint32_t)(sa1 >> j) & 1u;
+        lb1[j] = g_ext ? fGext(Q, llr[j], llr[h + j], s) : fG(Q, llr[j], llr[h + j], s);
+    }
+    uint64_t sb1 = spec_pn(h, g_ext ? Q + 1 : Q, lb1, (fb >> h) & msk64(h));
+    return (sb1 << h) | ((sa1 ^ sb1) & msk64(h));
 }
 
-/* Spec_Polar_Decoder<16,6> -> Spec_PolarDec_16 -> Spec_P16_ext<6> (library.h:149-172,
- * functions.h:808-818). llr: 16 six-bit SM patterns; fb bit k = frozen-table bit of lane k
- * (1 = information). */
-uint32_t orc_leaf16(const uint32_t *llr, uint32_t fb)
-{
-    return spec_pn_ext(16, LLR_BITS, llr, fb & 0xFFFFu);
-}
+/* Spec_Polar_Decoder<PAR, LLR_BITS> (library.h:149-172 -> functions.h:766-866) */
+static uint64_t leaf_par(const uint32_t *llr, uint64_t fb) { return spec_pn(PAR, LLR_BITS, llr, fb & msk64(PAR)); }
 
-/* ADD_TREE_16_SM<Q> + ADDER_TREE_16<Q> (functions.h:3036-3083, 3190-3205), Q = LLR_BITS.
- * llr: 16 Q-bit SM. old_sum / return: (Q+5)-bit SM (sign bit Q+4: 11 bits at Q = 6). */
-uint32_t orc_rep_add_tree16(const uint32_t *llr, uint32_t old_sum)
+/* PAR = 16 entry point of the primitive tests */
+uint32_t orc_leaf16(const uint32_t *llr, uint32_t fb) { return (uint32_t)spec_pn(16, LLR_BITS, llr, fb & 0xFFFFu); }
+
+/* ADDER_TREE_{PAR}<Q> (functions.h:3163-3320): the pair tree of the word (lanes j and
+ * j + n/2, a = lower lane, one bit wider per level) accumulated into old_sum, a
+ * (Q + LOG2_PAR + 1)-bit pattern.
+ *   SIGMAG: ADD_TREE_{n}_SM (qfull_adder_sm), extended by one bit (sign moved up), then
+ *           VECTOR_FULL_ADDER_SAT_SM<1, Q+L+1> (magnitude clamp 2^(Q+L-1)-1, 511 at Q 6 L 4)
+ *   CA2:    ADD_TREE_{n}_CA2 (exact two's complement), sign-extended, then VECTOR_ADD<1, Q+L+1>
+ *           (qadd: clamp +-(2^(Q+L)-1)) */
+static uint32_t rep_add_tree(int n, const uint32_t *llr, uint32_t old_sum)
 {
-    uint32_t v[16];
-    int n = 16, Q = LLR_BITS;
-    for (int i = 0; i < 16; i++) v[i] = llr[i] & msk(Q);
-    while (n > 1) {  /* ADD_TREE_{n}_SM<Q>: lanes j and j+n/2, a = lower lane */
-        int h = n / 2;
-        for (int j = 0; j < h; j++) v[j] = orc_full_adder_sm(Q, v[j], v[j + h]);
-        n = h;
+    const int L = ilog2(n), Q0 = LLR_BITS, W = Q0 + L + 1;
+    if (g_ca2) {
+        int32_t v[PAR_MAX];
+        for (int i = 0; i < n; i++) v[i] = sx(Q0, llr[i]);
+        for (int m = n; m > 1; m /= 2)
+            for (int j = 0; j < m / 2; j++) v[j] += v[j + m / 2];
+        int32_t s = v[0] + sx(W, old_sum);
+        const int32_t hi = (int32_t)msk(W - 1);
+        s = s > hi ? hi : (s < -hi ? -hi : s);
+        return (uint32_t)s & msk(W);
+    }
+    uint32_t v[PAR_MAX];
+    int Q = Q0;
+    for (int i = 0; i < n; i++) v[i] = llr[i] & msk(Q);
+    for (int m = n; m > 1; m /= 2) {
+        for (int j = 0; j < m / 2; j++) v[j] = orc_full_adder_sm(Q, v[j], v[j + m / 2]);
         Q += 1;
     }
-    /* add_tree is Q+4 bits (sign bit Q+3), extended to the Q+5 bits of the accumulator
-     * (functions.h:3200-3202) */
-    const int W = LLR_BITS + 4;
-    uint32_t add_tree = v[0] & msk(W);
-    uint32_t ext = (((add_tree >> (W - 1)) & 1u) << W) | (add_tree & msk(W - 1));
-    return orc_full_adder_sat_sm(W + 1, ext, old_sum & msk(W + 1));
+    /* add_tree is Q0+L bits (sign bit Q0+L-1), extended to the W bits of the accumulator */
+    uint32_t add_tree = v[0] & msk(W - 1);
+    uint32_t ext = (((add_tree >> (W - 2)) & 1u) << (W - 1)) | (add_tree & msk(W - 2));
+    return orc_full_adder_sat_sm(W, ext, old_sum & msk(W));
 }
 
-/* Min_Mask_16_SM<5> via Min_Mask_TREE_16<6> (functions.h:3652-3747, 3900-3913).
- * Returns (min << 16) | one-hot mask. */
-static void min_mask_rec(int n, const uint32_t *mag, uint32_t *min_out, uint32_t *mask_out, int sel)
+/* PAR = 16 entry point of the primitive tests */
+uint32_t orc_rep_add_tree16(const uint32_t *llr, uint32_t old_sum) { return rep_add_tree(16, llr, old_sum); }
+
+/* Min_Mask_{n}_SM<Q-1> / Min_Mask_{n}_CA2<Q> (functions.h:3450-3747; via Min_Mask_TREE_{n},
+ * :3750-3980) and the SPC(_SPC2)_Min_Mask_* node versions (:1701-2023, 2365-2700):
+ * is_min = mb < ma (mb the upper half; CA2: signed values), the winners recurse, mask =
+ * mask_A & (i_mask, i_mask). sel = 1 (SPC2): the last stage returns mask 11. */
+static void min_mask_rec(int n, const int32_t *mag, int32_t *min_out, uint64_t *mask_out, int sel)
 {
-    if (n == 2) {   /* Min_Mask_2_SM: is_min = mb < ma ; mask = (is_min, ~is_min) */
-        uint32_t is_min = (mag[1] < mag[0]) ? 1u : 0u;
+    if (n == 1) { *min_out = mag[0]; *mask_out = 1; return; }
+    if (n == 2) {
+        uint64_t is_min = (mag[1] < mag[0]) ? 1u : 0u;
         *min_out = is_min ? mag[1] : mag[0];
-        *mask_out = (is_min << 1) | (is_min ^ 1u);
-        if (sel) *mask_out = 3u;   /* SPC_SPC2_Min_Mask_2_SM, sel 1: mask2 = 11 (functions.h:2534-2551) */
+        *mask_out = sel ? 3u : ((is_min << 1) | (is_min ^ 1u));
         return;
     }
     int h = n / 2;
-    uint32_t is_min = 0, m[8];
+    uint64_t is_min = 0;
+    int32_t m[PAR_MAX / 2];
     for (int j = 0; j < h; j++) {
-        uint32_t im = (mag[h + j] < mag[j]) ? 1u : 0u;
+        uint64_t im = (mag[h + j] < mag[j]) ? 1u : 0u;
         is_min |= im << j;
         m[j] = im ? mag[h + j] : mag[j];
     }
-    uint32_t mask_a = (is_min << h) | ((~is_min) & msk(h));
-    uint32_t rmin, imask;
+    uint64_t mask_a = (is_min << h) | ((~is_min) & msk64(h));
+    int32_t rmin;
+    uint64_t imask;
     min_mask_rec(h, m, &rmin, &imask, sel);
-    uint32_t mask_b = (imask << h) | imask;
     *min_out = rmin;
-    *mask_out = mask_a & mask_b;
+    *mask_out = mask_a & ((imask << h) | imask);
 }
 
+/* the magnitudes the min trees compare: VECTOR_ABS_SM (Q-1 bits) or VECTOR_ABS (qabs,
+ * signed Q-bit values) */
+static void mags(int n, const uint32_t *llr, int32_t *mag)
+{
+    for (int i = 0; i < n; i++)
+        mag[i] = g_ca2 ? sx(LLR_BITS, qabs_ca2(LLR_BITS, llr[i])) : (int32_t)(llr[i] & msk(LLR_BITS - 1));
+}
+
+/* MIN_MASK_TREE_FCT<PAR, LLR_BITS> as G_SPC_STATE reads it (my_module.h:1768-1776): the min
+ * field as an unsigned LLR_BITS-bit value, and the one-hot mask */
+static uint32_t min_mask_tree(const uint32_t *llr, uint64_t *mask)
+{
+    int32_t mag[PAR_MAX], mn;
+    mags(PAR, llr, mag);
+    min_mask_rec(PAR, mag, &mn, mask, 0);
+    return (uint32_t)mn & msk(LLR_BITS);
+}
+
+/* PAR = 16 entry point of the primitive tests: (min << 16) | mask */
 uint32_t orc_min_mask16(const uint32_t *llr)
 {
-    uint32_t mag[16];
-    for (int i = 0; i < 16; i++) mag[i] = llr[i] & msk(LLR_BITS - 1);
-    uint32_t mn, mask;
+    int32_t mag[16], mn;
+    uint64_t mask;
+    mags(16, llr, mag);
     min_mask_rec(16, mag, &mn, &mask, 0);
-    return (mn << 16) | (mask & 0xFFFFu);
-}
-
-/* do_prunning group classification (my_module.h:75-155), priority R0 > R1 > REP > SPC
- * (REP2/SPC2 disabled). fb bit k = frozen-table bit 16g+k. */
-int orc_classify_group(uint32_t fb)
-{
-    fb &= 0xFFFFu;
-    if (fb == 0) return NODE_R0;
-    if (fb == 0xFFFFu) return NODE_R1;
-    if (fb == 0x8000u) return NODE_REP;            /* last bit 1, others 0 */
-    if (fb == 0xFFFEu) return NODE_SPC;            /* first bit 0, others 1 */
-    return NODE_RN;
+    return (((uint32_t)mn & msk(LLR_BITS)) << 16) | (uint32_t)(mask & 0xFFFFu);
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -279,83 +375,107 @@ int orc_classify_group(uint32_t fb)
 typedef struct { int pr, r1, rep, spc, rep2, spc2, h0; } orc_cfg_t;
 static const orc_cfg_t ORC_DEFAULT_CFG = { 2, 1, 1, 1, 0, 0, 1 };
 
-/* do_prunning classification with the ELAG switches (my_module.h:86-153): R0 > R1 > REP >
- * SPC > REP2 > SPC2 > RN, nothing but RN at PRUNING_LEVEL 0 */
-static uint32_t classify_cfg(uint32_t fb, const orc_cfg_t *c)
+/* do_prunning classification of one PAR-bit group (my_module.h:75-155) with the ELAG
+ * switches: R0 > R1 > REP (only the last bit information) > SPC (only the first frozen) >
+ * REP2 (the last two) > SPC2 (the first two frozen) > RN; nothing but RN at PRUNING_LEVEL 0 */
+static uint32_t classify_cfg(uint64_t fb, const orc_cfg_t *c)
 {
-    fb &= 0xFFFFu;
+    const uint64_t all = msk64(PAR);
+    fb &= all;
     if (c->pr == 0) return NODE_RN;
     if (fb == 0) return NODE_R0;
-    if (c->r1 && fb == 0xFFFFu) return NODE_R1;
-    if (c->rep && fb == 0x8000u) return NODE_REP;       /* REP_last & ~REP_R0 */
-    if (c->spc && fb == 0xFFFEu) return NODE_SPC;       /* ~SPC_1st & SPC_R1 */
-    if (c->rep2 && fb == 0xC000u) return NODE_REP2;     /* REP_2Last & ~REP_2Last_R0 */
-    if (c->spc2 && fb == 0xFFFCu) return NODE_SPC2;     /* ~SPC_2nd & SPC_2nd_R1 */
+    if (c->r1 && fb == all) return NODE_R1;
+    if (c->rep && fb == 1ull << (PAR - 1)) return NODE_REP;       /* REP_last & ~REP_R0 */
+    if (c->spc && fb == (all & ~1ull)) return NODE_SPC;           /* ~SPC_1st & SPC_R1 */
+    if (c->rep2 && fb == 3ull << (PAR - 2)) return NODE_REP2;     /* REP_2Last & ~REP_2Last_R0 */
+    if (c->spc2 && fb == (all & ~3ull)) return NODE_SPC2;         /* ~SPC_2nd & SPC_2nd_R1 */
     return NODE_RN;
 }
 
-/* REP_REP2_16_SM<Q> (functions.h:1353-1420); sel = 0 is REP_16_SM (functions.h:996-1060):
- * exact SM pair sums (j, j+h), a = lower half, down to two values, then REP_REP2_2_SM:
- * sel 0 -> 16 copies of (|a| < |b| ? sign b : sign a); sel 1 -> (sign b, sign a) repeated,
- * i.e. even positions take sign a, odd positions sign b. */
-uint32_t orc_leaf_rep16(const uint32_t *llr, int sel)
+/* shipped configuration at PAR 16 (primitive tests) */
+int orc_classify_group(uint32_t fb)
 {
-    uint32_t v[16];
-    int n = 16, Q = LLR_BITS;
-    for (int i = 0; i < 16; i++) v[i] = llr[i] & msk(Q);
-    while (n > 2) {
-        int h = n / 2;
-        for (int j = 0; j < h; j++) v[j] = orc_full_adder_sm(Q, v[j], v[j + h]);
-        n = h;
-        Q += 1;
+    int p = g_par;
+    g_par = 16;
+    int r = (int)classify_cfg(fb, &ORC_DEFAULT_CFG);
+    g_par = p;
+    return r;
+}
+
+/* REP_REP2_{n}_SM / _CA2 (functions.h:1229-1500); sel = 0 is REP_{n}_SM / _CA2
+ * (functions.h:870-1224): pair sums (j, j+h), a = lower half, down to two values la, lb,
+ * then sel 0 -> n copies of the sign of la + lb (SM: |la| < |lb| ? sign lb : sign la),
+ * sel 1 -> (sign lb, sign la) repeated: even positions take sign la, odd positions sign lb. */
+static uint64_t leaf_rep(int n, const uint32_t *llr, int sel)
+{
+    uint32_t siga, sigb, sig;
+    if (g_ca2) {
+        int32_t v[PAR_MAX];
+        for (int i = 0; i < n; i++) v[i] = sx(LLR_BITS, llr[i]);
+        for (int m = n; m > 2; m /= 2)
+            for (int j = 0; j < m / 2; j++) v[j] += v[j + m / 2];
+        siga = v[0] < 0; sigb = v[1] < 0; sig = (v[0] + v[1]) < 0;
+    } else {
+        uint32_t v[PAR_MAX];
+        int Q = LLR_BITS;
+        for (int i = 0; i < n; i++) v[i] = llr[i] & msk(Q);
+        for (int m = n; m > 2; m /= 2) {
+            for (int j = 0; j < m / 2; j++) v[j] = orc_full_adder_sm(Q, v[j], v[j + m / 2]);
+            Q += 1;
+        }
+        siga = sgn(Q, v[0]); sigb = sgn(Q, v[1]);
+        uint32_t is_min = ((v[0] & msk(Q - 1)) < (v[1] & msk(Q - 1))) ? 1u : 0u;
+        sig = is_min ? sigb : siga;
     }
-    uint32_t siga = (v[0] >> (Q - 1)) & 1u, sigb = (v[1] >> (Q - 1)) & 1u;
-    uint32_t is_min = ((v[0] & msk(Q - 1)) < (v[1] & msk(Q - 1))) ? 1u : 0u;
-    uint32_t sig = is_min ? sigb : siga, x = 0;
-    for (int i = 0; i < 16; i++) x |= (sel ? ((i & 1) ? sigb : siga) : sig) << i;
+    uint64_t x = 0;
+    for (int i = 0; i < n; i++) x |= (uint64_t)(sel ? ((i & 1) ? sigb : siga) : sig) << i;
     return x;
 }
 
-/* SPC_SPC2_Node_16 SM path (functions.h:2786-2811); sel = 0 is SPC_Node_16
- * (functions.h:2111-2136): x = sign ^ (parity & min_mask). Parity: XOR folds of the sign
- * halves down to two bits (SPC_SPC2_Parity_*, :2254-2300), then sel 0 -> both = their XOR,
- * sel 1 -> kept per position class. Min mask: the Min_Mask tournament, last stage
+uint32_t orc_leaf_rep16(const uint32_t *llr, int sel) { return (uint32_t)leaf_rep(16, llr, sel); }
+
+/* SPC_SPC2_Node_{n} (functions.h:2700-2930); sel = 0 is SPC_Node_{n} (functions.h:2024-2250):
+ * x = sign ^ (parity & min_mask). Parity: XOR folds of the sign halves down to two bits
+ * (SPC(_SPC2)_Parity_*, :1592-1696, 2254-2360), then sel 0 -> both = their XOR, sel 1 ->
+ * kept per position class. Min mask: the tournament on VECTOR_ABS(_SM), last stage
  * (is_min, ~is_min) or, sel 1, 11. */
-uint32_t orc_leaf_spc16(const uint32_t *llr, int sel)
+static uint64_t leaf_spc(int n, const uint32_t *llr, int sel)
 {
-    uint32_t sign = 0, mag[16];
-    for (int i = 0; i < 16; i++) {
-        sign |= ((llr[i] >> (LLR_BITS - 1)) & 1u) << i;
-        mag[i] = llr[i] & msk(LLR_BITS - 1);
-    }
-    uint32_t f = sign;
-    for (int n = 16; n > 2; n /= 2) f = (f & msk(n / 2)) ^ ((f >> (n / 2)) & msk(n / 2));
-    uint32_t p2 = sel ? (f & 3u) : (((f ^ (f >> 1)) & 1u) * 3u);
-    uint32_t parity = 0;
-    for (int i = 0; i < 16; i++) parity |= ((p2 >> (i & 1)) & 1u) << i;
-    uint32_t mn, mask;
-    min_mask_rec(16, mag, &mn, &mask, sel);
-    return (sign ^ (parity & mask)) & 0xFFFFu;
+    uint64_t sign = 0;
+    int32_t mag[PAR_MAX];
+    for (int i = 0; i < n; i++) sign |= (uint64_t)sgn(LLR_BITS, llr[i]) << i;
+    mags(n, llr, mag);
+    uint64_t f = sign;
+    for (int m = n; m > 2; m /= 2) f = (f & msk64(m / 2)) ^ ((f >> (m / 2)) & msk64(m / 2));
+    uint64_t p2 = n == 1 ? 0 : (sel ? (f & 3u) : (((f ^ (f >> 1)) & 1u) * 3u));
+    uint64_t parity = 0;
+    for (int i = 0; i < n; i++) parity |= ((p2 >> (i & 1)) & 1u) << i;
+    int32_t mn;
+    uint64_t mask;
+    min_mask_rec(n, mag, &mn, &mask, sel);
+    return (sign ^ (parity & mask)) & msk64(n);
 }
+
+uint32_t orc_leaf_spc16(const uint32_t *llr, int sel) { return (uint32_t)leaf_spc(16, llr, sel); }
+
+static uint64_t word_sign(const uint32_t *a)
+{ uint64_t s = 0; for (int l = 0; l < PAR; l++) s |= (uint64_t)sgn(LLR_BITS, a[l]) << l; return s; }
 
 /* R_STATE decoder of a group (my_module.h:566-596): the plain leaf, or at PRUNING_LEVEL 1
  * the node decoder of the group's class (type = Node[3:1], sel = Node[0]) */
-static uint32_t leaf_cfg(const uint32_t *llr, uint32_t fb, uint32_t node, const orc_cfg_t *c)
+static uint64_t leaf_cfg(const uint32_t *llr, uint64_t fb, uint32_t node, const orc_cfg_t *c)
 {
     if (c->pr == 1) {
         uint32_t type = (node >> 1) & 7u, sel = node & 1u;
         switch (type) {
         case 0x0: return 0;                                        /* Spec_Node_R0 */
-        case 0x7: if (c->r1) { uint32_t x = 0;                      /* Spec_Node_R1: VECTOR_SIGN */
-                      for (int i = 0; i < 16; i++) x |= ((llr[i] >> (LLR_BITS - 1)) & 1u) << i;
-                      return x; }
-                  break;
-        case 0x1: if (c->rep) return orc_leaf_rep16(llr, c->rep2 ? (int)sel : 0); break;
-        case 0x2: if (c->spc) return orc_leaf_spc16(llr, c->spc2 ? (int)sel : 0); break;
+        case 0x7: if (c->r1) return word_sign(llr); break;          /* Spec_Node_R1: VECTOR_SIGN */
+        case 0x1: if (c->rep) return leaf_rep(PAR, llr, c->rep2 ? (int)sel : 0); break;
+        case 0x2: if (c->spc) return leaf_spc(PAR, llr, c->spc2 ? (int)sel : 0); break;
         default: break;
         }
     }
-    return orc_leaf16(llr, fb);
+    return leaf_par(llr, fb);
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -371,7 +491,7 @@ static uint32_t stk_read(const stk_t *s, int adr) { return s->e[adr - 1]; }
 /* ------------------------------------------------------------------------------------ */
 /* Literal FSM (my_module.h)                                                              */
 /* ------------------------------------------------------------------------------------ */
-typedef uint32_t word_t[PAR];   /* one TYPE_LLRS: 16 six-bit SM patterns */
+typedef uint32_t word_t[PAR_MAX];   /* one TYPE_LLRS: PAR LLR_BITS-bit patterns */
 
 enum { ST_INIT, ST_F, ST_R, ST_G, ST_H, ST_H0, ST_F_REP, ST_G_R1, ST_G_SPC, ST_END, ST_F_R0, ST_COUNT };
 
@@ -379,23 +499,21 @@ typedef struct {
     int N, NDIV, DEPTH_DIV;
     uint32_t cmask;                 /* COUNTER = sc_uint<log2N + 1> */
     word_t *llr_mem_a, *llr_mem_b;
-    uint16_t *bit_mem_1, *bit_mem_2;
-    uint16_t *bit_frozen;
+    uint64_t *bit_mem_1, *bit_mem_2;
+    uint64_t *bit_frozen;
     uint8_t *node_type;
     stk_t nts;                      /* Node_type_stack: 8-bit entries, never reset by INIT */
     long state_count[ST_COUNT];
     orc_cfg_t cfg;                  /* config.h switches (#if branches taken at run time) */
 } fsm_t;
 
-static int ilog2(int v) { int l = 0; while ((1 << l) < v) l++; return l; }
-
 /* my_module::do_prunning (my_module.h:61-166) */
 static void fsm_prune(fsm_t *m, const uint8_t *mask)
 {
     for (int i = 0; i < m->NDIV; i++) {
-        uint32_t tab = 0;
-        for (int k = 0; k < PAR; k++) tab |= (uint32_t)(mask[i * PAR + k] & 1u) << k;
-        m->bit_frozen[i] = (uint16_t)tab;
+        uint64_t tab = 0;
+        for (int k = 0; k < PAR; k++) tab |= (uint64_t)(mask[i * PAR + k] & 1u) << k;
+        m->bit_frozen[i] = tab;
         m->node_type[i] = (uint8_t)classify_cfg(tab, &m->cfg);
     }
 }
@@ -418,12 +536,10 @@ static uint32_t aggregate(const fsm_t *m, int g0, int cnt)
     return NODE_RN;
 }
 
-static void word_F(word_t r, const word_t a, const word_t b)
-{ for (int l = 0; l < PAR; l++) r[l] = orc_F_sm(LLR_BITS, a[l], b[l]); }
-static void word_G(word_t r, const word_t a, const word_t b, uint32_t sa)
-{ for (int l = 0; l < PAR; l++) r[l] = orc_G_sm(LLR_BITS, a[l], b[l], (sa >> l) & 1u); }
-static uint32_t word_sign(const word_t a)
-{ uint32_t s = 0; for (int l = 0; l < PAR; l++) s |= ((a[l] >> (LLR_BITS - 1)) & 1u) << l; return s; }
+static void word_F(uint32_t *r, const uint32_t *a, const uint32_t *b)
+{ for (int l = 0; l < PAR; l++) r[l] = fF(LLR_BITS, a[l], b[l]); }
+static void word_G(uint32_t *r, const uint32_t *a, const uint32_t *b, uint64_t sa)
+{ for (int l = 0; l < PAR; l++) r[l] = fG(LLR_BITS, a[l], b[l], (uint32_t)(sa >> l) & 1u); }
 
 /* the G-type state chosen from the right child's class (my_module.h:495-502, 623-652,
  * 965-993, 1165-1190, 1360-1388): pruned G only at PRUNING_LEVEL 2 with the switch on */
@@ -437,10 +553,11 @@ static int g_next(const fsm_t *m, uint32_t rn)
 
 #define CNT(x) ((x) & m->cmask)
 #define CHK(i) do { if ((uint32_t)(i) >= (uint32_t)m->NDIV) return -100; } while (0)
+#define WCPY(d, s) memcpy((d), (s), sizeof(uint32_t) * (size_t)PAR)
 
 /* one frame through do_action (my_module.h:174-1877); in: N_DIV words (wrapper_in output),
  * out: N_DIV bit words (wrapper_out input) */
-static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
+static int fsm_frame(fsm_t *m, const word_t *in, uint64_t *out)
 {
     const int NDIV = m->NDIV;
     uint32_t ptr_FB = 0, N_REG = 0, NB_ITER = 0;
@@ -458,8 +575,8 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
         m->state_count[st]++;
         switch (st) {
         case ST_INIT: {                                             /* :285-333 */
-            for (int i = 0; i < NDIV / 2; i++) memcpy(m->llr_mem_a[i], in[i], sizeof(word_t));
-            for (int i = 0; i < NDIV / 2; i++) memcpy(m->llr_mem_b[i], in[NDIV / 2 + i], sizeof(word_t));
+            for (int i = 0; i < NDIV / 2; i++) WCPY(m->llr_mem_a[i], in[i]);
+            for (int i = 0; i < NDIV / 2; i++) WCPY(m->llr_mem_b[i], in[NDIV / 2 + i]);
             ptr_FB = 0;
             N_REG = (uint32_t)NDIV;
             adr_a = 0; adr_b = 0;
@@ -487,18 +604,18 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
                 if (isF) {
                     word_F(res, m->llr_mem_a[adr_a], m->llr_mem_b[adr_b]);
                 } else {
-                    uint32_t sa = 0;
+                    uint64_t sa = 0;
                     if (G_stack_value != 2) { CHK(ps_adr); sa = m->bit_mem_1[ps_adr]; }
                     word_G(res, m->llr_mem_a[adr_a], m->llr_mem_b[adr_b], sa);
                 }
-                memcpy(reg_result, res, sizeof(word_t));
+                WCPY(reg_result, res);
                 if (NB_ITER == 1) {
-                    if (isF) { CHK(adr_w_a); memcpy(m->llr_mem_a[adr_w_a], res, sizeof(word_t)); }
-                    else     { CHK(adr_w_b); memcpy(m->llr_mem_b[adr_w_b], res, sizeof(word_t)); }
+                    if (isF) { CHK(adr_w_a); WCPY(m->llr_mem_a[adr_w_a], res); }
+                    else     { CHK(adr_w_b); WCPY(m->llr_mem_b[adr_w_b], res); }
                 } else if (i < (NB_ITER >> 1)) {
-                    CHK(adr_w_a); memcpy(m->llr_mem_a[adr_w_a], res, sizeof(word_t)); adr_w_a = CNT(adr_w_a + 1);
+                    CHK(adr_w_a); WCPY(m->llr_mem_a[adr_w_a], res); adr_w_a = CNT(adr_w_a + 1);
                 } else {
-                    CHK(adr_w_b); memcpy(m->llr_mem_b[adr_w_b], res, sizeof(word_t)); adr_w_b = CNT(adr_w_b + 1);
+                    CHK(adr_w_b); WCPY(m->llr_mem_b[adr_w_b], res); adr_w_b = CNT(adr_w_b + 1);
                 }
                 adr_a = CNT(adr_a + 1); adr_b = CNT(adr_b + 1);
                 if (!isF) ps_adr = CNT(ps_adr + 1);
@@ -543,12 +660,12 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
         }
         case ST_R: {                                                /* :544-665 */
             CHK(ptr_FB);
-            uint32_t is_frozen = m->bit_frozen[ptr_FB];
+            uint64_t is_frozen = m->bit_frozen[ptr_FB];
             uint32_t node = m->node_type[ptr_FB];
             ptr_FB = CNT(ptr_FB + 1);
-            uint32_t ps = leaf_cfg(reg_result, is_frozen, node, &m->cfg);
+            uint64_t ps = leaf_cfg(reg_result, is_frozen, node, &m->cfg);
             CHK(adr_s);
-            m->bit_mem_1[adr_s] = (uint16_t)ps; m->bit_mem_2[adr_s] = (uint16_t)ps;
+            m->bit_mem_1[adr_s] = ps; m->bit_mem_2[adr_s] = ps;
             adr_s = CNT(adr_s + 1);
             uint32_t rn = stk_read(&m->nts, 2) & 0xFu;
             uint32_t condition = stk_read(&stack, 1);
@@ -574,8 +691,7 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             stk_pop(&m->nts, 0x00);
             for (uint32_t i = 0; i < NB_ITER; i++) {
                 CHK(ps_adr_a); CHK(ps_adr_b);
-                uint16_t v = isH ? (uint16_t)(m->bit_mem_1[ps_adr_a] ^ m->bit_mem_2[ps_adr_b])
-                                 : m->bit_mem_2[ps_adr_b];
+                uint64_t v = isH ? (m->bit_mem_1[ps_adr_a] ^ m->bit_mem_2[ps_adr_b]) : m->bit_mem_2[ps_adr_b];
                 m->bit_mem_1[ps_adr_a] = v; m->bit_mem_2[ps_adr_a] = v;
                 ps_adr_a = CNT(ps_adr_a + 1); ps_adr_b = CNT(ps_adr_b + 1);
             }
@@ -603,20 +719,20 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             N_REG = CNT(N_REG >> 1);
             stk_push(&stack, 0);
             stk_push(&m->nts, 0x00);
-            uint32_t sum = 0;   /* sc_bigint<LLR_BITS + LOG2_PAR + 1>: (Q+5)-bit SM pattern */
+            uint32_t sum = 0;   /* sc_bigint<LLR_BITS + LOG2_PAR + 1> pattern */
             for (uint32_t i = 0; i < NB_ITER; i++) {
                 word_t res;
                 CHK(adr_a); CHK(adr_b); CHK(adr_s);
                 word_F(res, m->llr_mem_a[adr_a], m->llr_mem_b[adr_b]);
-                sum = orc_rep_add_tree16(res, sum);
+                sum = rep_add_tree(PAR, res, sum);
                 m->bit_mem_1[adr_s] = 0; m->bit_mem_2[adr_s] = 0;
                 adr_a = CNT(adr_a + 1); adr_b = CNT(adr_b + 1); adr_s = CNT(adr_s + 1);
             }
-            if ((sum >> (LLR_BITS + 4)) & 1u) {   /* VECTOR_SIGN<1, LLR_BITS + LOG2_PAR + 1> */
+            if ((sum >> (LLR_BITS + LOG2_PAR)) & 1u) {   /* VECTOR_SIGN<1, LLR_BITS + LOG2_PAR + 1> */
                 adr_s = CNT(adr_s - NB_ITER);
                 for (uint32_t i = 0; i < NB_ITER; i++) {
                     CHK(adr_s);
-                    m->bit_mem_1[adr_s] = 0xFFFF; m->bit_mem_2[adr_s] = 0xFFFF;
+                    m->bit_mem_1[adr_s] = msk64(PAR); m->bit_mem_2[adr_s] = msk64(PAR);
                     adr_s = CNT(adr_s + 1);
                 }
             }
@@ -652,30 +768,28 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
             NB_ITER = N_REG;
             stk_write(&stack, G_stack_value);
             stk_write(&m->nts, 0x00);
-            uint32_t parity = 0, old_min = 0xFFFFu & msk(LLR_BITS), old_mask = 0, adr_min = 0, sign_min = 0;
+            uint32_t parity = 0, old_min = 0xFFFFu & msk(LLR_BITS), adr_min = 0;
+            uint64_t old_mask = 0, sign_min = 0;
             for (uint32_t i = 0; i < NB_ITER; i++) {
                 word_t res;
                 CHK(adr_a); CHK(adr_b); CHK(adr_s);
-                uint32_t sa = 0;
+                uint64_t sa = 0;
                 if (G_stack_value != 2) { CHK(ps_adr); sa = m->bit_mem_1[ps_adr]; }
                 word_G(res, m->llr_mem_a[adr_a], m->llr_mem_b[adr_b], sa);
-                uint32_t sign = word_sign(res);
-                m->bit_mem_1[adr_s] = (uint16_t)sign; m->bit_mem_2[adr_s] = (uint16_t)sign;
+                uint64_t sign = word_sign(res);
+                m->bit_mem_1[adr_s] = sign; m->bit_mem_2[adr_s] = sign;
                 adr_a = CNT(adr_a + 1); adr_b = CNT(adr_b + 1); ps_adr = CNT(ps_adr + 1); adr_s = CNT(adr_s + 1);
                 if (isSPC) {
-                    uint32_t p = 0;                               /* Parity_TREE_16 */
-                    for (int l = 0; l < PAR; l++) p ^= (sign >> l) & 1u;
-                    parity ^= p;
-                    uint32_t mm = orc_min_mask16(res);            /* MIN_MASK_TREE_FCT */
-                    uint32_t new_min = (mm >> 16) & msk(LLR_BITS);
-                    uint32_t new_mask = mm & 0xFFFFu;
+                    parity ^= (uint32_t)__builtin_parityll(sign);  /* PARITY_TREE_FUNCTION */
+                    uint64_t new_mask;
+                    uint32_t new_min = min_mask_tree(res, &new_mask);   /* MIN_MASK_TREE_FCT */
                     if (new_min < old_min) { old_min = new_min; old_mask = new_mask; adr_min = i; sign_min = sign; }
                 }
             }
             if (isSPC && parity != 0) {
                 uint32_t a = CNT(adr_s - NB_ITER + adr_min);
                 CHK(a);
-                uint16_t v = (uint16_t)(sign_min ^ old_mask);
+                uint64_t v = sign_min ^ old_mask;
                 m->bit_mem_1[a] = v; m->bit_mem_2[a] = v;
             }
             ptr_FB = CNT(ptr_FB + NB_ITER);
@@ -699,17 +813,16 @@ static int fsm_frame(fsm_t *m, const word_t *in, uint16_t *out)
     return -102;
 }
 
-/* wrapper_in (wrapper_in.h:26-44): 6-bit CA2 stream -> SM, 16 per word, lane i = i-th */
-static void wrap_in(const int8_t *llr, int N, word_t *w)
+/* wrapper_in (wrapper_in.h:26-44) + Adapt_format (library.h:18-28): LLR_BITS-bit two's
+ * complement stream -> SIGMAG (qconv_format) or unchanged (CA2), PAR per word */
+static void wrap_in(const int16_t *llr, int N, word_t *w)
 {
-    for (int i = 0; i < N; i++)
-        w[i / PAR][i % PAR] = orc_qconv_format(LLR_BITS, (uint32_t)(uint8_t)llr[i] & msk(LLR_BITS));
+    for (int i = 0; i < N; i++) {
+        uint32_t v = (uint32_t)(uint16_t)llr[i] & msk(LLR_BITS);
+        w[i / PAR][i % PAR] = g_ca2 ? v : orc_qconv_format(LLR_BITS, v);
+    }
 }
 
-/* decode nframes frames with the literal FSM. mask: N bytes (1 = information bit).
- * llr: nframes*N int8 (2's complement, low 6 bits used as sc_bigint<6>).
- * xhat: nframes*N bytes 0/1 (wrapper_out order). Returns 0 or a negative error.
- * state_counts (optional, ST_COUNT longs): per-state visit counts over all frames. */
 static int cfg_from(const int32_t *c7, orc_cfg_t *c)
 {
     *c = ORC_DEFAULT_CFG;
@@ -718,21 +831,16 @@ static int cfg_from(const int32_t *c7, orc_cfg_t *c)
     return (c->pr < 0 || c->pr > 2) ? -22 : 0;
 }
 
-int orc_decode_fsm_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
-                       long *state_counts, const int32_t *cfg7);
-
-int orc_decode_fsm(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
-                   long *state_counts)
-{
-    return orc_decode_fsm_cfg(N, mask, llr, xhat, nframes, state_counts, NULL);
-}
-
-/* cfg7 = {PRUNING_LEVEL, ELAG_R1, ELAG_REP, ELAG_SPC, ELAG_REP2, ELAG_SPC2, ELAG_H0}, NULL =
+/* decode nframes frames with the literal FSM. mask: N bytes (1 = information bit).
+ * llr: nframes*N int16 (2's complement, the low LLR_BITS used as sc_bigint<LLR_BITS>).
+ * xhat: nframes*N bytes 0/1 (wrapper_out order). Returns 0 or a negative error.
+ * state_counts (optional, ST_COUNT longs): per-state visit counts over all frames.
+ * cfg7 = {PRUNING_LEVEL, ELAG_R1, ELAG_REP, ELAG_SPC, ELAG_REP2, ELAG_SPC2, ELAG_H0}, NULL =
  * the shipped config.h */
-int orc_decode_fsm_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
-                       long *state_counts, const int32_t *cfg7)
+int orc_decode_fsm16(int N, const uint8_t *mask, const int16_t *llr, uint8_t *xhat, int nframes,
+                     long *state_counts, const int32_t *cfg7)
 {
-    if (N < 32 || (N & (N - 1)) != 0) return -22;
+    if (N < 2 * PAR || (N & (N - 1)) != 0) return -22;         /* INIT needs N_DIV >= 2 */
     fsm_t m;
     memset(&m, 0, sizeof m);
     if (cfg_from(cfg7, &m.cfg)) return -22;
@@ -742,12 +850,12 @@ int orc_decode_fsm_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *x
     m.nts.D = m.DEPTH_DIV;
     m.llr_mem_a = (word_t *)calloc((size_t)m.NDIV, sizeof(word_t));
     m.llr_mem_b = (word_t *)calloc((size_t)m.NDIV, sizeof(word_t));
-    m.bit_mem_1 = (uint16_t *)calloc((size_t)m.NDIV, 2);
-    m.bit_mem_2 = (uint16_t *)calloc((size_t)m.NDIV, 2);
-    m.bit_frozen = (uint16_t *)calloc((size_t)m.NDIV, 2);
+    m.bit_mem_1 = (uint64_t *)calloc((size_t)m.NDIV, 8);
+    m.bit_mem_2 = (uint64_t *)calloc((size_t)m.NDIV, 8);
+    m.bit_frozen = (uint64_t *)calloc((size_t)m.NDIV, 8);
     m.node_type = (uint8_t *)calloc((size_t)m.NDIV, 1);
     word_t *in = (word_t *)calloc((size_t)m.NDIV, sizeof(word_t));
-    uint16_t *out = (uint16_t *)calloc((size_t)m.NDIV, 2);
+    uint64_t *out = (uint64_t *)calloc((size_t)m.NDIV, 8);
     int rc = 0;
     if (!m.llr_mem_a || !m.llr_mem_b || !m.bit_mem_1 || !m.bit_mem_2 || !m.bit_frozen ||
         !m.node_type || !in || !out) { rc = -12; goto done; }
@@ -765,14 +873,39 @@ done:
     return rc;
 }
 
+static int16_t *widen(const int8_t *llr, size_t n)
+{
+    int16_t *w = (int16_t *)malloc((n ? n : 1) * sizeof(int16_t));
+    if (w) for (size_t i = 0; i < n; i++) w[i] = llr[i];
+    return w;
+}
+
+/* int8 channel (LLR_BITS <= 8) */
+int orc_decode_fsm_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
+                       long *state_counts, const int32_t *cfg7)
+{
+    if (N < 1 || nframes < 0) return -22;
+    int16_t *w = widen(llr, (size_t)N * (size_t)nframes);
+    if (!w) return -12;
+    int rc = orc_decode_fsm16(N, mask, w, xhat, nframes, state_counts, cfg7);
+    free(w);
+    return rc;
+}
+
+int orc_decode_fsm(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
+                   long *state_counts)
+{
+    return orc_decode_fsm_cfg(N, mask, llr, xhat, nframes, state_counts, NULL);
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* Recursive restatement -- independent of the FSM registers     */
 /* ------------------------------------------------------------------------------------ */
 typedef struct {
     int G;
-    const uint16_t *fb;     /* per group */
+    const uint64_t *fb;     /* per group */
     const uint8_t *type;    /* per group */
-    uint16_t *x;            /* per group, encoded bits */
+    uint64_t *x;            /* per group, encoded bits */
     orc_cfg_t cfg;
 } rec_t;
 
@@ -793,10 +926,17 @@ static uint32_t node_type(const rec_t *r, int g0, int cnt)
     return NODE_RN;
 }
 
-/* decode node covering groups [g0, g0+cnt) with LLR words lam[0..cnt) (6-bit SM) */
+static uint32_t bitrev(uint32_t v, int bits)
+{
+    uint32_t r = 0;
+    for (int b = 0; b < bits; b++) r |= ((v >> b) & 1u) << (bits - 1 - b);
+    return r;
+}
+
+/* decode node covering groups [g0, g0+cnt) with LLR words lam[0..cnt) */
 static void rec_node(rec_t *r, int g0, int cnt, const word_t *lam, int is_root)
 {
-    if (cnt == 1) { r->x[g0] = (uint16_t)leaf_cfg(lam[0], r->fb[g0], r->type[g0], &r->cfg); return; }
+    if (cnt == 1) { r->x[g0] = leaf_cfg(lam[0], r->fb[g0], r->type[g0], &r->cfg); return; }
     int h = cnt / 2;
     /* node pruning at PRUNING_LEVEL 2 only, each kind behind its switch; REP2 / SPC2
      * classes are never pruned above the leaves (node_type returns RN for them) */
@@ -813,8 +953,8 @@ static void rec_node(rec_t *r, int g0, int cnt, const word_t *lam, int is_root)
         for (int i = 0; i < h; i++) r->x[g0 + i] = 0;
     } else if (tl == NODE_REP) {
         uint32_t acc = 0;
-        for (int i = 0; i < h; i++) { word_t t; word_F(t, lam[i], lam[h + i]); acc = orc_rep_add_tree16(t, acc); }
-        uint16_t d = ((acc >> (LLR_BITS + 4)) & 1u) ? 0xFFFF : 0;
+        for (int i = 0; i < h; i++) { word_t t; word_F(t, lam[i], lam[h + i]); acc = rep_add_tree(PAR, t, acc); }
+        uint64_t d = ((acc >> (LLR_BITS + LOG2_PAR)) & 1u) ? msk64(PAR) : 0;
         for (int i = 0; i < h; i++) r->x[g0 + i] = d;
     } else {
         for (int i = 0; i < h; i++) word_F(child[i], lam[i], lam[h + i]);
@@ -823,55 +963,51 @@ static void rec_node(rec_t *r, int g0, int cnt, const word_t *lam, int is_root)
     /* right child: lambda = G(a, b, x_left) (saturated) */
     for (int i = 0; i < h; i++) word_G(child[i], lam[i], lam[h + i], left_zero ? 0u : r->x[g0 + i]);
     if (tr == NODE_R1) {
-        for (int i = 0; i < h; i++) r->x[g0 + h + i] = (uint16_t)word_sign(child[i]);
+        for (int i = 0; i < h; i++) r->x[g0 + h + i] = word_sign(child[i]);
     } else if (tr == NODE_SPC) {
         /* Wagner: parity of hard decisions; flip the min |lambda| position
-         * (lexicographic (|l|, group, bitrev4(lane)) -- equivalent to the in-group tournament
-         * of Min_Mask_16_SM plus the strict '<' across groups) */
-        uint32_t parity = 0, best = 0xFFFFFFFFu; int bg = 0, bl = 0;
+         * (lexicographic (|l|, group, bitrev_LOG2PAR(lane)) -- equivalent to the in-group
+         * tournament of Min_Mask_PAR plus the strict '<' across groups) */
+        uint32_t parity = 0;
+        uint64_t best = ~0ull;
+        int bg = 0, bl = 0;
         for (int i = 0; i < h; i++) {
-            uint32_t s = word_sign(child[i]);
-            r->x[g0 + h + i] = (uint16_t)s;
+            uint64_t s = word_sign(child[i]);
+            r->x[g0 + h + i] = s;
+            int32_t mag[PAR_MAX];
+            mags(PAR, child[i], mag);
             for (int l = 0; l < PAR; l++) {
-                parity ^= (s >> l) & 1u;
-                uint32_t br = ((l & 1) << 3) | ((l & 2) << 1) | ((l & 4) >> 1) | ((l & 8) >> 3);
-                uint32_t key = ((child[i][l] & msk(LLR_BITS - 1)) << 24) | ((uint32_t)i << 4) | br;
+                parity ^= (uint32_t)(s >> l) & 1u;
+                uint64_t key = ((uint64_t)((uint32_t)mag[l] & msk(LLR_BITS)) << 40) | ((uint64_t)i << 8) |
+                               bitrev((uint32_t)l, LOG2_PAR);
                 if (key < best) { best = key; bg = i; bl = l; }
             }
         }
-        if (parity) r->x[g0 + h + bg] ^= (uint16_t)(1u << bl);
+        if (parity) r->x[g0 + h + bg] ^= 1ull << bl;
     } else {
         rec_node(r, g0 + h, h, child, 0);
     }
     /* combine: H (xor) or H0 (copy) */
-    for (int i = 0; i < h; i++) r->x[g0 + i] = left_zero ? r->x[g0 + h + i] : (uint16_t)(r->x[g0 + i] ^ r->x[g0 + h + i]);
+    for (int i = 0; i < h; i++) r->x[g0 + i] = left_zero ? r->x[g0 + h + i] : (r->x[g0 + i] ^ r->x[g0 + h + i]);
     free(child);
 }
 
-int orc_decode_rec_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
-                       const int32_t *cfg7);
-
-int orc_decode_rec(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes)
+int orc_decode_rec16(int N, const uint8_t *mask, const int16_t *llr, uint8_t *xhat, int nframes,
+                     const int32_t *cfg7)
 {
-    return orc_decode_rec_cfg(N, mask, llr, xhat, nframes, NULL);
-}
-
-int orc_decode_rec_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
-                       const int32_t *cfg7)
-{
-    if (N < 32 || (N & (N - 1)) != 0) return -22;
+    if (N < 2 * PAR || (N & (N - 1)) != 0) return -22;
     orc_cfg_t cfg;
     if (cfg_from(cfg7, &cfg)) return -22;
     int G = N / PAR;
-    uint16_t *fb = (uint16_t *)calloc((size_t)G, 2);
+    uint64_t *fb = (uint64_t *)calloc((size_t)G, 8);
     uint8_t *type = (uint8_t *)calloc((size_t)G, 1);
-    uint16_t *x = (uint16_t *)calloc((size_t)G, 2);
+    uint64_t *x = (uint64_t *)calloc((size_t)G, 8);
     word_t *in = (word_t *)calloc((size_t)G, sizeof(word_t));
     if (!fb || !type || !x || !in) { free(fb); free(type); free(x); free(in); return -12; }
     for (int g = 0; g < G; g++) {
-        uint32_t t = 0;
-        for (int k = 0; k < PAR; k++) t |= (uint32_t)(mask[g * PAR + k] & 1u) << k;
-        fb[g] = (uint16_t)t; type[g] = (uint8_t)classify_cfg(t, &cfg);
+        uint64_t t = 0;
+        for (int k = 0; k < PAR; k++) t |= (uint64_t)(mask[g * PAR + k] & 1u) << k;
+        fb[g] = t; type[g] = (uint8_t)classify_cfg(t, &cfg);
     }
     rec_t r = { G, fb, type, x, cfg };
     for (int f = 0; f < nframes; f++) {
@@ -881,6 +1017,22 @@ int orc_decode_rec_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *x
     }
     free(fb); free(type); free(x); free(in);
     return 0;
+}
+
+int orc_decode_rec_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
+                       const int32_t *cfg7)
+{
+    if (N < 1 || nframes < 0) return -22;
+    int16_t *w = widen(llr, (size_t)N * (size_t)nframes);
+    if (!w) return -12;
+    int rc = orc_decode_rec16(N, mask, w, xhat, nframes, cfg7);
+    free(w);
+    return rc;
+}
+
+int orc_decode_rec(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes)
+{
+    return orc_decode_rec_cfg(N, mask, llr, xhat, nframes, NULL);
 }
 
 /* ------------------------------------------------------------------------------------ */

@@ -9,6 +9,7 @@
 #include <string.h>
 
 int orc_set_llr_bits(int q);
+int orc_set_format(int q, int par, int ca2, int ext);
 int orc_decode_fsm_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
                        long *state_counts, const int32_t *cfg7);
 int orc_decode_rec_cfg(int N, const uint8_t *mask, const int8_t *llr, uint8_t *xhat, int nframes,
@@ -34,9 +35,10 @@ int main(void)
     const int ncfg = (int)(sizeof cfgs / sizeof cfgs[0]);
     int bad = 0, runs = 0;
     for (int it = 0; it < 120; it++) {
-        const int N = 32 << (rnd() % 7);                 /* 32 .. 2048 */
+        const int par = 2 << (rnd() % 6);                /* PAR 2 .. 64 */
+        const int N = (2 * par > 32 ? 2 * par : 32) << (rnd() % 6);
         const int B = 1 + (int)(rnd() % 3);
-        const int q = 5 + (int)(rnd() % 4);
+        const int q = 5 + (int)(rnd() % 5);
         uint8_t *mask = malloc((size_t)N);
         int8_t *llr = malloc((size_t)N * B);
         uint8_t *x1 = malloc((size_t)N * B), *x2 = malloc((size_t)N * B);
@@ -46,7 +48,7 @@ int main(void)
             const uint32_t k = rnd() % 8;
             llr[i] = k == 0 ? (int8_t)-32 : k == 1 ? 0 : (int8_t)(rnd() & 0xFFu);
         }
-        orc_set_llr_bits(q);
+        if (orc_set_format(q, par, (int)(rnd() & 1u), (int)(rnd() & 1u))) bad++;
         const int32_t *c = cfgs[rnd() % ncfg];
         long counts[16] = {0};
         int r1 = orc_decode_fsm_cfg(N, mask, llr, x1, B, counts, c);
@@ -58,7 +60,7 @@ int main(void)
         }
         free(mask); free(llr); free(x1); free(x2);
     }
-    orc_set_llr_bits(6);
+    orc_set_format(6, 16, 0, 1);
     /* frame source + error counter */
     {
         const int N = 1024, B = 5;

@@ -121,4 +121,4 @@ def test_fsm_equals_recursive_other_llr_bits(oracle_mod, q):
     llr, _ = util.synth_frames(mask, 6, ebn0_db=1.0, seed=5)
     np.testing.assert_array_equal(oracle_mod.decode_fsm(mask, llr, llr_bits=6), oracle_mod.decode_fsm(mask, llr))
     with pytest.raises(ValueError):
-        oracle_mod.decode_fsm(mask, llr, llr_bits=9)
+        oracle_mod.decode_fsm(mask, llr, llr_bits=10)

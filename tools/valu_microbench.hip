@@ -1,106 +1,119 @@
-// VALU issue-cost microbenchmark for gfx950: throughput (cycles per wave-instruction per
-// SIMD) of the instruction classes the decode kernels use, with 8 waves per SIMD and 8
-// independent chains per wave (no dependency stalls).
-// build: hipcc --offload-arch=gfx950 -O3 tools/valu_microbench.hip -o /tmp/valu_mb
+// VALU issue-cost microbenchmark for gfx950, timed in-kernel with the shader clock
+// (s_memtime = shader cycles, MI355X_MICROARCH.md 'Per-instruction cycle constants') so that
+// no clock has to be assumed. For each instruction class the decoder issues:
+//   * throughput: cycles per wave64 instruction per SIMD at 1, 2, 4 and 8 waves per SIMD,
+//     8 independent chains per wave (no dependency stalls);
+//   * latency: one dependent chain, one wave per SIMD.
+// Every wave stamps s_memtime around its loop; cycles per SIMD-instruction =
+// median(wave delta) / (instructions per wave * waves per SIMD). The clock itself is
+// reported as s_memtime ticks / s_memrealtime (100 MHz) ticks.
+// build: hipcc --offload-arch=gfx950 -O3 tools/valu_microbench.hip -o build_tools/valu_mb
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #define REP8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 
 template <int OP>
-__global__ void __launch_bounds__(256) bench(unsigned *out, int iters)
+__device__ __forceinline__ void op(unsigned &r, unsigned k)
 {
-    unsigned r0 = threadIdx.x, r1 = r0 * 3, r2 = r0 * 5, r3 = r0 * 7, r4 = r0 * 11, r5 = r0 * 13, r6 = r0 * 17,
-             r7 = r0 * 19, k = 0x01230123u;
-    for (int i = 0; i < iters; i++) {
-#define OPX(n)                                                                                            \
-    if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(r##n) : "v"(k));                 \
-    if constexpr (OP == 1) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r##n) : "v"(k));                 \
-    if constexpr (OP == 2) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(r##n) : "v"(k));              \
-    if constexpr (OP == 3) asm volatile("v_pk_min_u16 %0, %0, %1" : "+v"(r##n) : "v"(k));              \
-    if constexpr (OP == 4) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x36" : "+v"(r##n) : "v"(k)); \
-    if constexpr (OP == 5) asm volatile("v_mov_b32_dpp %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf" : "+v"(r##n)); \
-    if constexpr (OP == 6) asm volatile("v_add_u32_dpp %0, %0, %1 row_ror:8 row_mask:0xf bank_mask:0xf" : "+v"(r##n) : "v"(k)); \
-    if constexpr (OP == 7) asm volatile("v_and_or_b32 %0, %0, %1, %1" : "+v"(r##n) : "v"(k));          \
-    if constexpr (OP == 8) asm volatile("v_pk_ashrrev_i16 %0, 15, %0" : "+v"(r##n));                    \
-    if constexpr (OP == 9) asm volatile("v_add_f32 %0, %0, %1" : "+v"(r##n) : "v"(k));                 \
-    if constexpr (OP == 10) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(r##n));                       \
-    if constexpr (OP == 11) asm volatile("v_bfi_b32 %0, %0, %1, %1" : "+v"(r##n) : "v"(k));             \
-    if constexpr (OP == 12) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(r##n)); \
-    if constexpr (OP == 13) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(*(double *)&r##n) : "v"(*(double *)&k)); \
-    if constexpr (OP == 14) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(r##n) : "v"(k));            \
-    if constexpr (OP == 15) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(r##n) : "v"(k));       \
-    if constexpr (OP == 16) asm volatile("v_pk_mad_u16 %0, %0, %1, %1" : "+v"(r##n) : "v"(k));          \
-    if constexpr (OP == 17) asm volatile("v_min_u32 %0, %0, %1" : "+v"(r##n) : "v"(k));                 \
-    if constexpr (OP == 18) asm volatile("v_xor_b32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(r##n) : "v"(k)); \
-    if constexpr (OP == 19) asm volatile("v_min3_u32 %0, %0, %1, %1" : "+v"(r##n) : "v"(k));
-        REP8(OPX)
-    }
-    out[blockIdx.x * 256 + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;
+    if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 1) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 2) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 3) asm volatile("v_pk_min_u16 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 4) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x36" : "+v"(r) : "v"(k));
+    if constexpr (OP == 5) asm volatile("v_mov_b32_dpp %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf" : "+v"(r));
+    if constexpr (OP == 6) asm volatile("v_add_u32_dpp %0, %0, %1 row_ror:8 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
+    if constexpr (OP == 7) asm volatile("v_and_or_b32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 8) asm volatile("v_pk_ashrrev_i16 %0, 15, %0" : "+v"(r));
+    if constexpr (OP == 9) asm volatile("v_add_f32 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 10) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 11) asm volatile("v_pk_mad_u16 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 12) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 13) asm volatile("v_xor_b32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
+    if constexpr (OP == 14) asm volatile("v_min3_u32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
 }
-
 static const char *names[] = {"v_add_u32", "v_xor_b32", "v_pk_add_u16", "v_pk_min_u16", "v_bitop3_b32",
-                              "v_mov_b32_dpp row_ror", "v_add_u32_dpp", "v_and_or_b32", "v_pk_ashrrev_i16",
-                              "v_add_f32", "v_lshlrev_b32", "v_bfi_b32", "v_mov_b32_dpp quad_perm", "v_pk_add_f32",
-                              "v_perm_b32", "v_cndmask_b32", "v_pk_mad_u16", "v_min_u32", "v_xor_b32_dpp",
-                              "v_min3_u32"};
+                              "v_mov_b32_dpp row_ror", "v_add_u32_dpp row_ror", "v_and_or_b32",
+                              "v_pk_ashrrev_i16", "v_add_f32", "v_fma_f32", "v_pk_mad_u16", "v_perm_b32",
+                              "v_xor_b32_dpp quad_perm", "v_min3_u32"};
+constexpr int NOPS = 15;
 
-template <int OP>
-double run(unsigned *buf, int blocks, int iters)
+// CHAINS independent accumulators per wave; stamps[wave] = {memtime delta, memrealtime delta}
+template <int OP, int CHAINS>
+__global__ void __launch_bounds__(256) bench(unsigned *out, unsigned long long *stamps, int iters)
 {
-    hipEvent_t a, b;
-    hipEventCreate(&a);
-    hipEventCreate(&b);
-    bench<OP><<<blocks, 256>>>(buf, iters);
-    hipEventRecord(a);
-    bench<OP><<<blocks, 256>>>(buf, iters);
-    hipEventRecord(b);
-    hipEventSynchronize(b);
-    float ms = 0;
-    hipEventElapsedTime(&ms, a, b);
-    return ms;
+    unsigned r[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) r[c] = threadIdx.x * (2 * c + 3);
+    const unsigned k = 0x01230123u;
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), w0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int rep = 0; rep < 8 / CHAINS; rep++) {
+#pragma unroll
+            for (int c = 0; c < CHAINS; c++) op<OP>(r[c], k);
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), w1 = __builtin_amdgcn_s_memrealtime();
+    unsigned x = 0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) x ^= r[c];
+    out[blockIdx.x * 256 + threadIdx.x] = x;
+    if ((threadIdx.x & 63) == 0) {
+        const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+        stamps[2 * w] = t1 - t0;
+        stamps[2 * w + 1] = w1 - w0;
+    }
+}
+
+template <int OP, int CHAINS>
+void one(unsigned *buf, unsigned long long *st, int cus, int wps)
+{
+    const int iters = 2048, blocks = cus * wps;   // 256-thread blocks: one wave per SIMD each
+    hipLaunchKernelGGL((bench<OP, CHAINS>), dim3(blocks), dim3(256), 0, 0, buf, st, iters);   // warm
+    hipLaunchKernelGGL((bench<OP, CHAINS>), dim3(blocks), dim3(256), 0, 0, buf, st, iters);
+    hipDeviceSynchronize();
+    std::vector<unsigned long long> h(2 * blocks * 4);
+    hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost);
+    std::vector<double> cyc, ghz;
+    for (int w = 0; w < blocks * 4; w++) {
+        cyc.push_back((double)h[2 * w]);
+        ghz.push_back(h[2 * w + 1] ? (double)h[2 * w] / (double)h[2 * w + 1] / 10.0 : 0.0);
+    }
+    std::sort(cyc.begin(), cyc.end());
+    std::sort(ghz.begin(), ghz.end());
+    const double insts = 8.0 * iters;
+    const double med = cyc[cyc.size() / 2];
+    // CHAINS == 8: throughput per SIMD (waves share the SIMD); CHAINS == 1: dependent latency
+    printf("{\"op\": \"%s\", \"chains\": %d, \"waves_per_simd\": %d, \"cycles_per_wave_inst_per_simd\": %.3f, "
+           "\"cycles_per_inst_in_wave\": %.3f, \"clock_ghz\": %.3f}\n",
+           names[OP], CHAINS, wps, med / insts / wps, med / insts, ghz[ghz.size() / 2]);
 }
 
 template <int OP>
-void one(unsigned *buf, int cus, double ghz)
+void all(unsigned *buf, unsigned long long *st, int cus)
 {
-    const int waves_per_simd = 8, iters = 4096;
-    const int blocks = cus * waves_per_simd;   // 4 waves per block -> one per SIMD
-    double ms = run<OP>(buf, blocks, iters);
-    double insts_per_simd = (double)waves_per_simd * iters * 8;
-    double cyc = ms * 1e-3 * ghz * 1e9 / insts_per_simd;
-    printf("{\"op\": \"%s\", \"ms\": %.4f, \"cycles_per_wave_inst\": %.3f}\n", names[OP], ms, cyc);
+    for (int wps : {1, 2, 4, 8}) one<OP, 8>(buf, st, cus, wps);
+    one<OP, 1>(buf, st, cus, 1);
+    if constexpr (OP + 1 < NOPS) all<OP + 1>(buf, st, cus);
 }
 
-int main(int argc, char **argv)
+int main()
 {
-    double ghz = argc > 1 ? atof(argv[1]) : 2.4;
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, 0);
+    const int cus = prop.multiProcessorCount;
     unsigned *buf;
-    hipMalloc(&buf, (size_t)prop.multiProcessorCount * 8 * 256 * 4);
-    one<0>(buf, prop.multiProcessorCount, ghz);
-    one<1>(buf, prop.multiProcessorCount, ghz);
-    one<2>(buf, prop.multiProcessorCount, ghz);
-    one<3>(buf, prop.multiProcessorCount, ghz);
-    one<4>(buf, prop.multiProcessorCount, ghz);
-    one<5>(buf, prop.multiProcessorCount, ghz);
-    one<6>(buf, prop.multiProcessorCount, ghz);
-    one<7>(buf, prop.multiProcessorCount, ghz);
-    one<8>(buf, prop.multiProcessorCount, ghz);
-    one<9>(buf, prop.multiProcessorCount, ghz);
-    one<10>(buf, prop.multiProcessorCount, ghz);
-    one<11>(buf, prop.multiProcessorCount, ghz);
-    one<12>(buf, prop.multiProcessorCount, ghz);
-    one<13>(buf, prop.multiProcessorCount, ghz);
-    one<14>(buf, prop.multiProcessorCount, ghz);
-    one<15>(buf, prop.multiProcessorCount, ghz);
-    one<16>(buf, prop.multiProcessorCount, ghz);
-    one<17>(buf, prop.multiProcessorCount, ghz);
-    one<18>(buf, prop.multiProcessorCount, ghz);
-    one<19>(buf, prop.multiProcessorCount, ghz);
+    unsigned long long *st;
+    hipMalloc(&buf, (size_t)cus * 8 * 256 * 4);
+    hipMalloc(&st, (size_t)cus * 8 * 4 * 2 * 8);
+    all<0>(buf, st, cus);
     hipFree(buf);
+    hipFree(st);
     return 0;
 }
