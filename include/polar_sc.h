@@ -33,12 +33,20 @@ extern "C" {
 /*
  * Decoder configuration. Mirrors the compile-time switches of the reference's
  * src/module/config.h:2-30 (+ PAR from polar_parameters.h:8). The default
- * (polar_sc_default_config) is the configuration the reference ships. Also accepted: the
- * pruning sweep of script/script_tests.sh:103-122, i.e. pruning_level 0/1/2 with any
- * combination of elag_r1 / elag_rep / elag_spc / elag_rep2 / elag_spc2 / elag_h0, at
- * llr_bits 5..8 (the sweep itself runs at QUANT = 8, script_tests.sh:9,25; the LLR is the low
- * llr_bits of each int8). elag_rare = 1 (does not compile in the reference, my_module.h:255
- * vs :1511) and any other par / sigmag / extended are rejected with -ENOTSUP.
+ * (polar_sc_default_config) is the configuration the reference ships. Also accepted, the
+ * design space the reference's scripts sweep:
+ *   * pruning_level 0/1/2 with any combination of elag_r1 / elag_rep / elag_spc / elag_rep2 /
+ *     elag_spc2 / elag_h0 (script/script_tests.sh:103-122);
+ *   * llr_bits 5..9 (QUANT, script/parser.sh:12, parser_comp.sh:12): the LLR is the low
+ *     llr_bits of each channel value (int8 frames, or int16 frames via polar_sc_decode_i16);
+ *   * sigmag 1 (SIGMAG) or 0 (CA2, the two's complement datapath of functions.h:48-118)
+ *     (script/parser.sh:15,43);
+ *   * extended 1/0 (config.h:14: exact or saturating leaves);
+ *   * par 16, 32 or 64 (script_tests.sh:11 runs 16 and 64).
+ * The shipped datapath (sigmag 1, par 16, extended 1, llr_bits <= 8) runs the specialised
+ * kernels; every other format runs the schedule interpreter compiled for it. elag_rare = 1
+ * (does not compile in the reference, my_module.h:255 vs :1511) and par below 16 are rejected
+ * with -ENOTSUP.
  */
 typedef struct polar_sc_config {
     int32_t llr_bits;       /* LLR_BITS            (config.h:2)      default 6  */
@@ -74,8 +82,11 @@ typedef struct polar_sc_op {
     int32_t n;      /* words (16 LLRs / 16 bits) per operand half */
     int32_t pos;    /* first bit_mem word written (or combined, for H/H0) */
     int32_t upos;   /* first bit_mem word of partial sums for G-type ops, -1 = zero (H0 route) */
-    uint32_t fb;    /* leaf ops only: bits 0..15 frozen pattern of the group, bits 16..18 the
-                       leaf decoder (POLAR_LEAF_*; non-plain only at pruning_level 1) */
+    uint32_t fb;    /* leaf ops: bits 0..15 frozen pattern of the 16-LLR word, bits 16..18 the
+                       leaf decoder (POLAR_LEAF_*; non-plain only at pruning_level 1).
+                       PAR > 16 leaves (expanded into F / G / FLEAF / GLEAF / H records):
+                       bit 19 = G_extended (no clamp), bits 20..23 = operand width above
+                       llr_bits */
     int32_t reserved[2];
 } polar_sc_op;
 
@@ -89,7 +100,9 @@ enum {
     POLAR_OP_SPC = 7,    /* G_SPC_STATE              (my_module.h:1737-1842) */
     POLAR_OP_H = 8,      /* H_STATE                  (my_module.h:881-998)   */
     POLAR_OP_H0 = 9,     /* H0_STATE                 (my_module.h:1002-1104) */
-    POLAR_OP_END = 10    /* END                      (my_module.h:1848-1869) */
+    POLAR_OP_END = 10,   /* END                      (my_module.h:1848-1869) */
+    POLAR_OP_PLEAF = 14  /* PAR > 16: R_STATE PRUNING_LEVEL 1 decoder (fb bits 16..18) of the
+                            PAR word whose n words are the level-`level` node at pos */
 };
 
 /* leaf decoders of R_STATE at PRUNING_LEVEL 1 (my_module.h:566-593) */
@@ -102,7 +115,7 @@ enum {
 };
 
 typedef struct polar_sc_plan_stats {
-    uint32_t N, K, groups;            /* N, information bits, N/16                    */
+    uint32_t N, K, groups;            /* N, information bits, N/PAR (do_prunning groups) */
     uint32_t n_r0, n_r1, n_rep, n_spc, n_rn;   /* do_prunning group census          */
     uint32_t n_ops;                   /* schedule length (incl. END)                   */
     uint32_t op_count[16];            /* per POLAR_OP_* code                           */
@@ -151,6 +164,12 @@ int polar_sc_decode(const polar_sc_plan *plan, const int8_t *llr_dev, uint64_t *
 /* Same, with the output as [batch][N/16] uint16 words (bit i of word j = x^[16 j + i]),
  * which is exactly the sequence of TYPE_BITS tokens my_module writes to its `s` port. */
 int polar_sc_decode_u16(const polar_sc_plan *plan, const int8_t *llr_dev, uint16_t *bits_dev,
+                        size_t batch, void *stream);
+
+/* Same as polar_sc_decode with int16 channel values ([batch][N] int16, the low llr_bits of
+ * each are the LLR): the channel for 9-bit LLRs beyond the int8 range (LLR_BITS 9,
+ * script/parser_comp.sh:12). Runs the schedule interpreter of the plan's format. */
+int polar_sc_decode_i16(const polar_sc_plan *plan, const int16_t *llr_dev, uint64_t *hard_bits_dev,
                         size_t batch, void *stream);
 
 /* Upload the schedule and reserve device scratch for up to max_batch frames on the

@@ -28,7 +28,7 @@ __all__ = [
 
 build = _build.build
 
-OPS = {1: "F", 2: "G", 3: "FLEAF", 4: "GLEAF", 5: "REP", 6: "R1", 7: "SPC", 8: "H", 9: "H0", 10: "END"}
+OPS = {1: "F", 2: "G", 3: "FLEAF", 4: "GLEAF", 5: "REP", 6: "R1", 7: "SPC", 8: "H", 9: "H0", 10: "END", 14: "PLEAF"}
 # device-only records of polar_sc_trace (include/polar_sc.h)
 TRACE_OPS = {**OPS, 11: "WOPEN", 12: "WFLUSH", 13: "SUB"}
 
@@ -82,7 +82,7 @@ EXPORTS = (
     "polar_sc_abi_version", "polar_sc_plan_compile", "polar_sc_plan_kernel_source",
     "polar_csim_frames", "polar_csim_states", "polar_count_errors",
     "polar_mask_from_order", "polar_write_frozen_tab", "polar_write_parameters_h", "polar_parse_parameters_h",
-    "polar_sc_trace",
+    "polar_sc_trace", "polar_sc_decode_i16",
 )
 
 _lib = None
@@ -104,6 +104,7 @@ def lib():
         "polar_sc_plan_destroy": [p],
         "polar_sc_decode": [p, p, p, sz, p],
         "polar_sc_decode_u16": [p, p, p, sz, p],
+        "polar_sc_decode_i16": [p, p, p, sz, p],
         "polar_sc_plan_prepare": [p, sz],
         "polar_sc_decode_host": [p, p, p, sz],
         "polar_load_frozen_tab": [ctypes.c_char_p, u32, u32, p, u32, ctypes.POINTER(u32)],
@@ -314,10 +315,11 @@ class Decoder:
         _check("polar_sc_plan_prepare", lib().polar_sc_plan_prepare(self._plan, int(max_batch)))
 
     # -- e -> s ports -----------------------------------------------------------------------
-    def _check_llr(self, llr):
+    def _check_llr(self, llr, allow16=False):
         torch = _torch()
-        if not (isinstance(llr, torch.Tensor) and llr.is_cuda and llr.dtype == torch.int8):
-            raise TypeError("llr must be a CUDA int8 tensor")
+        dtypes = (torch.int8, torch.int16) if allow16 else (torch.int8,)
+        if not (isinstance(llr, torch.Tensor) and llr.is_cuda and llr.dtype in dtypes):
+            raise TypeError("llr must be a CUDA %s tensor" % ("int8 or int16" if allow16 else "int8"))
         if llr.dim() != 2 or llr.shape[1] != self.N or not llr.is_contiguous():
             raise ValueError("llr must be contiguous [B, %d]" % self.N)
         return torch
@@ -336,18 +338,20 @@ class Decoder:
 
         llr: torch.int8 CUDA tensor [B, N] (contiguous). Returns (or fills `out`) a torch.int64
         CUDA tensor [B, ceil(N/64)] whose bits are x^ (bit i of word j = x^[64j+i]).
-        Asynchronous on `stream` (default: torch's current stream of llr's device).
+        Asynchronous on `stream` (default: torch's current stream of llr's device). An int16
+        tensor goes through polar_sc_decode_i16 (the channel for 9-bit LLRs).
         """
-        torch = self._check_llr(llr)
+        torch = self._check_llr(llr, allow16=True)
         B = llr.shape[0]
         if out is None:
             out = torch.empty((B, self.words), dtype=torch.int64, device=llr.device)
         else:
             self._check_out(out, llr, (B, self.words), torch.int64)
         # the C side picks the code objects / scratch of the current HIP device
+        fn = "polar_sc_decode_i16" if llr.dtype == torch.int16 else "polar_sc_decode"
         with torch.cuda.device(llr.device):
             s = stream if stream is not None else torch.cuda.current_stream(llr.device)
-            _check("polar_sc_decode", lib().polar_sc_decode(
+            _check(fn, getattr(lib(), fn)(
                 self._plan, ctypes.c_void_p(llr.data_ptr()), ctypes.c_void_p(out.data_ptr()), B,
                 ctypes.c_void_p(s.cuda_stream)))
         return out

@@ -17,17 +17,45 @@ typedef short i16x2 __attribute__((ext_vector_type(2)));
 constexpr u32 SGN = 0x80008000u;   // sign flags of both halves
 constexpr u32 MAG = 0x7FFF7FFFu;   // magnitudes of both halves
 
-// LLR_BITS (config.h:2). The hipcc-built schedule interpreter is the shipped 6; generated
-// (hipRTC) kernels of plans with another llr_bits define POLAR_Q first. 5..8: the channel
-// is an int8 stream, and HBM slots keep SM8.
+// The datapath format (the reference's compile-time switches). The hipcc-built schedule
+// interpreter is the shipped configuration; generated (hipRTC) kernels of other plans define
+// these first:
+//   POLAR_Q     LLR_BITS (config.h:2), 5..9; 9-bit LLRs keep 16-bit HBM stage slots
+//   POLAR_CA2   1: two's complement datapath (config.h:11 CA2, functions.h:48-118), values
+//               are i16 per half; 0: SIGMAG (SM16: bit 15 sign, bits 0..14 magnitude)
+//   POLAR_EXT   EXTENDED (config.h:14): exact leaves (1) or saturating G inside leaves (0)
+//   POLAR_LPAR  log2 PAR (polar_parameters.h:8), 4..6 on the device: a PAR word is P16
+//               consecutive 16-LLR device words
+//   POLAR_CHAN16  channel stream of int16 LLRs instead of int8
 #ifndef POLAR_Q
 #define POLAR_Q 6
 #endif
-static_assert(POLAR_Q >= 5 && POLAR_Q <= 8, "LLR_BITS 5..8");
+#ifndef POLAR_CA2
+#define POLAR_CA2 0
+#endif
+#ifndef POLAR_EXT
+#define POLAR_EXT 1
+#endif
+#ifndef POLAR_LPAR
+#define POLAR_LPAR 4
+#endif
+#ifndef POLAR_CHAN16
+#define POLAR_CHAN16 0
+#endif
+static_assert(POLAR_Q >= 5 && POLAR_Q <= 9, "LLR_BITS 5..9");
+static_assert(POLAR_LPAR >= 4 && POLAR_LPAR <= 6, "PAR 16..64 on the device");
 constexpr int QB = POLAR_Q;
+constexpr bool CA2 = POLAR_CA2 != 0;
+constexpr bool EXT = POLAR_EXT != 0;
+constexpr int LPAR = POLAR_LPAR;
+constexpr int P16 = 1 << (LPAR - 4);            // device words per PAR word
+constexpr bool SLOT16 = QB > 8;                 // HBM stage slots hold 16-bit values
 constexpr u32 QMAG = (1u << (QB - 1)) - 1u;     // channel / F magnitude bound (31 at 6 bits)
-constexpr u32 GSAT = (1u << (QB - 2)) - 1u;     // G clamp, qsat_sm<Q-1> (15)
-constexpr u32 REPSAT = (1u << (QB + 3)) - 1u;   // REP accumulator clamp, qfull_adder_sat_sm<Q+5> (511)
+// G clamp: SIGMAG qsat_sm<Q-1> (15 at Q 6, functions.h:186-194), CA2 qsat<Q> (31, :63-75)
+constexpr u32 GSAT = CA2 ? (1u << (QB - 1)) - 1u : (1u << (QB - 2)) - 1u;
+// REP accumulator clamp (ADDER_TREE_{PAR}, functions.h:3163-3320): SIGMAG
+// qfull_adder_sat_sm<Q+L+1> -> 2^(Q+L-1)-1 (511 at Q 6, PAR 16); CA2 qadd<Q+L+1> -> 2^(Q+L)-1
+constexpr u32 REPSAT = CA2 ? (1u << (QB + LPAR)) - 1u : (1u << (QB + LPAR - 1)) - 1u;
 constexpr u32 GSAT2 = GSAT * 0x00010001u;
 
 // ---------------------------------------------------------------------------------------
@@ -482,4 +510,137 @@ __device__ __forceinline__ bool rep_any_zero(u32 acc)
     return __builtin_amdgcn_ballot_w64(z) != 0ull;
 }
 
+// ---------------------------------------------------------------------------------------
+// Format-generic datapath of the schedule interpreter (polar_sc_interp.h): SIGMAG on SM16
+// halves, or CA2 on i16 halves (config.h:11). The per-mask / generated-subtree kernels keep
+// the SIGMAG-only split-word code above; plans of any other format run the interpreter
+// compiled by hipRTC with their POLAR_* switches.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ u32 pk_min_i16(u32 a, u32 b)
+{
+    return __builtin_bit_cast(u32, __builtin_elementwise_min(__builtin_bit_cast(i16x2, a), __builtin_bit_cast(i16x2, b)));
+}
+__device__ __forceinline__ u32 pk_max_i16(u32 a, u32 b)
+{
+    return __builtin_bit_cast(u32, __builtin_elementwise_max(__builtin_bit_cast(i16x2, a), __builtin_bit_cast(i16x2, b)));
+}
+// both halves sign-extended from their low w bits (w-bit two's complement wrap)
+__device__ __forceinline__ u32 sext_w(u32 v, int w)
+{
+    const short s = (short)(16 - w);
+    return pk_sra(pk_shl(v, (unsigned short)s), s);
+}
+// qabs<w> (scalar.h:42-49): -v in w bits, so qabs(-2^(w-1)) = -2^(w-1)
+__device__ __forceinline__ u32 ca2_qabs(u32 v, int w) { return sext_w(pk_abs_i16(v), w); }
+// F_function_C2 (functions.h:48-61) at width w: signed min of the qabs values, negated in w
+// bits when the signs differ
+__device__ __forceinline__ u32 ca2_F(u32 a, u32 b, int w)
+{
+    const u32 mn = pk_min_i16(ca2_qabs(a, w), ca2_qabs(b, w));
+    const u32 m = pk_sra(a ^ b, 15);
+    return sext_w(pk_sub(mn ^ m, m), w);
+}
+// G_function_C2 / G_extended_C2 (functions.h:63-87): u flags (bits 15 / 31): b - a, else
+// b + a; SAT != 0: qsat to +-SAT
+template <u32 SAT>
+__device__ __forceinline__ u32 ca2_G(u32 a, u32 b, u32 u)
+{
+    const u32 m = pk_sra(u & SGN, 15);
+    u32 d = pk_add(b, pk_sub(a ^ m, m));
+    if constexpr (SAT != 0) d = pk_min_i16(pk_max_i16(d, (0x10000u - SAT) * 0x00010001u), SAT * 0x00010001u);
+    return d;
+}
+
+// Function_F / Function_G of the configured format (functions.h:287-308). w: width of the
+// operands (CA2 only: the qabs wrap point); stage values are QB bits wide, exact leaf
+// levels one bit wider per G_extended above them.
+__device__ __forceinline__ u32 dp_F(u32 a, u32 b, int w)
+{
+    if constexpr (CA2) return ca2_F(a, b, w);
+    else return F_sm(a, b);
+}
+template <bool SAT>
+__device__ __forceinline__ u32 dp_G(u32 a, u32 b, u32 u)
+{
+    if constexpr (CA2) return ca2_G<SAT ? GSAT : 0u>(a, b, u);
+    else return G_sm<SAT ? GSAT : 0>(a, b, u);
+}
+// channel word: raw = two LLRs (16-bit halves, sign-extended from the input type) ->
+// wrapper_in + Adapt_format (library.h:18-28): qconv_format (SIGMAG) or unchanged (CA2)
+__device__ __forceinline__ u32 dp_chan(u32 raw)
+{
+    if constexpr (CA2) return sext_w(raw, QB);
+    else return conv_pair(raw);
+}
+// HBM stage slots: two 8-bit values per lane (SM8 pairs / int8 pairs), or (9-bit LLRs) the
+// 32-bit register as is
+__device__ __forceinline__ u32 slot_unpack(u32 h)
+{
+    if constexpr (CA2) return pk_sra(__builtin_amdgcn_perm(h, h, 0x010C000Cu), 8);   // bytes 0,1 -> 1,3
+    else return sm8_pair(h, h >> 8);
+}
+__device__ __forceinline__ u32 slot_pack(u32 v)
+{
+    if constexpr (CA2) return __builtin_amdgcn_perm(v, v, 0x0C0C0200u);             // bytes 0,2 -> 0,1
+    else return sm16_to_sm8x2(v);
+}
+
+// Spec_Polar_Decoder on one 16-LLR word with run-time frozen pattern, both formats, exact
+// (EXTENDED = 1: G_extended, widths grow) or saturating (EXTENDED = 0: Function_G at Q)
+// (functions.h:354-760). w: width of the leaf's input values. An all-frozen block decodes to
+// 0; an all-information block to its hard decisions only in SIGMAG (CA2 F has no -0).
+template <int B, int W>
+__device__ __forceinline__ u32 leaf_dp(u32 L, u32 fb, u32 fbm, const Lanes &ln, int w)
+{
+    constexpr u32 bm = ((1u << W) - 1u) << B;
+    const u32 sub = fb & bm;
+    if (sub == 0u) return 0u;
+    if (!CA2 && sub == bm) return L & SGN;
+    if constexpr (W == 2) {
+        // Spec_P2 (functions.h:366-384): lane B = a, lane B+1 = b
+        u32 P = xorlane<1>(L);
+        u32 u0 = (L ^ P) & fbm;                   // F_simplified & fb[B]   (valid on a)
+        u32 u0p = xorlane<1>(u0);
+        u32 u1;
+        if constexpr (CA2) {
+            u1 = ca2_G<0>(P, L, u0p) & fbm;       // sign of b -+ a         (on b)
+        } else {
+            u32 d = pk_sub(P & MAG, L & MAG);     // |a| < |b|              (on b)
+            u1 = bsel(d, L, P ^ u0p) & fbm;       // G_simplified & fb[B+1] (valid on b)
+        }
+        u32 u1p = xorlane<1>(u1);
+        return bsel(ln.a1, u0 ^ u1p, u1);
+    } else {
+        constexpr int H = W / 2;
+        u32 P = xorlane<H>(L);
+        u32 La = dp_F(L, P, w);                              // valid on a-lanes
+        u32 xa = leaf_dp<B, H>(La, fb, fbm, ln, w);
+        u32 Lb = dp_G<!EXT>(P, L, xorlane<H>(xa));            // valid on b-lanes
+        u32 xb = leaf_dp<B + H, H>(Lb, fb, fbm, ln, EXT ? w + 1 : w);
+        return bsel(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
+    }
+}
+
+__device__ __forceinline__ u32 leaf16_dp(u32 L, u32 fb, const Lanes &ln, int w)
+{
+    u32 fbm = ((fb >> ln.pos) & 1u) ? SGN : 0u;   // the frozen bit of this lane's word position
+    return leaf_dp<0, 16>(L, fb, fbm, ln, w);
+}
+
+// 32-bit row sum (every lane gets the total of its 16-lane row)
+__device__ __forceinline__ u32 row_sum32(u32 v)
+{
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, true);   // row_ror:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x124, 0xF, 0xF, true);   // row_ror:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x122, 0xF, 0xF, true);   // row_ror:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x121, 0xF, 0xF, true);   // row_ror:1
+    return v;
+}
+// the two halves as signed 32-bit values (two's complement value; SIGMAG converted)
+__device__ __forceinline__ int val_lo(u32 v)
+{
+    if constexpr (CA2) return (int)(short)(v & 0xFFFFu);
+    else return (v & 0x8000u) ? -(int)(v & 0x7FFFu) : (int)(v & 0x7FFFu);
+}
+__device__ __forceinline__ int val_hi(u32 v) { return val_lo(v >> 16); }
 }  // namespace polar

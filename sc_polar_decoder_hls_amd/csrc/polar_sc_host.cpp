@@ -44,16 +44,19 @@ namespace {
 // > RN, each recognised only when PRUNING_LEVEL > 0 and its ELAG_* switch is on
 // (my_module.h:129-153). REP2 = only the last two bits information, SPC2 = only the first
 // two frozen (my_module.h:108-125).
+// PAR-bit groups (fb bit k = frozen-table bit PAR g + k): REP = only bit PAR-1 information,
+// SPC = only bit 0 frozen, REP2 / SPC2 = the last two / first two.
 constexpr uint32_t NODE_REP2 = 0x03, NODE_SPC2 = 0x05;
-uint32_t classify_group(uint32_t fb, const polar_sc_config &c)
+uint32_t classify_group(uint64_t fb, uint32_t par, const polar_sc_config &c)
 {
+    const uint64_t all = par >= 64 ? ~0ull : ((1ull << par) - 1ull);
     if (c.pruning_level == 0) return NODE_RN;
     if (fb == 0u) return NODE_R0;
-    if (c.elag_r1 && fb == 0xFFFFu) return NODE_R1;
-    if (c.elag_rep && fb == 0x8000u) return NODE_REP;
-    if (c.elag_spc && fb == 0xFFFEu) return NODE_SPC;
-    if (c.elag_rep2 && fb == 0xC000u) return NODE_REP2;
-    if (c.elag_spc2 && fb == 0xFFFCu) return NODE_SPC2;
+    if (c.elag_r1 && fb == all) return NODE_R1;
+    if (c.elag_rep && fb == 1ull << (par - 1)) return NODE_REP;
+    if (c.elag_spc && fb == (all & ~1ull)) return NODE_SPC;
+    if (c.elag_rep2 && fb == 3ull << (par - 2)) return NODE_REP2;
+    if (c.elag_spc2 && fb == (all & ~3ull)) return NODE_SPC2;
     return NODE_RN;
 }
 
@@ -153,17 +156,61 @@ void window_schedule(polar_sc_plan &p, const std::vector<polar_sc_op> &ops)
     }
 }
 
-// Decode the children of the node at `level` covering groups [g0, g0+cnt) (cnt >= 2) whose
-// LLR words are in stage buffer `level`. Mirrors the F/G/R/H/H0/F_REP/G_R1/G_SPC
-// transitions of my_module::do_action:
+// PAR > 16: decode the PAR-word leaf (Spec_PolarDec_{PAR}, library.h:149-172 ->
+// functions.h:766-866) whose LLRs are the node of `words` device words at (level, wpos) as
+// device ops: F, the left half, G (G_extended, flagged exact, when EXTENDED; the operands of
+// the right half one bit wider), the right half, H; 16-LLR words by FLEAF / GLEAF. fb: the
+// frozen bits of the node (bit k = LLR k). wd: operand width above LLR_BITS (CA2 wrap point).
+void par_expand(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int level, int wpos, int words, uint64_t fb,
+                int wd)
+{
+    const int h = words / 2;
+    const uint32_t wf = (uint32_t)wd << 20, gx = p.cfg.extended ? polar_host::FB_EXACT : 0u;
+    if (h == 1) {
+        emit(out, POLAR_OP_FLEAF, level, 1, wpos, -1, (uint32_t)(fb & 0xFFFFu) | wf);
+    } else {
+        emit(out, POLAR_OP_F, level, h, wpos, -1, wf);
+        par_expand(p, out, level + 1, wpos, h, fb, wd);
+    }
+    const uint64_t fbh = fb >> (16 * h);
+    if (h == 1) {
+        emit(out, POLAR_OP_GLEAF, level, 1, wpos + 1, wpos, (uint32_t)(fbh & 0xFFFFu) | gx | wf);
+    } else {
+        emit(out, POLAR_OP_G, level, h, wpos + h, wpos, gx | wf);
+        par_expand(p, out, level + 1, wpos + h, h, fbh, p.cfg.extended ? wd + 1 : wd);
+    }
+    emit(out, POLAR_OP_H, level, h, wpos, -1, 0);
+}
+
+// R_STATE of PAR group g whose parent node is at device `level`: F / G of the parent into
+// the group's words, then its leaf decoder. PAR 16: one FLEAF / GLEAF record. PAR > 16: the
+// stage F / G record, then the PR1 decoder of the whole PAR word (OP_PLEAF) or the expanded
+// exact leaf.
+void leaf_ops(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int level, uint32_t g, bool right, int upos)
+{
+    const int P = (int)p.p16, wpos = (int)g * P;
+    const uint32_t kind = leaf_kind(p, g);
+    if (P == 1) {
+        emit(out, right ? POLAR_OP_GLEAF : POLAR_OP_FLEAF, level, 1, wpos, right ? upos : -1,
+             (uint32_t)(p.fbp[g] & 0xFFFFu) | kind << 16);
+        return;
+    }
+    emit(out, right ? POLAR_OP_G : POLAR_OP_F, level, P, wpos, right ? upos : -1, 0);
+    if (kind != POLAR_LEAF_PLAIN) emit(out, polar_host::POLAR_OP_PLEAF, level + 1, P, wpos, -1, kind << 16);
+    else par_expand(p, out, level + 1, wpos, P, p.fbp[g], 0);
+}
+
+// Decode the children of the node at device `level` covering PAR groups [g0, g0+cnt)
+// (cnt >= 2) whose LLR words are in stage buffer `level`. Mirrors the
+// F/G/R/H/H0/F_REP/G_R1/G_SPC transitions of my_module::do_action:
 //  * left child R0  -> "H0 route" (my_module.h:481-507): no F, G with sa = 0, then H0
 //  * left child REP -> F_REP_STATE (my_module.h:1292-1390)
 //  * right child R1 -> G_R1_STATE, SPC -> G_SPC_STATE (selected from the node-type stack,
 //    my_module.h:614-664, 939-997)
 //  * the root's children are never pruned: INIT pushes (RN,RN) (my_module.h:328)
-// Hybrid plans (sc != NULL): a node of sc->words words that is not the root becomes one
-// POLAR_OP_SUB record; its own schedule, rebased to the subtree root, is kept once per
-// distinct content.
+// Device records count 16-LLR words (PAR / 16 per group). Hybrid plans (sc != NULL, PAR 16):
+// a node of sc->words words that is not the root becomes one POLAR_OP_SUB record; its own
+// schedule, rebased to the subtree root, is kept once per distinct content.
 void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int level, uint32_t g0, uint32_t cnt,
                   bool is_root, SubCtx *sc)
 {
@@ -190,6 +237,7 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
         return;
     }
     const uint32_t h = cnt / 2;
+    const int P = (int)p.p16, hw = (int)h * P, w0 = (int)g0 * P, w1 = (int)(g0 + h) * P;
     // node pruning only at PRUNING_LEVEL 2 (my_module.h:478-531, 623-652, 815-868, 965-993);
     // REP2 / SPC2 classes fall through to the plain F / G transitions there
     const bool prune = p.cfg.pruning_level == 2;
@@ -199,40 +247,48 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
     if (tl == NODE_R0) {
         left_zero = true;
     } else if (tl == NODE_REP) {
-        emit(out, POLAR_OP_REP, level, (int)h, (int)g0, -1, 0);
+        emit(out, POLAR_OP_REP, level, hw, w0, -1, 0);
     } else if (h == 1) {
-        emit(out, POLAR_OP_FLEAF, level, 1, (int)g0, -1, p.fb[g0] | leaf_kind(p, g0) << 16);
+        leaf_ops(p, out, level, g0, false, -1);
     } else {
-        emit(out, POLAR_OP_F, level, (int)h, (int)g0, -1, 0);
+        emit(out, POLAR_OP_F, level, hw, w0, -1, 0);
         compile_node(p, out, level + 1, g0, h, false, sc);
     }
-    const int upos = left_zero ? -1 : (int)g0;
+    const int upos = left_zero ? -1 : w0;
     if (tr == NODE_R1) {
-        emit(out, POLAR_OP_R1, level, (int)h, (int)(g0 + h), upos, 0);
+        emit(out, POLAR_OP_R1, level, hw, w1, upos, 0);
     } else if (tr == NODE_SPC) {
-        emit(out, POLAR_OP_SPC, level, (int)h, (int)(g0 + h), upos, 0);
+        emit(out, POLAR_OP_SPC, level, hw, w1, upos, 0);
     } else if (h == 1) {
-        emit(out, POLAR_OP_GLEAF, level, 1, (int)(g0 + h), upos, p.fb[g0 + h] | leaf_kind(p, g0 + h) << 16);
+        leaf_ops(p, out, level, g0 + h, true, upos);
     } else {
-        emit(out, POLAR_OP_G, level, (int)h, (int)(g0 + h), upos, 0);
+        emit(out, POLAR_OP_G, level, hw, w1, upos, 0);
         compile_node(p, out, level + 1, g0 + h, h, false, sc);
     }
-    emit(out, left_zero ? POLAR_OP_H0 : POLAR_OP_H, level, (int)h, (int)g0, -1, 0);
+    emit(out, left_zero ? POLAR_OP_H0 : POLAR_OP_H, level, hw, w0, -1, 0);
 }
 
-// The reference's swept configurations (script/script_tests.sh:103-122): PRUNING_LEVEL 0/1/2
-// with any ELAG_R1/REP/SPC/REP2/SPC2/H0 switches, at LLR_BITS 5..8 (the sweep itself runs at
-// QUANT = 8, script_tests.sh:9,25; the channel stays one int8 per LLR). ELAG_RARE = 1 does
-// not compile in the reference (my_module.h:255 vs :1511); PAR, CA2 and EXTENDED = 0 change
-// the datapath and are not built.
+// The reference's swept configurations: PRUNING_LEVEL 0/1/2 with any ELAG_R1/REP/SPC/REP2/
+// SPC2/H0 switches (script/script_tests.sh:103-122), LLR_BITS 5..9 (QUANT 6..9,
+// script/parser.sh:12, parser_comp.sh:12; 9-bit LLRs beyond the int8 range need the int16
+// channel of polar_sc_decode_i16), SIGMAG or CA2 (parser.sh:15,43), EXTENDED 0/1
+// (config.h:14) and PAR 16 / 32 / 64 (script_tests.sh:11,124 runs 16 and 64). ELAG_RARE = 1
+// does not compile in the reference (my_module.h:255 vs :1511); PAR below 16 is not built.
 bool config_supported(const polar_sc_config &c)
 {
-    polar_sc_config d;
-    polar_sc_default_config(&d);
     auto sw = [](int32_t v) { return v == 0 || v == 1; };
-    return c.llr_bits >= 5 && c.llr_bits <= 8 && c.par == d.par && c.sigmag == d.sigmag && c.extended == d.extended &&
-           c.pruning_level >= 0 && c.pruning_level <= 2 && sw(c.elag_r1) && sw(c.elag_rep) && sw(c.elag_spc) &&
-           sw(c.elag_rep2) && sw(c.elag_spc2) && c.elag_rare == 0 && sw(c.elag_h0) && sw(c.strict_llr);
+    return c.llr_bits >= 5 && c.llr_bits <= 9 && (c.par == 16 || c.par == 32 || c.par == 64) && sw(c.sigmag) &&
+           sw(c.extended) && c.pruning_level >= 0 && c.pruning_level <= 2 && sw(c.elag_r1) && sw(c.elag_rep) &&
+           sw(c.elag_spc) && sw(c.elag_rep2) && sw(c.elag_spc2) && c.elag_rare == 0 && sw(c.elag_h0) &&
+           sw(c.strict_llr);
+}
+
+// the shipped datapath (SIGMAG, PAR 16, EXTENDED, int8-range LLRs): the only one the per-mask
+// and generated-subtree kernels implement; every other format runs the schedule interpreter
+// compiled by hipRTC with its POLAR_* switches
+bool default_format(const polar_sc_config &c)
+{
+    return c.sigmag == 1 && c.par == 16 && c.extended == 1 && c.llr_bits <= 8;
 }
 
 int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
@@ -414,7 +470,8 @@ const char *polar_sc_strerror(int err)
     case 0: return "success";
     case -EINVAL: return "invalid argument";
     case -ENOMEM: return "out of memory";
-    case -ENOTSUP: return "configuration not supported (see polar_sc_config in include/polar_sc.h for the accepted ranges)";
+    case -ENOTSUP: return "configuration not supported (PAR other than 16/32/64, LLR_BITS outside 5..9, ELAG_RARE, "
+                          "or a switch outside 0/1; see polar_sc_config in include/polar_sc.h)";
     case -ENOENT: return "file not found";
     case -EIO: return "HIP runtime error";
     default: return "unknown error";
@@ -450,24 +507,28 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     if (cfg) c = *cfg; else polar_sc_default_config(&c);
     if (!config_supported(c)) return -ENOTSUP;
 
+    if (N < 2u * (uint32_t)c.par) return -EINVAL;   // INIT needs N_DIV >= 2 (my_module.h:294-309)
+
     polar_sc_plan *p = new (std::nothrow) polar_sc_plan();
     if (!p) return -ENOMEM;
     p->N = N;
-    p->G = N / POLAR_SC_PAR;
+    p->G = N / 16;
+    p->GP = N / (uint32_t)c.par;
+    p->p16 = (uint32_t)c.par / 16;
     p->cfg = c;
     p->mask.resize(N);
-    p->fb.resize(p->G);
-    p->type.resize(p->G);
+    p->fbp.resize(p->GP);
+    p->type.resize(p->GP);
     for (uint32_t i = 0; i < N; i++) {
         p->mask[i] = info_mask[i] ? 1 : 0;
         p->K += p->mask[i];
     }
     polar_sc_plan_stats &s = p->stats;
-    for (uint32_t g = 0; g < p->G; g++) {
-        uint32_t t = 0;
-        for (uint32_t k = 0; k < POLAR_SC_PAR; k++) t |= (uint32_t)p->mask[g * 16 + k] << k;
-        p->fb[g] = (uint16_t)t;
-        p->type[g] = (uint8_t)classify_group(t, c);
+    for (uint32_t g = 0; g < p->GP; g++) {
+        uint64_t t = 0;
+        for (uint32_t k = 0; k < (uint32_t)c.par; k++) t |= (uint64_t)p->mask[g * (uint32_t)c.par + k] << k;
+        p->fbp[g] = t;
+        p->type[g] = (uint8_t)classify_group(t, (uint32_t)c.par, c);
         switch (p->type[g]) {
         case NODE_R0: s.n_r0++; break;
         case NODE_R1: s.n_r1++; break;
@@ -476,12 +537,12 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         default: s.n_rn++; break;   // RN, REP2, SPC2
         }
     }
-    compile_node(*p, p->ops, 0, 0, p->G, true, nullptr);
+    compile_node(*p, p->ops, 0, 0, p->GP, true, nullptr);
     emit(p->ops, POLAR_OP_END, 0, 0, 0, -1, 0);
 
     s.N = N;
     s.K = p->K;
-    s.groups = p->G;
+    s.groups = p->GP;
     s.n_ops = (uint32_t)p->ops.size();
     for (const polar_sc_op &o : p->ops) {
         s.op_count[o.code & 15]++;
@@ -494,7 +555,8 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         // upper levels + bit dwords in HBM scratch; the levels of nodes <= 128 words in LDS,
         // plus an LDS window for the partial sums of the current 128-word subtree
         p->lds0 = (int)p->G - LDS_LOW_SLOTS;
-        p->hbm_group_dwords = p->lds0 * 32 + (int)nbd * 64;   // SM8-pair slots + bit dwords
+        // 8-bit-pair slots (16-bit values for 9-bit LLRs) + bit dwords
+        p->hbm_group_dwords = p->lds0 * (c.llr_bits > 8 ? 64 : 32) + (int)nbd * 64;
         p->lds_group_dwords = ((int)nslot - p->lds0 + LDS_LOW_SLOTS / 16) * 64;
     } else {
         p->lds0 = 0;
@@ -511,17 +573,18 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     bool kinds = false;
     for (const polar_sc_op &o : p->ops)
         if ((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && (o.fb >> 16)) kinds = true;
-    p->jit = (polar_host::jit_supported(N) && jit_on && !kinds) ? 1 : 0;
+    const bool dflt = default_format(c);
+    p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     int sub_words = 64;
     if (const char *e = std::getenv("POLAR_SC_SUB_WORDS")) {
         if (*e) sub_words = std::atoi(e);
     }
     const bool sub_ok = sub_words >= 2 && sub_words <= 64 && (sub_words & (sub_words - 1)) == 0;
     std::vector<polar_sc_op> dev_sched;
-    if (!p->jit && jit_on && !kinds && sub_ok && (uint32_t)sub_words < p->G) {
+    if (!p->jit && jit_on && !kinds && dflt && sub_ok && (uint32_t)sub_words < p->G) {
         SubCtx sc;
         sc.words = (uint32_t)sub_words;
-        compile_node(*p, dev_sched, 0, 0, p->G, true, &sc);
+        compile_node(*p, dev_sched, 0, 0, p->GP, true, &sc);
         emit(dev_sched, POLAR_OP_END, 0, 0, 0, -1, 0);
         p->hybrid = 1;
         p->hybrid_waves = polar_host::HYBRID_MAX_WAVES;
@@ -536,9 +599,10 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         s.n_sub_calls = sc.calls;
     } else {
         dev_sched = p->ops;
-        if (!p->jit && c.llr_bits != 6) {
-            // the hipcc-built interpreter is the shipped LLR_BITS = 6; other widths run the
-            // same interpreter compiled by hipRTC with POLAR_Q (a hybrid kernel without subtrees)
+        if (!p->jit && (c.llr_bits != 6 || !dflt)) {
+            // the hipcc-built interpreter is the shipped datapath; other formats run the same
+            // interpreter compiled by hipRTC with their POLAR_* switches (a hybrid kernel
+            // without subtrees)
             p->hybrid = 1;
             p->hybrid_waves = polar_host::HYBRID_MAX_WAVES;
         }
@@ -567,6 +631,7 @@ int polar_sc_plan_destroy(polar_sc_plan *p)
         if (kv.second.ops) (void)hipFree(kv.second.ops);
         if (kv.second.module) (void)hipModuleUnload(kv.second.module);
         if (kv.second.imodule) (void)hipModuleUnload(kv.second.imodule);
+        if (kv.second.module16) (void)hipModuleUnload(kv.second.module16);
         if (kv.second.scratch) (void)hipFree(kv.second.scratch);
     }
     if (have_dev && !p->dev.empty()) (void)hipSetDevice(cur);
@@ -597,6 +662,25 @@ int polar_sc_trace(const polar_sc_plan *p, const int8_t *llr_dev, uint64_t *hard
     const int stride16 = (int)(4 * ((p->G + 3) / 4));
     return trace_common(p, llr_dev, (uint16_t *)hard_bits_dev, batch, stride16, recs, cap, count, clock_ghz,
                         total_cycles);
+}
+
+int polar_sc_decode_i16(const polar_sc_plan *p, const int16_t *llr_dev, uint64_t *hard_bits_dev, size_t batch,
+                        void *stream)
+{
+    if (!p || (batch > 0 && (!llr_dev || !hard_bits_dev))) return -EINVAL;
+    if (batch == 0) return 0;
+    if (batch > (size_t)0x7FFFFFF8) return -EINVAL;
+    DevState *st = nullptr;
+    std::unique_lock<std::mutex> held;
+    int rc = ensure_device(p, batch, &st, true, &held);
+    if (rc) return rc;
+    rc = polar_host::jit_load16(*p, *st);
+    if (rc) return rc;
+    int wpg = waves_per_group(p, batch, st->simds);
+    if (wpg > polar_host::HYBRID_MAX_WAVES) wpg = polar_host::HYBRID_MAX_WAVES;
+    const int stride16 = (int)(4 * ((p->G + 3) / 4));
+    return polar_host::launch_interp_fn(st->fn16, *p, *st, (const int8_t *)llr_dev, (uint16_t *)hard_bits_dev,
+                                        (long)batch, stride16, wpg, stream, nullptr);
 }
 
 int polar_sc_decode_u16(const polar_sc_plan *p, const int8_t *llr_dev, uint16_t *bits_dev,

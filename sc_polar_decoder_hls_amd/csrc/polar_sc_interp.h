@@ -13,7 +13,11 @@
 //     cross-lane traffic is the leaf (Spec_PolarDec_16), the REP adder tree, the SPC
 //     min/parity trees and output packing, all done with DPP row ops.
 //   * LLRs are sign-magnitude in packed 16-bit halves (bit 15 = sign, bits 0..14 =
-//     magnitude): "SM16". All arithmetic is v_pk_* on two frames at once.
+//     magnitude): "SM16", or (POLAR_CA2) two's complement i16 halves. All arithmetic is
+//     v_pk_* on two frames at once (the dp_* datapath of polar_sc_device.h).
+//   * PAR > 16 (POLAR_LPAR): a PAR word is P16 consecutive 16-LLR device words. The host
+//     expands every PAR-word leaf into device ops (exact G flagged in the op), PR1 leaf
+//     decoders of whole PAR words are OP_PLEAF records, REP / SPC work per PAR word.
 //   * The control flow of the reference FSM does not depend on LLR values, so the host
 //     compiles it once per frozen mask into a flat op list (polar_sc_host.cpp); the kernel
 //     interprets it with wave-uniform (scalar) control.
@@ -44,8 +48,12 @@ enum : int {
     OP_F = 1, OP_G = 2, OP_FLEAF = 3, OP_GLEAF = 4, OP_REP = 5, OP_R1 = 6, OP_SPC = 7,
     OP_H = 8, OP_H0 = 9, OP_END = 10,
     OP_WOPEN = 11, OP_WFLUSH = 12,  // HBM-scratch plans: partial-sum window of a 128-word subtree
-    OP_SUB = 13                     // hybrid plans: generated subtree decoder `fb` at node (level, pos)
+    OP_SUB = 13,                    // hybrid plans: generated subtree decoder `fb` at node (level, pos)
+    OP_PLEAF = 14                   // PAR > 16: PRUNING_LEVEL 1 leaf decoder (fb kind) of the PAR word at (level, pos)
 };
+// op.fb fields besides the leaf frozen pattern (bits 0..15) and PR1 leaf kind (16..18)
+constexpr uint32_t FB_EXACT = 1u << 19;   // G / GLEAF inside a PAR-word leaf: G_extended (no clamp)
+__device__ __forceinline__ int fb_width(uint32_t fb) { return QB + (int)((fb >> 20) & 15u); }   // operand width
 constexpr int WIN_DWORDS = 16;      // 256 words of partial sums (polar_sc_host.cpp LDS_LOW_SLOTS / 16)
 
 struct Op {            // == polar_sc_op (include/polar_sc.h)
@@ -68,26 +76,40 @@ struct Ctx;
 template <class C> struct GMEM_OF;
 template <bool GMEM> struct GMEM_OF<Ctx<GMEM>> { static constexpr bool value = GMEM; };
 
+// HBM slot element: two 8-bit values, or a whole register when LLRs need 9 bits
+template <bool B> struct SlotT { typedef uint16_t T; };
+template <> struct SlotT<true> { typedef uint32_t T; };
+typedef SlotT<SLOT16>::T slot_t;
+#if POLAR_CHAN16
+typedef short chan_t;          // int16 channel stream (polar_sc_decode_i16)
+#else
+typedef int8_t chan_t;
+#endif
+
 template <bool GMEM>
 struct Ctx {
-    uint16_t *hs;          // HBM scratch (GMEM): slots [0, lds0) as SM8 pairs (128 B rows)
+    slot_t *hs;            // HBM scratch (GMEM): slots [0, lds0), 8-bit pairs (128 B rows)
     uint32_t *hbit;        // HBM scratch (GMEM): bit dwords (256 B rows)
     uint32_t *lb;          // LDS: slots [lds0, nslot) (GMEM) / slots + bit dwords (!GMEM)
     int lds0;              // first slot held in LDS (0 when !GMEM)
     int wd0;               // GMEM: first bit dword of the open partial-sum window, -1 = none
     uint32_t nslot;        // G - 1
     int G;
-    const int8_t *llr_lo, *llr_hi;   // frame rows (lane offset included)
+    const chan_t *llr_lo, *llr_hi;   // frame rows (lane offset included)
     Lanes ln;
     __device__ __forceinline__ bool in_lds(int slot) const { return !GMEM || slot >= lds0; }
     __device__ __forceinline__ uint32_t ldl(int slot) const { return lb[(slot - lds0) * 64]; }
     __device__ __forceinline__ uint32_t ldh(int slot) const
     {
-        const uint32_t h = hs[slot * 64];
-        return sm8_pair(h, h >> 8);
+        if constexpr (SLOT16) return hs[slot * 64];
+        else return slot_unpack(hs[slot * 64]);
     }
     __device__ __forceinline__ void stl(int slot, uint32_t v) const { lb[(slot - lds0) * 64] = v; }
-    __device__ __forceinline__ void sth(int slot, uint32_t v) const { hs[slot * 64] = (uint16_t)sm16_to_sm8x2(v); }
+    __device__ __forceinline__ void sth(int slot, uint32_t v) const
+    {
+        if constexpr (SLOT16) hs[slot * 64] = v;
+        else hs[slot * 64] = (uint16_t)slot_pack(v);
+    }
     __device__ __forceinline__ uint32_t ld(int slot) const { return in_lds(slot) ? ldl(slot) : ldh(slot); }
     // storage known at compile time (callers branch once per op on in_lds)
     template <bool L> __device__ __forceinline__ uint32_t ldx(int slot) const { return L ? ldl(slot) : ldh(slot); }
@@ -122,7 +144,7 @@ struct Ctx {
     __device__ __forceinline__ int lvl_off(int k) const { return G - (G >> (k - 1)); }  // k >= 1
     __device__ __forceinline__ uint32_t chan(int w) const
     {
-        return conv_pair((uint32_t)(uint8_t)llr_lo[16 * w] | ((uint32_t)(uint8_t)llr_hi[16 * w] << 16));
+        return dp_chan((uint32_t)(uint16_t)(short)llr_lo[16 * w] | ((uint32_t)(uint16_t)(short)llr_hi[16 * w] << 16));
     }
     // source word i of a level-k node (k = 0: channel)
     __device__ __forceinline__ uint32_t src(int k, int i) const
@@ -154,20 +176,21 @@ __device__ __forceinline__ void bits_put_small(const C &c, int pos, int n, uint3
 // ---------------------------------------------------------------------------------------
 // Ops
 // ---------------------------------------------------------------------------------------
-// SL / DL: source / destination slots in LDS (else HBM scratch)
-template <bool ISG, bool ROOT, bool SL, bool DL, class C>
-__device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int i0, int i1)
+// SL / DL: source / destination slots in LDS (else HBM scratch). X: exact G (G_extended
+// inside a PAR-word leaf, no clamp); w: operand width (CA2 F wrap point).
+template <bool ISG, bool ROOT, bool SL, bool DL, bool X, class C>
+__device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int i0, int i1, int w)
 {
     const int dst = c.lvl_off(k + 1);
     const int s0 = ROOT ? 0 : c.lvl_off(k);
-    auto src = [&](int w) -> uint32_t {
-        if constexpr (ROOT) return c.chan(w);
-        else if constexpr (SL) return c.ldl(s0 + w);
-        else return c.ldh(s0 + w);
+    auto src = [&](int w_) -> uint32_t {
+        if constexpr (ROOT) return c.chan(w_);
+        else if constexpr (SL) return c.ldl(s0 + w_);
+        else return c.ldh(s0 + w_);
     };
-    auto put = [&](int w, uint32_t v) {
-        if constexpr (DL) c.stl(dst + w, v);
-        else c.sth(dst + w, v);
+    auto put = [&](int w_, uint32_t v) {
+        if constexpr (DL) c.stl(dst + w_, v);
+        else c.sth(dst + w_, v);
     };
     int i = i0;
     // CH words per iteration: 2 CH independent source loads in flight (16 for HBM sources:
@@ -198,11 +221,11 @@ __device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int
             for (int j = 0; j < CH; j++) {
                 const int q = upos + i + j;
                 const uint32_t u = (upos >= 0) ? ubit(((q >> 4) == ((upos + i) >> 4)) ? u0 : u1, q) : 0u;
-                r[j] = G_sm<GSAT>(a[j], b[j], u);
+                r[j] = dp_G<!X>(a[j], b[j], u);
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < CH; j++) r[j] = F_sm(a[j], b[j]);
+            for (int j = 0; j < CH; j++) r[j] = dp_F(a[j], b[j], w);
         }
 #pragma unroll
         for (int j = 0; j < CH; j++) put(i + j, r[j]);
@@ -212,9 +235,9 @@ __device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int
         uint32_t r;
         if constexpr (ISG) {
             const uint32_t u = (upos >= 0) ? ubit(c.bld((upos + i) >> 4), upos + i) : 0u;
-            r = G_sm<GSAT>(a, b, u);
+            r = dp_G<!X>(a, b, u);
         } else {
-            r = F_sm(a, b);
+            r = dp_F(a, b, w);
         }
         put(i, r);
     }
@@ -223,90 +246,204 @@ __device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int
 // F_STATE / G_STATE word loops (my_module.h:373-445, 704-781) for n >= 2 output words:
 // dst[i] = F(src[i], src[n+i]) or G(src[i], src[n+i], bit_mem[upos+i]), i in [i0, i1)
 // (the words of this wave when the op is split across the waves of a group).
-template <bool ISG, class C>
-__device__ __forceinline__ void op_fg(const C &c, int k, int n, int upos, int i0, int i1)
+template <bool ISG, bool X, class C>
+__device__ __forceinline__ void op_fg_x(const C &c, int k, int n, int upos, int i0, int i1, int w)
 {
     const bool dl = c.in_lds(c.lvl_off(k + 1));
     if (k == 0) {
-        if (dl) fg_words<ISG, true, false, true>(c, k, n, upos, i0, i1);
-        else fg_words<ISG, true, false, false>(c, k, n, upos, i0, i1);
+        if (dl) fg_words<ISG, true, false, true, X>(c, k, n, upos, i0, i1, w);
+        else fg_words<ISG, true, false, false, X>(c, k, n, upos, i0, i1, w);
     } else if (c.in_lds(c.lvl_off(k))) {
-        fg_words<ISG, false, true, true>(c, k, n, upos, i0, i1);
+        fg_words<ISG, false, true, true, X>(c, k, n, upos, i0, i1, w);
     } else if (dl) {
-        fg_words<ISG, false, false, true>(c, k, n, upos, i0, i1);
+        fg_words<ISG, false, false, true, X>(c, k, n, upos, i0, i1, w);
     } else {
-        fg_words<ISG, false, false, false>(c, k, n, upos, i0, i1);
+        fg_words<ISG, false, false, false, X>(c, k, n, upos, i0, i1, w);
+    }
+}
+template <bool ISG, class C>
+__device__ __forceinline__ void op_fg(const C &c, int k, int n, int upos, int i0, int i1, uint32_t fb)
+{
+    // exact G only occurs inside PAR-word leaves (PAR > 16), always on LDS levels
+    if constexpr (ISG && P16 > 1) {
+        if (fb & FB_EXACT) {
+            fg_words<ISG, false, true, true, true>(c, k, n, upos, i0, i1, fb_width(fb));
+            return;
+        }
+    }
+    op_fg_x<ISG, false>(c, k, n, upos, i0, i1, fb_width(fb));
+}
+
+// PRUNING_LEVEL 1 leaf decoders of one 16-LLR word (R_STATE, my_module.h:566-593) in the
+// configured format: REP / REP2 (sel 1) / SPC / SPC2 (sel 1); w: operand width
+__device__ __forceinline__ uint32_t leaf_kind_dp(uint32_t L, uint32_t kind, const Lanes &ln, int w)
+{
+    if constexpr (!CA2) {
+        switch (kind) {
+        case 1: return leaf_rep(L, ln);
+        case 2: return leaf_spc<false>(L, ln);
+        case 3: return leaf_rep2(L, ln);
+        default: return leaf_spc<true>(L, ln);
+        }
+    } else {
+        // REP_{16}_CA2 / REP_REP2 (functions.h:870-1260): sign of the exact sum (of each
+        // position class for REP2); exact i16 sums, pairs at distance 8, 4, 2 (, 1)
+        if (kind == 1 || kind == 3) {
+            uint32_t v = L;
+            v = pk_add(v, xorlane<8>(v));
+            v = pk_add(v, xorlane<4>(v));
+            v = pk_add(v, xorlane<2>(v));
+            if (kind == 1) v = pk_add(v, xorlane<1>(v));
+            return v & SGN;
+        }
+        // SPC_{16} / SPC_SPC2 CA2 (functions.h:2024-2250, 2700-2930): sign ^ (parity & mask),
+        // the tournament on qabs (signed: the wrapped qabs(-2^(w-1)) is the minimum)
+        const bool spc2 = kind == 4;
+        const uint32_t h = L & SGN;
+        uint32_t par = h;
+        par ^= xorlane<8>(par);
+        par ^= xorlane<4>(par);
+        par ^= xorlane<2>(par);
+        if (!spc2) par ^= xorlane<1>(par);
+        const uint32_t qa = pk_add(ca2_qabs(L, w), (1u << (w - 1)) * 0x00010001u);   // order-preserving, >= 0
+        uint32_t klo = ((qa & 0xFFFFu) << 4) | ln.br, khi = ((qa >> 16) << 4) | ln.br;
+        const uint32_t mlo0 = klo, mhi0 = khi;
+        klo = __builtin_elementwise_min(klo, xorlane<8>(klo));
+        khi = __builtin_elementwise_min(khi, xorlane<8>(khi));
+        klo = __builtin_elementwise_min(klo, xorlane<4>(klo));
+        khi = __builtin_elementwise_min(khi, xorlane<4>(khi));
+        klo = __builtin_elementwise_min(klo, xorlane<2>(klo));
+        khi = __builtin_elementwise_min(khi, xorlane<2>(khi));
+        if (!spc2) {
+            klo = __builtin_elementwise_min(klo, xorlane<1>(klo));
+            khi = __builtin_elementwise_min(khi, xorlane<1>(khi));
+        }
+        const uint32_t flo = (klo == mlo0) ? (par & 0x8000u) : 0u;
+        const uint32_t fhi = (khi == mhi0) ? (par & 0x80000000u) : 0u;
+        return h ^ flo ^ fhi;
     }
 }
 
 // F/G with NB_ITER = 1 followed by R_STATE: Spec_Polar_Decoder on reg_result
-// (my_module.h:544-612)
+// (my_module.h:544-612). Inside a PAR-word leaf (PAR > 16) G may be exact (FB_EXACT) and
+// the operands wider than LLR_BITS.
 template <bool ISG, class C>
 __device__ __forceinline__ void op_leaf(const C &c, int k, int pos, int upos, uint32_t fb)
 {
     uint32_t a = c.src(k, 0), b = c.src(k, 1);
     uint32_t L;
+    int w = fb_width(fb);
     if constexpr (ISG) {
         uint32_t u = (upos >= 0) ? ubit(c.bld(upos >> 4), upos) : 0u;
-        L = G_sm<GSAT>(a, b, u);
+        if (P16 > 1 && (fb & FB_EXACT)) {
+            L = dp_G<false>(a, b, u);
+            w += 1;
+        } else {
+            L = dp_G<true>(a, b, u);
+        }
     } else {
-        L = F_sm(a, b);
+        L = dp_F(a, b, w);
     }
     // fb bits 16..18: PRUNING_LEVEL 1 leaf decoder (POLAR_LEAF_*, include/polar_sc.h)
-    uint32_t x;
-    switch (fb >> 16) {
-    case 1: x = leaf_rep(L, c.ln); break;
-    case 2: x = leaf_spc<false>(L, c.ln); break;
-    case 3: x = leaf_rep2(L, c.ln); break;
-    case 4: x = leaf_spc<true>(L, c.ln); break;
-    default: x = leaf16(L, fb & 0xFFFFu, c.ln); break;
-    }
+    const uint32_t kind = (fb >> 16) & 7u;
+    const uint32_t x = kind ? leaf_kind_dp(L, kind, c.ln, w) : leaf16_dp(L, fb & 0xFFFFu, c.ln, w);
     int b4 = pos & 15;
     uint32_t m = 0x10001u << b4;
     uint32_t d = c.bld(pos >> 4);
     c.bst(pos >> 4, (d & ~m) | (x >> (15 - b4)));
 }
 
-// F_REP_STATE (my_module.h:1292-1390): lambda = F(parent); per word the 16-lane exact SM
-// adder tree, accumulated over words in order by the 11-bit saturating SM adder
-// (ADDER_TREE_16, functions.h:3190-3205); x = all sign(acc).
-template <bool L, class C>
-__device__ __forceinline__ void rep_body(const C &c, int s0, int n, int pos)
+// The shipped datapath (SIGMAG, PAR 16, LLR_BITS <= 8): the packed fast paths below. Any
+// other format takes the generic 32-bit REP value path and PAR-word SPC keys.
+constexpr bool DEFAULT_FMT = !CA2 && P16 == 1 && QB <= 8;
+
+// bits [pos, pos + n) of the partial sums = per-half decision flags `full` (0xFFFF / 0)
+template <class C>
+__device__ __forceinline__ void bits_fill(const C &c, int pos, int n, uint32_t full)
 {
-    // value chain in two's complement (exact sums and 511 clamps, polar_sc_device.h); the
-    // exact SM chain only when some frame ends on a zero total (sign-of-zero rule). Source
-    // words are loaded 8 at a time (one round trip per 8 words for HBM slots).
-    uint32_t acc = 0;
-    auto word = [&](uint32_t lam) {
-        const uint32_t sg = pk_sra(lam, 15);
-        acc = rep_acc(acc, row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
-    };
-    int i = 0;
-    for (; i + 8 <= n; i += 8) {
-        uint32_t a[8], b[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            a[j] = c.template ldx<L>(s0 + i + j);
-            b[j] = c.template ldx<L>(s0 + n + i + j);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) word(F_sm(a[j], b[j]));
-    }
-    for (; i < n; i++) word(F_sm(c.template ldx<L>(s0 + i), c.template ldx<L>(s0 + n + i)));
-    if (rep_any_zero(acc)) {
-        acc = 0;
-        for (i = 0; i < n; i++) {
-            uint32_t lam = F_sm(c.template ldx<L>(s0 + i), c.template ldx<L>(s0 + n + i));
-            uint32_t t = row_add_tree(lam, c.ln);
-            acc = G_sm<REPSAT>(t, acc, 0u);
-        }
-    }
-    // two's complement or SM16: the decision is bit 15 / 31 either way
-    const uint32_t full = pk_sra(acc, 15);
     if (n >= 16) {
         for (int j = 0; j < n / 16; j++) c.bst((pos >> 4) + j, full);
     } else {
         bits_put_small(c, pos, n, full);
+    }
+}
+
+// F_REP_STATE (my_module.h:1292-1390): lambda = F(parent); per PAR word the exact pair tree
+// of its PAR LLRs (ADD_TREE_{PAR}), accumulated over the PAR words in order by the saturating
+// adder of ADDER_TREE_{PAR} (functions.h:3163-3320); x = all sign(acc).
+template <bool L, class C>
+__device__ __forceinline__ void rep_body(const C &c, int s0, int n, int pos)
+{
+    if constexpr (DEFAULT_FMT) {
+        // value chain in two's complement (exact sums and 511 clamps, polar_sc_device.h); the
+        // exact SM chain only when some frame ends on a zero total (sign-of-zero rule). Source
+        // words are loaded 8 at a time (one round trip per 8 words for HBM slots).
+        uint32_t acc = 0;
+        auto word = [&](uint32_t lam) {
+            const uint32_t sg = pk_sra(lam, 15);
+            acc = rep_acc(acc, row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
+        };
+        int i = 0;
+        for (; i + 8 <= n; i += 8) {
+            uint32_t a[8], b[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                a[j] = c.template ldx<L>(s0 + i + j);
+                b[j] = c.template ldx<L>(s0 + n + i + j);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) word(F_sm(a[j], b[j]));
+        }
+        for (; i < n; i++) word(F_sm(c.template ldx<L>(s0 + i), c.template ldx<L>(s0 + n + i)));
+        if (rep_any_zero(acc)) {
+            acc = 0;
+            for (i = 0; i < n; i++) {
+                uint32_t lam = F_sm(c.template ldx<L>(s0 + i), c.template ldx<L>(s0 + n + i));
+                uint32_t t = row_add_tree(lam, c.ln);
+                acc = G_sm<REPSAT>(t, acc, 0u);
+            }
+        }
+        // two's complement or SM16: the decision is bit 15 / 31 either way
+        bits_fill(c, pos, n, pk_sra(acc, 15));
+    } else {
+        // every format: the exact PAR-word totals as 32-bit values per frame, the saturating
+        // chain in 32 bits (CA2: qadd, the decision is the sign; SIGMAG: the same value chain,
+        // with the exact SM chain when a frame ends on zero)
+        int alo = 0, ahi = 0;
+        const int sat = (int)REPSAT;
+        for (int i = 0; i < n; i += P16) {
+            int tlo = 0, thi = 0;
+            for (int j = 0; j < P16; j++) {
+                const uint32_t lam = dp_F(c.template ldx<L>(s0 + i + j), c.template ldx<L>(s0 + n + i + j), QB);
+                tlo += val_lo(lam);
+                thi += val_hi(lam);
+            }
+            tlo = (int)row_sum32((uint32_t)tlo);
+            thi = (int)row_sum32((uint32_t)thi);
+            alo = __builtin_elementwise_min(__builtin_elementwise_max(alo + tlo, -sat), sat);
+            ahi = __builtin_elementwise_min(__builtin_elementwise_max(ahi + thi, -sat), sat);
+        }
+        uint32_t full = (alo < 0 ? 0xFFFFu : 0u) | (ahi < 0 ? 0xFFFF0000u : 0u);
+        if constexpr (!CA2) {
+            if (__builtin_amdgcn_ballot_w64(alo == 0 || ahi == 0) != 0ull) {
+                // ADD_TREE_{PAR}_SM pair tree (words at distance P16/2 .. 1, then the row) and
+                // qfull_adder_sat_sm over the PAR words: the sign of a zero total
+                uint32_t acc = 0;
+                for (int i = 0; i < n; i += P16) {
+                    uint32_t v[P16];
+#pragma unroll
+                    for (int j = 0; j < P16; j++)
+                        v[j] = F_sm(c.template ldx<L>(s0 + i + j), c.template ldx<L>(s0 + n + i + j));
+#pragma unroll
+                    for (int m = P16; m > 1; m /= 2)
+#pragma unroll
+                        for (int j = 0; j < m / 2; j++) v[j] = G_sm<0>(v[j], v[j + m / 2], 0u);
+                    acc = G_sm<REPSAT>(row_add_tree(v[0], c.ln), acc, 0u);
+                }
+                full = pk_sra(acc, 15);
+            }
+        }
+        bits_fill(c, pos, n, full);
     }
 }
 
@@ -318,10 +455,35 @@ __device__ __forceinline__ void op_rep(const C &c, int k, int n, int pos)
     else rep_body<false>(c, s0, n, pos);
 }
 
+// bit reversal of the low `bits` bits
+__device__ __forceinline__ uint32_t bitrev_n(uint32_t v, int bits)
+{
+    return bits ? (__builtin_bitreverse32(v) >> (32 - bits)) : 0u;
+}
+// SPC search key of device word i (the lane's bitrev4 position is ORed in later, shifted by
+// LPAR - 4): PAR word index, then bitrev_{LPAR}(position in the PAR word) -- the order of the
+// Min_Mask_{PAR} tournament within a PAR word plus the strict '<' across PAR words
+__device__ __forceinline__ uint32_t spc_word_key(int i)
+{
+    return ((uint32_t)(i / P16) << LPAR) | bitrev_n((uint32_t)(i % P16), LPAR - 4);
+}
+// device word of a min key
+__device__ __forceinline__ int spc_key_word(uint32_t key)
+{
+    const uint32_t k = key & 0xFFFFFFu;
+    return (int)((k >> LPAR) * P16 + bitrev_n(k & (uint32_t)(P16 - 1), LPAR - 4));
+}
+// |lambda| of a (saturated) G output as the SPC trees compare it (VECTOR_ABS_SM / qabs)
+__device__ __forceinline__ uint32_t spc_mag(uint32_t lam)
+{
+    if constexpr (CA2) return pk_abs_i16(lam);
+    else return lam & MAG;
+}
+
 // G_R1_STATE (my_module.h:1571-1642) and G_SPC_STATE (my_module.h:1737-1842):
 // lambda = G(parent, bits[upos..]); x = sign(lambda); SPC additionally flips the first
-// minimum-|lambda| position (lexicographic (|l|, word, bitrev4(lane)) == Min_Mask_16_SM
-// tournament + strict '<' across words) when the parity of x is odd.
+// minimum-|lambda| position (lexicographic (|l|, PAR word, bitrev(position)) == Min_Mask
+// tournament + strict '<' across PAR words) when the parity of x is odd.
 // [i0, i1): the words of this wave (R1 split in whole 16-word chunks; SPC is never split).
 template <bool SPC, bool L, class C>
 __device__ __forceinline__ void r1spc_body(const C &c, int s0, int n, int upos, int pos, int i0, int i1)
@@ -334,15 +496,16 @@ __device__ __forceinline__ void r1spc_body(const C &c, int s0, int n, int upos, 
             if (((upos + i) & 15) == 0 || i == i0) ud = c.bld((upos + i) >> 4);
             u = ubit(ud, upos + i);
         }
-        uint32_t lam = G_sm<GSAT>(a, b, u);
+        uint32_t lam = dp_G<true>(a, b, u);
         uint32_t h = lam & SGN;
         int q = (pos + i) & 15;
         acc |= h >> (15 - q);
         if (n >= 16 && q == 15) { c.bst((pos + i) >> 4, acc); acc = 0; }
         if constexpr (SPC) {
             par ^= h;
-            uint32_t klo = ((lam & QMAG) << 24) | ((uint32_t)i << 4);
-            uint32_t khi = (((lam >> 16) & QMAG) << 24) | ((uint32_t)i << 4);
+            const uint32_t mg = spc_mag(lam), wk = spc_word_key(i);
+            uint32_t klo = ((mg & 0xFFu) << 24) | wk;
+            uint32_t khi = (((mg >> 16) & 0xFFu) << 24) | wk;
             key_lo = __builtin_elementwise_min(key_lo, klo);
             key_hi = __builtin_elementwise_min(key_hi, khi);
         }
@@ -363,32 +526,113 @@ __device__ __forceinline__ void r1spc_body(const C &c, int s0, int n, int upos, 
     if (n < 16) bits_put_small(c, pos, n, acc);
     if constexpr (SPC) {
         par = row_xor(par);
-        key_lo = row_min_u32(key_lo | c.ln.br);
-        key_hi = row_min_u32(key_hi | c.ln.br);
-        uint32_t flip_lo = ((par & 0x8000u) && (key_lo & 15u) == c.ln.br) ? 1u : 0u;
-        uint32_t flip_hi = ((par & 0x80000000u) && (key_hi & 15u) == c.ln.br) ? 1u : 0u;
+        const uint32_t lk = c.ln.br << (LPAR - 4);
+        key_lo = row_min_u32(key_lo | lk);
+        key_hi = row_min_u32(key_hi | lk);
+        const uint32_t bm = 15u << (LPAR - 4);
+        uint32_t flip_lo = ((par & 0x8000u) && (key_lo & bm) == lk) ? 1u : 0u;
+        uint32_t flip_hi = ((par & 0x80000000u) && (key_hi & bm) == lk) ? 1u : 0u;
         if (flip_lo) {
-            int w = pos + (int)((key_lo >> 4) & 0xFFFFFu);
+            int w = pos + spc_key_word(key_lo);
             c.bst(w >> 4, c.bld(w >> 4) ^ (1u << (w & 15)));
         }
         if (flip_hi) {
-            int w = pos + (int)((key_hi >> 4) & 0xFFFFFu);
+            int w = pos + spc_key_word(key_hi);
             c.bst(w >> 4, c.bld(w >> 4) ^ (0x10000u << (w & 15)));
         }
     }
 }
 
-// G_R1_STATE (my_module.h:1571-1642) and G_SPC_STATE (my_module.h:1737-1842):
-// lambda = G(parent, bits[upos..]); x = sign(lambda); SPC additionally flips the first
-// minimum-|lambda| position (lexicographic (|l|, word, bitrev4(lane)) == Min_Mask_16_SM
-// tournament + strict '<' across words) when the parity of x is odd.
-// [i0, i1): the words of this wave (R1 split in whole 16-word chunks; SPC is never split).
 template <bool SPC, class C>
 __device__ __forceinline__ void op_r1spc(const C &c, int k, int n, int upos, int pos, int i0, int i1)
 {
     const int s0 = c.lvl_off(k);
     if (c.in_lds(s0)) r1spc_body<SPC, true>(c, s0, n, upos, pos, i0, i1);
     else r1spc_body<SPC, false>(c, s0, n, upos, pos, i0, i1);
+}
+
+// PAR > 16: the PRUNING_LEVEL 1 leaf decoders (R_STATE, my_module.h:566-593; library.h:
+// 187-280) of the PAR word whose P16 device words are the level-k node at `pos` (the LLRs
+// F / G wrote there): REP (kind 1) / SPC (2) / REP2 (3, sel 1) / SPC2 (4, sel 1), the pair
+// trees and tournaments over PAR positions (words at distance P16/2 .. 1 first, then the row).
+template <class C>
+__device__ __forceinline__ void op_pleaf(const C &c, int k, int pos, uint32_t kind)
+{
+    if constexpr (P16 > 1) {
+        const int s0 = c.lvl_off(k);   // a node of <= 4 words: always an LDS level
+        uint32_t v[P16];
+#pragma unroll
+        for (int j = 0; j < P16; j++) v[j] = c.ldl(s0 + j);
+        uint32_t x[P16];
+        if (kind == 1 || kind == 3) {
+            uint32_t t[P16];
+#pragma unroll
+            for (int j = 0; j < P16; j++) t[j] = v[j];
+#pragma unroll
+            for (int m = P16; m > 1; m /= 2)
+#pragma unroll
+                for (int j = 0; j < m / 2; j++) t[j] = CA2 ? pk_add(t[j], t[j + m / 2]) : G_sm<0>(t[j], t[j + m / 2], 0u);
+            uint32_t r;
+            if constexpr (CA2) {
+                r = t[0];
+                r = pk_add(r, xorlane<8>(r));
+                r = pk_add(r, xorlane<4>(r));
+                r = pk_add(r, xorlane<2>(r));
+                if (kind == 1) r = pk_add(r, xorlane<1>(r));
+                r &= SGN;
+            } else {
+                r = kind == 1 ? leaf_rep(t[0], c.ln) : leaf_rep2(t[0], c.ln);
+            }
+#pragma unroll
+            for (int j = 0; j < P16; j++) x[j] = r;
+        } else {
+            const bool spc2 = kind == 4;
+            uint32_t par = 0;
+#pragma unroll
+            for (int j = 0; j < P16; j++) par ^= v[j] & SGN;
+            par ^= xorlane<8>(par);
+            par ^= xorlane<4>(par);
+            par ^= xorlane<2>(par);
+            if (!spc2) par ^= xorlane<1>(par);
+            // keys: (magnitude, bitrev_LPAR(16 j + pos)); SIGMAG: the Q-1-bit |l|; CA2: qabs at
+            // QB bits (the wrapped -2^(QB-1) is the minimum), biased to stay non-negative
+            const uint32_t lk = c.ln.br << (LPAR - 4);
+            uint32_t klo = 0xFFFFFFFFu, khi = 0xFFFFFFFFu, mlo[P16], mhi[P16];
+#pragma unroll
+            for (int j = 0; j < P16; j++) {
+                const uint32_t mg = CA2 ? pk_add(ca2_qabs(v[j], QB), (1u << (QB - 1)) * 0x00010001u) : (v[j] & MAG);
+                const uint32_t wk = lk | bitrev_n((uint32_t)j, LPAR - 4);
+                mlo[j] = ((mg & 0xFFFFu) << 8) | wk;
+                mhi[j] = ((mg >> 16) << 8) | wk;
+                klo = __builtin_elementwise_min(klo, mlo[j]);
+                khi = __builtin_elementwise_min(khi, mhi[j]);
+            }
+            klo = __builtin_elementwise_min(klo, xorlane<8>(klo));
+            khi = __builtin_elementwise_min(khi, xorlane<8>(khi));
+            klo = __builtin_elementwise_min(klo, xorlane<4>(klo));
+            khi = __builtin_elementwise_min(khi, xorlane<4>(khi));
+            klo = __builtin_elementwise_min(klo, xorlane<2>(klo));
+            khi = __builtin_elementwise_min(khi, xorlane<2>(khi));
+            if (!spc2) {
+                klo = __builtin_elementwise_min(klo, xorlane<1>(klo));
+                khi = __builtin_elementwise_min(khi, xorlane<1>(khi));
+            }
+#pragma unroll
+            for (int j = 0; j < P16; j++) {
+                const uint32_t flo = (klo == mlo[j]) ? (par & 0x8000u) : 0u;
+                const uint32_t fhi = (khi == mhi[j]) ? (par & 0x80000000u) : 0u;
+                x[j] = (v[j] & SGN) ^ flo ^ fhi;
+            }
+        }
+        // x (sign-position flags per lane, word pos + j) into the partial sums
+#pragma unroll
+        for (int j = 0; j < P16; j++) {
+            const int wd = pos + j, b4 = wd & 15;
+            const uint32_t m = 0x10001u << b4;
+            const uint32_t d = c.bld(wd >> 4);
+            c.bst(wd >> 4, (d & ~m) | (x[j] >> (15 - b4)));
+        }
+    }
 }
 
 // H_STATE / H0_STATE (my_module.h:903-932, 1020-1042):
@@ -453,7 +697,7 @@ __device__ __forceinline__ bool op_split(int code, int n, int wpg)
 // at start and finish, to calibrate the clock.
 template <bool GMEM, bool TRACE = false>
 __device__ __forceinline__ void decode_body(
-    const int8_t *__restrict__ llr, uint16_t *__restrict__ out, const Op *__restrict__ ops,
+    const chan_t *__restrict__ llr, uint16_t *__restrict__ out, const Op *__restrict__ ops,
     uint32_t *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb,
     int group_dwords, int lds_dwords, int lds0, unsigned long long *__restrict__ trace = nullptr)
 {
@@ -478,8 +722,8 @@ __device__ __forceinline__ void decode_body(
     c.lb = smem + (size_t)gib * (size_t)lds_dwords + lane;
     // HBM part of the group: lds0 slots of 64 u16 (SM8 pairs), then the bit dwords
     uint32_t *const gbase = GMEM ? scratch + (size_t)group * (size_t)group_dwords : nullptr;
-    c.hs = GMEM ? (uint16_t *)gbase + lane : nullptr;
-    c.hbit = GMEM ? gbase + (size_t)lds0 * 32 + lane : nullptr;
+    c.hs = GMEM ? (slot_t *)gbase + lane : nullptr;
+    c.hbit = GMEM ? gbase + (size_t)lds0 * (SLOT16 ? 64 : 32) + lane : nullptr;
     long f_lo = group * 8 + row, f_hi = group * 8 + 4 + row;
     const long f_lo_c = f_lo < batch ? f_lo : (long)batch - 1;
     const long f_hi_c = f_hi < batch ? f_hi : (long)batch - 1;
@@ -543,8 +787,8 @@ __device__ __forceinline__ void decode_body(
         const int i0 = split ? (int)(((long)n * wi) / wpg) : 0;
         const int i1 = split ? (int)(((long)n * (wi + 1)) / wpg) : n;
         switch (code) {
-        case OP_F: op_fg<false>(c, k, n, -1, i0, i1); break;
-        case OP_G: op_fg<true>(c, k, n, upos, i0, i1); break;
+        case OP_F: op_fg<false>(c, k, n, -1, i0, i1, fb); break;
+        case OP_G: op_fg<true>(c, k, n, upos, i0, i1, fb); break;
         case OP_FLEAF: op_leaf<false>(c, k, pos, -1, fb); break;
         case OP_GLEAF: op_leaf<true>(c, k, pos, upos, fb); break;
         case OP_REP: op_rep(c, k, n, pos); break;
@@ -552,6 +796,7 @@ __device__ __forceinline__ void decode_body(
         case OP_SPC: op_r1spc<true>(c, k, n, upos, pos, 0, n); break;
         case OP_H: op_h<false>(c, pos, n, i0 >> 4, i1 >> 4); break;
         case OP_H0: op_h<true>(c, pos, n, i0 >> 4, i1 >> 4); break;
+        case OP_PLEAF: op_pleaf(c, k, pos, (fb >> 16) & 7u); break;
 #if POLAR_SC_SUBS
         case OP_SUB:
             // a whole subtree as generated straight-line code (hybrid plans, polar_sc_jit.cpp):

@@ -459,13 +459,17 @@ struct Gen {
 // subtree decoder per distinct mixed subtree of p.sub_words words. with_subs = false: the
 // plain interpreter alone, specialised on the plan's POLAR_Q (the per-op monitor of per-mask
 // plans whose LLR_BITS is not the hipcc-built 6).
-std::string hybrid_source(const polar_sc_plan &p, bool with_subs = true)
+std::string hybrid_source(const polar_sc_plan &p, bool with_subs = true, bool chan16 = false)
 {
     std::ostringstream o;
     const bool gm = p.gmem != 0;
     const int waves = with_subs ? p.hybrid_waves : HYBRID_MAX_WAVES;
+    int lpar = 0;
+    while ((16 << lpar) < p.cfg.par) lpar++;
     o << "#define POLAR_LANE_REMAP 1\n#define POLAR_SC_SUBS " << (with_subs ? 1 : 0) << "\n#define POLAR_Q "
-      << p.cfg.llr_bits << "\n#include \"polar_sc_interp.h\"\n";
+      << p.cfg.llr_bits << "\n#define POLAR_CA2 " << (p.cfg.sigmag ? 0 : 1) << "\n#define POLAR_EXT "
+      << (p.cfg.extended ? 1 : 0) << "\n#define POLAR_LPAR " << 4 + lpar << "\n#define POLAR_CHAN16 " << (chan16 ? 1 : 0)
+      << "\n#include \"polar_sc_interp.h\"\n";
     if (with_subs) {
         o << "namespace polar {\n#define CH(w) cin_[(w) * 64]\n";
         int lg = 0;
@@ -483,14 +487,14 @@ std::string hybrid_source(const polar_sc_plan &p, bool with_subs = true)
         o << "  default: return;\n  }\n}\n}  // namespace polar\n";
     }
     o << "extern \"C\" __global__ void __launch_bounds__(" << waves * 64 << ") polar_sc_hybrid_kernel(\n"
-      << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
+      << "    const polar::chan_t *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
       << "    unsigned int *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb, int group_dwords,\n"
       << "    int lds_dwords, int lds0)\n{\n"
       << "  polar::decode_body<" << (gm ? "true" : "false")
       << ">(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords, lds0);\n}\n"
       // the per-op monitor variant (polar_sc_trace)
       << "extern \"C\" __global__ void __launch_bounds__(" << waves * 64 << ") polar_sc_hybrid_trace_kernel(\n"
-      << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
+      << "    const polar::chan_t *__restrict__ llr, unsigned short *__restrict__ out, const polar::Op *__restrict__ ops,\n"
       << "    unsigned int *__restrict__ scratch, int N, int batch, int out_stride, int wpg, int gpb, int group_dwords,\n"
       << "    int lds_dwords, int lds0, unsigned long long *__restrict__ trace)\n{\n"
       << "  polar::decode_body<" << (gm ? "true" : "false")
@@ -606,6 +610,19 @@ int rtc_compile(const std::string &src, std::vector<char> &code, std::string &lo
     return 0;
 }
 }  // namespace
+
+// int16 channel (polar_sc_decode_i16): the interpreter of the plan's format on int16 LLRs
+int jit_load16(const polar_sc_plan &p, DevState &st)
+{
+    if (st.fn16) return 0;
+    if (p.code16.empty()) {
+        int rc = rtc_compile(hybrid_source(p, false, true), p.code16, p.jit_log);
+        if (rc) return rc;
+    }
+    if (hipModuleLoadData(&st.module16, p.code16.data()) != hipSuccess) return -EIO;
+    if (hipModuleGetFunction(&st.fn16, st.module16, "polar_sc_hybrid_kernel") != hipSuccess) return -EIO;
+    return 0;
+}
 
 int jit_compile(const polar_sc_plan &p)
 {

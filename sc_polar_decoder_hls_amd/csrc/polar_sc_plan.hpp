@@ -23,6 +23,8 @@ struct DevState {
     hipFunction_t fn_trace = nullptr;   // hybrid plans: the per-op monitor variant
     hipModule_t imodule = nullptr;      // per-mask plans with llr_bits != 6: hipRTC interpreter
     hipFunction_t ifn_trace = nullptr;  //   (per-op monitor only)
+    hipModule_t module16 = nullptr;     // interpreter on the int16 channel (polar_sc_decode_i16)
+    hipFunction_t fn16 = nullptr;
     int simds = 0;                // SIMDs of the device (4 per CU), for launch sizing
 };
 
@@ -37,7 +39,10 @@ struct HostBufs {
 
 // device-internal schedule records (never exported): the partial-sum window of HBM-scratch
 // plans, and the generated-subtree call of hybrid plans
-enum { POLAR_OP_WOPEN = 11, POLAR_OP_WFLUSH = 12, POLAR_OP_SUB = 13 };
+enum { POLAR_OP_WOPEN = 11, POLAR_OP_WFLUSH = 12, POLAR_OP_SUB = 13, POLAR_OP_PLEAF = 14 };
+// polar_sc_op.fb of G / GLEAF records inside a PAR-word leaf (PAR > 16): G_extended (no
+// clamp); bits 20..23: operand width above LLR_BITS (polar_sc_interp.h)
+constexpr uint32_t FB_EXACT = 1u << 19;
 
 // hybrid kernels: by default at most 8 waves per 8-frame group (one 512-thread block, the
 // kernel's launch bound); POLAR_SC_HYBRID_WAVES (4 or 8) at plan creation changes it.
@@ -49,12 +54,13 @@ constexpr int HYBRID_MAX_WAVES = 8;
 }  // namespace polar_host
 
 struct polar_sc_plan {
-    uint32_t N = 0, G = 0, K = 0;
+    uint32_t N = 0, G = 0, K = 0;    // G: 16-LLR device words (N / 16)
+    uint32_t GP = 0, p16 = 1;        // PAR groups (N / PAR), device words per group
     int lg = 0;                      // log2(N/16)
     polar_sc_config cfg{};
     std::vector<uint8_t> mask;       // N, 1 = information
-    std::vector<uint16_t> fb;        // G, Bit_Frozen (bit k = mask[16g+k])
-    std::vector<uint8_t> type;       // G, Node_Type
+    std::vector<uint64_t> fbp;       // GP, Bit_Frozen (bit k = mask[PAR g + k])
+    std::vector<uint8_t> type;       // GP, Node_Type
     std::vector<polar_sc_op> ops;
     std::vector<polar_sc_op> dev_ops;   // device copy when it differs (HBM-scratch plans)
     polar_sc_plan_stats stats{};
@@ -76,6 +82,7 @@ struct polar_sc_plan {
     mutable std::map<int, polar_host::HostBufs> host_bufs;
     mutable std::vector<char> jit_code;   // compiled code object (lazily built)
     mutable std::vector<char> interp_code;   // per-mask plans, llr_bits != 6: traced interpreter
+    mutable std::vector<char> code16;        // interpreter on the int16 channel (polar_sc_decode_i16)
     mutable std::string jit_log;
 };
 
@@ -90,6 +97,7 @@ int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, ui
 int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
                       int out_stride, int wpg, void *stream, unsigned long long *trace = nullptr);
 int jit_load_interp(const polar_sc_plan &p, DevState &st);
+int jit_load16(const polar_sc_plan &p, DevState &st);
 int launch_interp_fn(hipFunction_t fn, const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out,
                      long batch, int out_stride, int wpg, void *stream, unsigned long long *trace);
 bool jit_supported(uint32_t N);

@@ -48,7 +48,7 @@ def test_plan_argument_validation(pkg):
             pkg.Decoder(np.ones(N, np.uint8))
         assert e.value.rc == -22
     c = pkg.default_config()
-    c.llr_bits = 9
+    c.llr_bits = 10
     with pytest.raises(pkg.PolarError) as e:
         pkg.Decoder(np.ones(64, np.uint8), c)
     assert e.value.rc == -95

@@ -1,0 +1,97 @@
+"""GPU parity across the reference's swept datapath formats: PAR 16 / 32 / 64
+(polar_parameters.h:8; script_tests.sh:11,124 sweeps 16 and 64), CA2 vs SIGMAG (config.h:11;
+script/parser.sh:15,43), EXTENDED 0/1 (config.h:14) and LLR_BITS up to 9 (parser_comp.sh:12;
+int16 channel). Every format runs the schedule interpreter compiled by hipRTC with its
+POLAR_* switches and must equal the literal FSM at the same format bit for bit, on AWGN
+frames, on the whole input range (incl. the -2^(Q-1) wrap of CA2) and under PRUNING_LEVEL 0 /
+1 / 2 configurations. Masks cover the LDS (N <= 4096) and HBM-scratch (N = 16384) storage."""
+import numpy as np
+import pytest
+
+import util
+from test_gpu_parity import _assert_same
+
+pytestmark = pytest.mark.gpu
+
+# (par, sigmag, extended, llr_bits)
+FORMATS = [
+    (16, 0, 1, 6), (16, 0, 1, 8), (16, 0, 0, 6), (16, 1, 0, 6), (16, 1, 1, 9), (16, 0, 1, 9),
+    (32, 1, 1, 6), (32, 0, 1, 6), (64, 1, 1, 6), (64, 1, 1, 8), (64, 0, 1, 6), (64, 1, 0, 6), (64, 0, 0, 8),
+    (64, 1, 1, 9),
+]
+CONFIGS = ((2, 1, 1, 1, 0, 0, 1), (1, 1, 1, 1, 1, 1, 0), (0, 0, 0, 0, 0, 0, 0), (2, 1, 1, 1, 1, 1, 0))
+
+
+def _planted_mask(rng, N, par):
+    """Random mask with PAR groups of every pruned class (R0 / R1 / REP / SPC / REP2 / SPC2)."""
+    all1 = (1 << par) - 1
+    pats = [0, all1, 1 << (par - 1), all1 & ~1, 3 << (par - 2), all1 & ~3]
+    mask = (rng.random(N) < 0.5).astype(np.uint8)
+    for g in range(N // par):
+        if rng.random() < 0.6:
+            p = int(rng.choice(pats))
+            mask[par * g:par * g + par] = [(p >> k) & 1 for k in range(par)]
+    return mask
+
+
+def _decoder(pkg, mask, fmt, c7):
+    par, sigmag, ext, q = fmt
+    c = pkg.default_config()
+    (c.pruning_level, c.elag_r1, c.elag_rep, c.elag_spc, c.elag_rep2, c.elag_spc2, c.elag_h0) = c7
+    c.par, c.sigmag, c.extended, c.llr_bits = par, sigmag, ext, q
+    return pkg.Decoder(mask, config=c)
+
+
+@pytest.mark.parametrize("fmt", FORMATS, ids=lambda f: "p%d_%s_e%d_q%d" % (f[0], "sm" if f[1] else "ca2", f[2], f[3]))
+def test_formats_vs_oracle(pkg, cuda, oracle_mod, fmt):
+    par, sigmag, ext, q = fmt
+    rng = np.random.default_rng(par * 7 + sigmag * 3 + ext + q * 11)
+    amp = (1 << (q - 1)) - 1
+    masks = [("FB_N1024_K512", util.mask("FB_N1024_K512")), ("planted_4096", _planted_mask(rng, 4096, par)),
+             ("frozen_n_16384_k_8192", util.mask("frozen_n_16384_k_8192"))]
+    for name, mask in masks:
+        B = 24 if mask.size <= 4096 else 9
+        awgn, _ = util.synth_frames(mask, B // 2, ebn0_db=1.0, seed=q)
+        awgn = np.clip(awgn.astype(np.int32) * (1 << q) // 64, -amp, amp)
+        edge = rng.integers(-(amp + 1), amp + 1, size=(B - B // 2, mask.size))
+        edge[:, rng.integers(0, mask.size, 64)] = -(amp + 1)          # the -2^(Q-1) corner
+        llr = np.concatenate([awgn, edge]).astype(np.int16 if q > 8 else np.int8)
+        for c7 in CONFIGS:
+            dec = _decoder(pkg, mask, fmt, c7)
+            out = dec.decode(cuda.from_numpy(llr).cuda())
+            cuda.cuda.synchronize()
+            got = pkg.unpack_bits(out.cpu().numpy(), mask.size)
+            ref = oracle_mod.decode_fsm(mask, llr, config=c7, llr_bits=q, par=par, sigmag=sigmag, extended=ext)
+            _assert_same(got, ref, "%s fmt %s cfg %s storage %d" % (name, fmt, c7, dec.stats["storage"]))
+
+
+@pytest.mark.parametrize("q", [6, 9])
+def test_int16_channel_matches_int8(pkg, cuda, oracle_mod, q):
+    """polar_sc_decode_i16: int16 frames decode like the same values as int8 (where they fit),
+    for the shipped format too (whose int8 path is the per-mask kernel)."""
+    mask = util.mask("FB_N1024_K512")
+    llr, _ = util.synth_frames(mask, 32, ebn0_db=2.0, seed=16)
+    c = pkg.default_config()
+    c.llr_bits = q
+    dec = pkg.Decoder(mask, config=c)
+    a = dec.decode(cuda.from_numpy(llr).cuda())
+    b = dec.decode(cuda.from_numpy(llr.astype(np.int16)).cuda())
+    cuda.cuda.synchronize()
+    assert (a.cpu().numpy() == b.cpu().numpy()).all()
+    _assert_same(pkg.unpack_bits(b.cpu().numpy(), mask.size), oracle_mod.decode_fsm(mask, llr, llr_bits=q), "i16")
+
+
+def test_formats_noiseless_full_size(pkg, cuda):
+    """PAR 64 and CA2 at a full C2 batch (65536 frames): noiseless codewords decode exactly
+    (size-independent property)."""
+    mask = util.mask("FB_N1024_K512")
+    rng = np.random.default_rng(64)
+    u = rng.integers(0, 2, size=(65536, mask.size), dtype=np.uint8) & mask[None, :]
+    x = util.encode_np(u)
+    llr = np.where(x == 1, -17, 17).astype(np.int8)
+    t = cuda.from_numpy(llr).cuda()
+    for fmt in ((64, 1, 1, 6), (16, 0, 1, 6), (64, 0, 0, 8)):
+        dec = _decoder(pkg, mask, fmt, (2, 1, 1, 1, 0, 0, 1))
+        out = dec.decode(t)
+        cuda.cuda.synchronize()
+        assert (pkg.unpack_bits(out.cpu().numpy(), mask.size) == x).all(), fmt

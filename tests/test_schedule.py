@@ -154,8 +154,42 @@ def test_sweep_configs_change_results(pkg, oracle_mod):
 
 def test_unsupported_configs(pkg):
     mask = util.mask("FB_N128_K64")
-    for field, val in (("elag_rare", 1), ("llr_bits", 9), ("llr_bits", 4), ("par", 64), ("sigmag", 0), ("pruning_level", 3)):
+    for field, val in (("elag_rare", 1), ("llr_bits", 10), ("llr_bits", 4), ("par", 8), ("par", 128), ("par", 48),
+                       ("sigmag", 2), ("extended", 2), ("pruning_level", 3)):
         c = pkg.default_config()
         setattr(c, field, val)
         with pytest.raises(pkg.PolarError):
             pkg.Decoder(mask, config=c)
+    # N must hold two PAR words (INIT, my_module.h:294-309)
+    c = pkg.default_config()
+    c.par = 64
+    with pytest.raises(pkg.PolarError):
+        pkg.Decoder(np.ones(64, np.uint8), config=c)
+    for field, val in (("llr_bits", 9), ("par", 64), ("par", 32), ("sigmag", 0), ("extended", 0)):
+        c = pkg.default_config()
+        setattr(c, field, val)
+        dec = pkg.Decoder(mask, config=c)
+        assert dec.stats["kernel"] == 2   # the interpreter compiled for the format
+
+
+@pytest.mark.parametrize("par", [32, 64])
+def test_schedule_par_words_equals_fsm(pkg, oracle_mod, par):
+    """PAR 32 / 64 (polar_parameters.h:8; script_tests.sh:11 sweeps 16 and 64): the schedule of
+    16-LLR device words -- PAR-word leaves expanded into exact F / G / leaf records, PR1 leaf
+    decoders as PLEAF records, REP / SPC per PAR word -- interpreted in numpy equals the
+    literal FSM at that PAR under every pruning-sweep configuration."""
+    rng = np.random.default_rng(par)
+    for c7 in oracle_mod.SWEEP_CONFIGS + (None,):
+        for name in ("FB_N1024_K512", "frozen_n_2048_k_1024", "frozen_n_4096_k_2048"):
+            mask = util.mask(name)
+            cfg = pkg.default_config()
+            cfg.par = par
+            if c7 is not None:
+                (cfg.pruning_level, cfg.elag_r1, cfg.elag_rep, cfg.elag_spc, cfg.elag_rep2, cfg.elag_spc2,
+                 cfg.elag_h0) = c7
+            dec = pkg.Decoder(mask, cfg)
+            llr, _ = util.synth_frames(mask, 12, ebn0_db=1.0, seed=par)
+            llr[:, :40] = rng.integers(-32, 32, size=(12, 40))
+            got = util.run_schedule(dec.schedule(), mask.size, llr, par=par)
+            np.testing.assert_array_equal(got, oracle_mod.decode_fsm(mask, llr, config=c7, par=par),
+                                          err_msg="%s %s" % (name, c7))

@@ -63,9 +63,10 @@ def synth_frames(info_mask, batch, ebn0_db=2.5, seed=0xF0, rate=None):
 # ----------------------------------------------------------------------------------------
 # numpy SM primitives: values are (s, m) int arrays
 # ----------------------------------------------------------------------------------------
-def sm_from_llr(llr):
-    t = ((llr.astype(np.int32) & 63) ^ 32) - 32          # sign-extend 6 bits
-    m = np.abs(t) & 31
+def sm_from_llr(llr, q=6):
+    h = 1 << (q - 1)
+    t = ((llr.astype(np.int32) & (2 * h - 1)) ^ h) - h   # sign-extend q bits
+    m = np.abs(t) & (h - 1)
     s = ((t < 0) & (m != 0)).astype(np.int32)
     return s, m
 
@@ -102,26 +103,27 @@ def leaf(lam, fb):
 
 
 def leaf_kind(lam, kind):
-    """PRUNING_LEVEL 1 leaf decoders (POLAR_LEAF_REP/SPC/REP2/SPC2) on lam = (s, m) [B, 16]."""
+    """PRUNING_LEVEL 1 leaf decoders (POLAR_LEAF_REP/SPC/REP2/SPC2) on lam = (s, m) [B, P]."""
     s, m = lam
-    B = s.shape[0]
-    if kind in (1, 3):                      # REP_REP2_16_SM: folds 8, 4, 2 (exact), then REP_2
+    B, P = s.shape
+    L = P.bit_length() - 1
+    if kind in (1, 3):                      # REP_REP2_P_SM: folds P/2 .. 2 (exact), then REP_2
         ts, tm = s, m
-        n = 16
+        n = P
         while n > 2:
             h = n // 2
             ts, tm = G((ts[:, :h], tm[:, :h]), (ts[:, h:n], tm[:, h:n]), 0)
             n = h
         if kind == 1:
             sig = np.where(tm[:, 0] < tm[:, 1], ts[:, 1], ts[:, 0])
-            return np.repeat(sig[:, None], 16, axis=1)
-        return np.tile(ts[:, :2], (1, 8))
-    # SPC / SPC2: flip the tournament minimum (ties -> smallest bitrev4) of the whole word or
+            return np.repeat(sig[:, None], P, axis=1)
+        return np.tile(ts[:, :2], (1, P // 2))
+    # SPC / SPC2: flip the tournament minimum (ties -> smallest bitrev_L) of the whole word or
     # of each class of even / odd positions when its sign parity is odd
-    br = np.array([int("{:04b}".format(l)[::-1], 2) for l in range(16)])
-    key = (m << 4) | br[None, :]
+    br = np.array([int(format(l, "0%db" % L)[::-1], 2) for l in range(P)])
+    key = (m << L) | br[None, :]
     x = s.copy()
-    classes = [np.arange(16)] if kind == 2 else [np.arange(0, 16, 2), np.arange(1, 16, 2)]
+    classes = [np.arange(P)] if kind == 2 else [np.arange(0, P, 2), np.arange(1, P, 2)]
     for c in classes:
         par = s[:, c].sum(axis=1) & 1
         j = c[key[:, c].argmin(axis=1)]
@@ -139,14 +141,19 @@ def rep_tree(lam):
     return s[:, 0], m[:, 0]
 
 
-def run_schedule(ops, N, llr):
-    """Interpret a compiled schedule (list of dicts from Decoder.schedule()) on a batch."""
+def run_schedule(ops, N, llr, par=16, q=6):
+    """Interpret a compiled schedule (list of dicts from Decoder.schedule(), SIGMAG) on a
+    batch. Records count 16-LLR words; PAR > 16 groups are par / 16 consecutive words."""
     B = llr.shape[0]
     Gw = N // 16
-    s, m = sm_from_llr(llr)
+    P16 = par // 16
+    L = par.bit_length() - 1
+    gsat, repsat = (1 << (q - 2)) - 1, (1 << (q + L - 1)) - 1
+    s, m = sm_from_llr(llr, q)
     chan = (s.reshape(B, Gw, 16), m.reshape(B, Gw, 16))
     buf = {0: chan}
     bits = np.zeros((B, Gw, 16), dtype=np.int32)
+    brp = np.array([int(format(l, "0%db" % L)[::-1], 2) for l in range(par)])
 
     def words(k, lo, hi):
         return buf[k][0][:, lo:hi], buf[k][1][:, lo:hi]
@@ -156,8 +163,12 @@ def run_schedule(ops, N, llr):
             return 0
         return bits[:, upos:upos + n]
 
+    def flat(x, i):   # PAR word i of a [B, n, 16] array as [B, par] positions
+        return x[:, i * P16:(i + 1) * P16].reshape(x.shape[0], par)
+
     for op in ops:
         code, k, n, pos, upos, fb = op["op"], op["level"], op["n"], op["pos"], op["upos"], op["fb"]
+        exact = bool(fb & (1 << 19))
         if code == "END":
             break
         if code in ("F", "G", "FLEAF", "GLEAF", "REP", "R1", "SPC"):
@@ -165,28 +176,34 @@ def run_schedule(ops, N, llr):
         if code == "F":
             buf[k + 1] = F(a, b)
         elif code == "G":
-            buf[k + 1] = G(a, b, ubits(upos, n), 15)
+            buf[k + 1] = G(a, b, ubits(upos, n), None if exact else gsat)
         elif code in ("FLEAF", "GLEAF"):
-            lam = F(a, b) if code == "FLEAF" else G(a, b, ubits(upos, 1), 15)
+            lam = F(a, b) if code == "FLEAF" else G(a, b, ubits(upos, 1), None if exact else gsat)
             w = (lam[0][:, 0], lam[1][:, 0])
-            bits[:, pos] = leaf(w, fb & 0xFFFF) if (fb >> 16) == 0 else leaf_kind(w, fb >> 16)
+            kind = (fb >> 16) & 7
+            bits[:, pos] = leaf(w, fb & 0xFFFF) if kind == 0 else leaf_kind(w, kind)
+        elif code == "PLEAF":
+            w = (buf[k][0][:, 0:n].reshape(B, par), buf[k][1][:, 0:n].reshape(B, par))
+            bits[:, pos:pos + n] = leaf_kind(w, (fb >> 16) & 7).reshape(B, n, 16)
         elif code == "REP":
             lam = F(a, b)
             acc = (np.zeros(B, np.int32), np.zeros(B, np.int32))
-            for i in range(n):
-                t = rep_tree((lam[0][:, i], lam[1][:, i]))
-                acc = G(t, acc, 0, 511)
+            for i in range(n // P16):
+                t = rep_tree((flat(lam[0], i), flat(lam[1], i)))
+                acc = G(t, acc, 0, repsat)
             bits[:, pos:pos + n] = acc[0][:, None, None]
         elif code in ("R1", "SPC"):
-            lam = G(a, b, ubits(upos, n), 15)
+            lam = G(a, b, ubits(upos, n), gsat)
             h = lam[0].copy()
             if code == "SPC":
-                par = h.reshape(B, -1).sum(axis=1) & 1
-                br = np.array([int("{:04b}".format(l)[::-1], 2) for l in range(16)])
-                key = (lam[1] << 24) | (np.arange(n)[None, :, None] << 4) | br[None, None, :]
+                par_ = h.reshape(B, -1).sum(axis=1) & 1
+                wi = np.arange(n)
+                # key: (|l|, PAR word, bitrev_L(position in the PAR word))
+                posp = (wi % P16)[:, None] * 16 + np.arange(16)[None, :]
+                key = (lam[1].astype(np.int64) << 32) | ((wi // P16)[None, :, None] << L) | brp[posp][None, :, :]
                 idx = key.reshape(B, -1).argmin(axis=1)
                 fl = np.zeros(B * n * 16, dtype=np.int32)
-                fl[np.arange(B) * n * 16 + idx] = par
+                fl[np.arange(B) * n * 16 + idx] = par_
                 h ^= fl.reshape(B, n, 16)
             bits[:, pos:pos + n] = h
         elif code == "H":
