@@ -111,7 +111,10 @@ enum {
     POLAR_LEAF_REP = 1,     /* Spec_REP_Node (library.h:189-210, functions.h:1167-1176)     */
     POLAR_LEAF_SPC = 2,     /* Spec_SPC_Node (library.h:235-256, functions.h:2111-2136)     */
     POLAR_LEAF_REP2 = 3,    /* Spec_REP_REP2_Node, sel 1 (library.h:212-233, functions.h:1353-1420) */
-    POLAR_LEAF_SPC2 = 4     /* Spec_SPC_SPC2_Node, sel 1 (library.h:258-280, functions.h:2786-2811) */
+    POLAR_LEAF_SPC2 = 4,    /* Spec_SPC_SPC2_Node, sel 1 (library.h:258-280, functions.h:2786-2811) */
+    POLAR_LEAF_R1 = 5       /* Spec_Node_R1 (library.h:180-185): the hard decisions. SIGMAG plans
+                               decode R1 groups with the plain leaf, which gives the same bits;
+                               in CA2 it does not (F has no -0) */
 };
 
 typedef struct polar_sc_plan_stats {

@@ -14,7 +14,8 @@ SOURCES = [os.path.join(PKG, "csrc", "polar_sc_kernels.hip"), os.path.join(PKG, 
            os.path.join(PKG, "csrc", "polar_sc_tables.cpp")]
 DEVICE_H = os.path.join(PKG, "csrc", "polar_sc_device.h")
 INTERP_H = os.path.join(PKG, "csrc", "polar_sc_interp.h")
-HEADERS = [os.path.join(ROOT, "include", "polar_sc.h"), DEVICE_H, INTERP_H, os.path.join(PKG, "csrc", "polar_sc_plan.hpp")]
+HEADERS = [os.path.join(ROOT, "include", "polar_sc.h"), DEVICE_H, INTERP_H, os.path.join(PKG, "csrc", "polar_sc_plan.hpp"),
+           os.path.join(PKG, "csrc", "polar_sc_glibcf.h")]
 GEN_DIR = os.path.join(PKG, "build")
 CLI_SRC = os.path.join(ROOT, "examples", "polar_decode_cli.c")
 CLI = os.path.join(PKG, "lib", "polar_decode_cli")

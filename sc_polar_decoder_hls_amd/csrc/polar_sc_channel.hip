@@ -11,10 +11,12 @@
 // generated in parallel, one thread per frame.
 //
 // Float results follow the reference's operation order with contraction off; logf / sinf /
-// cosf come from the device math library, so a quantized LLR can differ by 1 from the
-// x86 glibc C-sim when the unquantized value lies within an ulp of a step (tests bound it).
+// cosf are glibc's own algorithms (polar_sc_glibcf.h, checked bit for bit against the host's
+// glibc over their whole input domain here), so the LLRs equal the x86 C-sim's exactly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "polar_sc_glibcf.h"
 
 #include <cerrno>
 #include <cstring>
@@ -167,8 +169,8 @@ __global__ void __launch_bounds__(256) csim_kernel(const uint32_t *__restrict__ 
         for (uint32_t k = 0; k < 8; k++) {
             const float r1 = 1.0f - (float)xs_next(a0, a1, a2, a3) * (1.0f / 4294967296.0f);
             const float y = PI2 * (1.0f - (float)xs_next(b0, b1, b2, b3) * (1.0f / 4294967296.0f));
-            const float x = sqrtf(-2.0f * logf(r1));
-            const float noise[2] = {x * sinf(y), x * cosf(y)};
+            const float x = sqrtf(-2.0f * glibcf::logf(r1));
+            const float noise[2] = {x * glibcf::sinf(y), x * glibcf::cosf(y)};
             for (int h = 0; h < 2; h++) {
                 const uint32_t i = base + 2 * k + (uint32_t)h;
                 const uint32_t bit = c ? (c[i] & 1u) : 0u;

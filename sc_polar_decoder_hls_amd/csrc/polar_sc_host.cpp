@@ -62,8 +62,8 @@ uint32_t classify_group(uint64_t fb, uint32_t par, const polar_sc_config &c)
 
 // PRUNING_LEVEL 1 leaf decoders selected in R_STATE by the group's class
 // (my_module.h:566-593; library.h:175-280): REP / SPC, or with ELAG_REP2 / ELAG_SPC2 the
-// REP_REP2 / SPC_SPC2 decoders (sel = class bit 0). R0 and R1 groups give the plain leaf's
-// result (all zero / the hard decisions), so they keep the plain leaf.
+// REP_REP2 / SPC_SPC2 decoders (sel = class bit 0). R0 groups give the plain leaf's result
+// (all zero); so do R1 groups in SIGMAG (the hard decisions), not in CA2.
 uint32_t leaf_kind(const polar_sc_plan &p, uint32_t g)
 {
     if (p.cfg.pruning_level != 1) return POLAR_LEAF_PLAIN;
@@ -72,6 +72,7 @@ uint32_t leaf_kind(const polar_sc_plan &p, uint32_t g)
     case NODE_SPC: return POLAR_LEAF_SPC;
     case NODE_REP2: return p.cfg.elag_rep ? POLAR_LEAF_REP2 : POLAR_LEAF_PLAIN;
     case NODE_SPC2: return p.cfg.elag_spc ? POLAR_LEAF_SPC2 : POLAR_LEAF_PLAIN;
+    case NODE_R1: return p.cfg.sigmag ? POLAR_LEAF_PLAIN : POLAR_LEAF_R1;
     default: return POLAR_LEAF_PLAIN;
     }
 }

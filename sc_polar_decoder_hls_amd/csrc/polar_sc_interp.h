@@ -278,6 +278,7 @@ __device__ __forceinline__ void op_fg(const C &c, int k, int n, int upos, int i0
 // configured format: REP / REP2 (sel 1) / SPC / SPC2 (sel 1); w: operand width
 __device__ __forceinline__ uint32_t leaf_kind_dp(uint32_t L, uint32_t kind, const Lanes &ln, int w)
 {
+    if (kind == 5) return L & SGN;   // Spec_Node_R1: VECTOR_SIGN
     if constexpr (!CA2) {
         switch (kind) {
         case 1: return leaf_rep(L, ln);
@@ -564,7 +565,10 @@ __device__ __forceinline__ void op_pleaf(const C &c, int k, int pos, uint32_t ki
 #pragma unroll
         for (int j = 0; j < P16; j++) v[j] = c.ldl(s0 + j);
         uint32_t x[P16];
-        if (kind == 1 || kind == 3) {
+        if (kind == 5) {   // Spec_Node_R1: VECTOR_SIGN
+#pragma unroll
+            for (int j = 0; j < P16; j++) x[j] = v[j] & SGN;
+        } else if (kind == 1 || kind == 3) {
             uint32_t t[P16];
 #pragma unroll
             for (int j = 0; j < P16; j++) t[j] = v[j];

@@ -107,6 +107,8 @@ def leaf_kind(lam, kind):
     s, m = lam
     B, P = s.shape
     L = P.bit_length() - 1
+    if kind == 5:                           # Spec_Node_R1
+        return s.copy()
     if kind in (1, 3):                      # REP_REP2_P_SM: folds P/2 .. 2 (exact), then REP_2
         ts, tm = s, m
         n = P
