@@ -95,3 +95,45 @@ def test_formats_noiseless_full_size(pkg, cuda):
         out = dec.decode(t)
         cuda.cuda.synchronize()
         assert (pkg.unpack_bits(out.cpu().numpy(), mask.size) == x).all(), fmt
+
+
+def _sweep_cfg(pkg, c7, par):
+    c = pkg.default_config()
+    (c.pruning_level, c.elag_r1, c.elag_rep, c.elag_spc, c.elag_rep2, c.elag_spc2, c.elag_h0) = c7
+    c.par, c.llr_bits = par, 8
+    return c
+
+
+@pytest.mark.parametrize("par", [16, 64])
+def test_script_tests_pruning_sweep(pkg, cuda, oracle_mod, par, monkeypatch):
+    """script/script_tests.sh:103-213 as the reference runs it: the 11 pruning configurations
+    on frozen_n_32768_k_29492 (its lines 105-106) at QUANT 8, for PAR 16 and 64 (line 124).
+    PAR 16 plans run on the schedule interpreter here (POLAR_SC_JIT=0, one code object for
+    the format); the generated-subtree kernels are swept in test_gpu_configs.py."""
+    monkeypatch.setenv("POLAR_SC_JIT", "0")
+    mask = util.mask("frozen_n_32768_k_29492")
+    awgn, _ = util.synth_frames(mask, 8, ebn0_db=3.5, seed=par)
+    llr = np.clip(awgn.astype(np.int32) * 4, -127, 127).astype(np.int8)
+    t = cuda.from_numpy(llr).cuda()
+    for c7 in oracle_mod.SWEEP_CONFIGS:
+        dec = pkg.Decoder(mask, config=_sweep_cfg(pkg, c7, par))
+        out = dec.decode(t)
+        cuda.cuda.synchronize()
+        got = pkg.unpack_bits(out.cpu().numpy(), mask.size)
+        _assert_same(got, oracle_mod.decode_fsm(mask, llr, config=c7, llr_bits=8, par=par), "PAR %d %s" % (par, c7))
+
+
+@pytest.mark.parametrize("par", [16, 64])
+@pytest.mark.parametrize("name", ["frozen_n_2048_k_1844", "frozen_n_4096_k_3686", "frozen_n_8192_k_7372",
+                                  "frozen_n_16384_k_14746"])
+def test_script_tests_rate09_codes(pkg, cuda, oracle_mod, par, name):
+    """script/script_tests.sh:7-58: the rate-0.9 codes N = 2048 .. 16384 at QUANT 8, PAR 16 and
+    64, shipped pruning configuration (PAR 16: the per-mask / hybrid kernels)."""
+    mask = util.mask(name)
+    awgn, _ = util.synth_frames(mask, 16, ebn0_db=4.0, seed=par)
+    llr = np.clip(awgn.astype(np.int32) * 4, -127, 127).astype(np.int8)
+    dec = pkg.Decoder(mask, config=_sweep_cfg(pkg, oracle_mod.DEFAULT_CONFIG, par))
+    out = dec.decode(cuda.from_numpy(llr).cuda())
+    cuda.cuda.synchronize()
+    got = pkg.unpack_bits(out.cpu().numpy(), mask.size)
+    _assert_same(got, oracle_mod.decode_fsm(mask, llr, llr_bits=8, par=par), "%s PAR %d" % (name, par))

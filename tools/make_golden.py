@@ -76,6 +76,11 @@ TABLES = [
     ("frozen_n_8192_k_4096", "mask", "Generated_Frozen_Bit/frozen_n_8192_k_4096.txt", 8192, 4096),
     ("frozen_n_16384_k_8192", "mask", "Generated_Frozen_Bit/frozen_n_16384_k_8192.txt", 16384, 8192),
     ("frozen_n_32768_k_29492", "mask", "Generated_Frozen_Bit/frozen_n_32768_k_29492.txt", 32768, 29492),
+    # the rate-0.9 codes of script/script_tests.sh:7-8 (PAR 16 / 64 sweep at QUANT 8)
+    ("frozen_n_2048_k_1844", "mask", "Generated_Frozen_Bit/frozen_n_2048_k_1844.txt", 2048, 1844),
+    ("frozen_n_4096_k_3686", "mask", "Generated_Frozen_Bit/frozen_n_4096_k_3686.txt", 4096, 3686),
+    ("frozen_n_8192_k_7372", "mask", "Generated_Frozen_Bit/frozen_n_8192_k_7372.txt", 8192, 7372),
+    ("frozen_n_16384_k_14746", "mask", "Generated_Frozen_Bit/frozen_n_16384_k_14746.txt", 16384, 14746),
     ("frozen_n_65536_k_32768", "mask", "Generated_Frozen_Bit/frozen_n_65536_k_32768.txt", 65536, 32768),
     ("frozen_n_262144_k_131072", "mask", "Generated_Frozen_Bit/frozen_n_262144_k_131072.txt", 262144, 131072),
 ]

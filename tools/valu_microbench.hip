@@ -52,9 +52,11 @@ __global__ void __launch_bounds__(256) bench(unsigned *out, unsigned long long *
     const unsigned k = 0x01230123u;
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), w0 = __builtin_amdgcn_s_memrealtime();
-    for (int i = 0; i < iters; i++) {
+    // 64 instructions per loop iteration: the loop branch (an instruction-buffer refill for a
+    // lone wave) stays below 2 % of the issue time
+    for (int i = 0; i < iters; i += 8) {
 #pragma unroll
-        for (int rep = 0; rep < 8 / CHAINS; rep++) {
+        for (int rep = 0; rep < 64 / CHAINS; rep++) {
 #pragma unroll
             for (int c = 0; c < CHAINS; c++) op<OP>(r[c], k);
         }
@@ -87,7 +89,7 @@ void one(unsigned *buf, unsigned long long *st, int cus, int wps)
     }
     std::sort(cyc.begin(), cyc.end());
     std::sort(ghz.begin(), ghz.end());
-    const double insts = 8.0 * iters;
+    const double insts = 8.0 * iters;   // iters / 8 iterations x 64 instructions
     const double med = cyc[cyc.size() / 2];
     // CHAINS == 8: throughput per SIMD (waves share the SIMD); CHAINS == 1: dependent latency
     printf("{\"op\": \"%s\", \"chains\": %d, \"waves_per_simd\": %d, \"cycles_per_wave_inst_per_simd\": %.3f, "
