@@ -139,6 +139,11 @@ typedef struct polar_sc_plan_stats {
     uint32_t sub_words;               /* hybrid: subtree size in 16-LLR words, else 0     */
     uint32_t n_sub_kinds;             /* hybrid: distinct generated subtree decoders      */
     uint32_t n_sub_calls;             /* hybrid: subtree decoder calls per frame group    */
+    uint32_t tier_steps;              /* hybrid, large N: launches per decode of the grid
+                                         tier (upper-level F / G over all frame groups +
+                                         the schedule segments between them), else 0     */
+    uint32_t tier_words;              /* grid tier: F / G records of >= this many output
+                                         words run grid-wide, else 0                     */
 } polar_sc_plan_stats;
 
 /* Fill *cfg with the reference configuration (config.h as shipped). */

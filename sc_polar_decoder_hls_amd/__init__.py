@@ -70,7 +70,8 @@ class polar_sc_plan_stats(ctypes.Structure):
                 ("op_count", ctypes.c_uint32 * 16), ("word_ops", ctypes.c_uint64),
                 ("storage", ctypes.c_uint32), ("lds_bytes_per_wave", ctypes.c_uint32),
                 ("scratch_bytes_per_wave", ctypes.c_uint64), ("kernel", ctypes.c_uint32),
-                ("sub_words", ctypes.c_uint32), ("n_sub_kinds", ctypes.c_uint32), ("n_sub_calls", ctypes.c_uint32)]
+                ("sub_words", ctypes.c_uint32), ("n_sub_kinds", ctypes.c_uint32), ("n_sub_calls", ctypes.c_uint32),
+                ("tier_steps", ctypes.c_uint32), ("tier_words", ctypes.c_uint32)]
 
 
 # exported symbols of include/polar_sc.h (tests check that the library exports all of them)

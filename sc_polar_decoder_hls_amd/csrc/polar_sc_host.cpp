@@ -157,6 +157,63 @@ void window_schedule(polar_sc_plan &p, const std::vector<polar_sc_op> &ops)
     }
 }
 
+// Grid tier: cut the device schedule of a hybrid HBM-scratch plan at every F / G record of
+// at least `tw` output words (the upper tree levels; their source and destination levels are
+// HBM slots). Those records become grid-wide launches over all frame groups; the records
+// between them become segments for the hybrid kernel, closed by POLAR_OP_SEGEND (the last one
+// by the END record) and opened by POLAR_OP_SEGCONT after the first. The H / H0 records of
+// the cut nodes stay in the segments, in schedule order, so every launch sees the partial
+// sums of the launches before it (kernel boundaries order the HBM traffic).
+void tier_schedule(polar_sc_plan &p, int tw)
+{
+    p.tier.clear();
+    p.seg_ops.clear();
+    p.tier_words = 0;
+    const std::vector<polar_sc_op> &ops = p.dev_ops;
+    bool any = false;
+    for (const polar_sc_op &o : ops)
+        if ((o.code == POLAR_OP_F || o.code == POLAR_OP_G) && o.n >= tw) any = true;
+    if (!any) return;
+    bool open = false;
+    auto mark = [&](int code) {
+        polar_sc_op o{};
+        o.code = code;
+        o.upos = -1;
+        p.seg_ops.push_back(o);
+    };
+    for (const polar_sc_op &o : ops) {
+        if (o.code == POLAR_OP_END) break;
+        if ((o.code == POLAR_OP_F || o.code == POLAR_OP_G) && o.n >= tw) {
+            if (open) {
+                mark(polar_host::POLAR_OP_SEGEND);
+                open = false;
+            }
+            polar_host::TierStep st;
+            st.grid = 1;
+            st.op = o;
+            p.tier.push_back(st);
+            continue;
+        }
+        if (!open) {
+            polar_host::TierStep st;
+            st.off = (int)p.seg_ops.size();
+            p.tier.push_back(st);
+            if (st.off > 0) mark(polar_host::POLAR_OP_SEGCONT);
+            open = true;
+        }
+        p.seg_ops.push_back(o);
+    }
+    if (!open) {   // the schedule ended on a grid record: an empty last segment writes the output
+        polar_host::TierStep st;
+        st.off = (int)p.seg_ops.size();
+        p.tier.push_back(st);
+        mark(polar_host::POLAR_OP_SEGCONT);
+    }
+    mark(POLAR_OP_END);
+    p.seg_ops.push_back(p.seg_ops.back());   // spare END: the kernel loads record i + 1 early
+    p.tier_words = tw;
+}
+
 // PAR > 16: decode the PAR-word leaf (Spec_PolarDec_{PAR}, library.h:149-172 ->
 // functions.h:766-866) whose LLRs are the node of `words` device words at (level, wpos) as
 // device ops: F, the left half, G (G_extended, flagged exact, when EXTENDED; the operands of
@@ -330,6 +387,11 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool int
         size_t bytes = dops.size() * sizeof(polar_sc_op);
         if (hipMalloc(&st.ops, bytes) != hipSuccess) return -ENOMEM;
         if (hipMemcpy(st.ops, dops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+    }
+    if (!p->tier.empty() && !st.seg_ops) {
+        const size_t bytes = p->seg_ops.size() * sizeof(polar_sc_op);
+        if (hipMalloc(&st.seg_ops, bytes) != hipSuccess) return -ENOMEM;
+        if (hipMemcpy(st.seg_ops, p->seg_ops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
     }
     if (p->gmem) {
         size_t waves = (batch + 7) / 8;
@@ -610,6 +672,17 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     }
     if (p->gmem) window_schedule(*p, dev_sched);
     else if (p->hybrid) p->dev_ops = dev_sched;
+    // grid tier for the upper levels of large hybrid plans: F / G of at least 1024 output
+    // words (nodes of 32768+ LLRs). POLAR_SC_TIER_WORDS overrides (0 = off).
+    if (p->gmem && p->hybrid && p->sub_words > 0) {
+        int tw = p->G >= 4096 ? 1024 : 0;   // N >= 65536: the two or more levels above 16384-LLR nodes
+        if (const char *e = std::getenv("POLAR_SC_TIER_WORDS")) {
+            if (*e) tw = std::atoi(e);
+        }
+        if (tw > LDS_LOW_SLOTS && (uint32_t)tw <= p->G / 2) tier_schedule(*p, tw);
+    }
+    s.tier_steps = (uint32_t)p->tier.size();
+    s.tier_words = (uint32_t)p->tier_words;
     s.kernel = p->jit ? 1u : (p->hybrid ? 2u : 0u);
     s.storage = p->jit ? 2u : (uint32_t)p->gmem;
     s.lds_bytes_per_wave = p->jit ? 8u * (N + 16u) : (uint32_t)p->lds_group_dwords * 4u;
@@ -630,6 +703,7 @@ int polar_sc_plan_destroy(polar_sc_plan *p)
     for (auto &kv : p->dev) {
         if (have_dev) (void)hipSetDevice(kv.first);
         if (kv.second.ops) (void)hipFree(kv.second.ops);
+        if (kv.second.seg_ops) (void)hipFree(kv.second.seg_ops);
         if (kv.second.module) (void)hipModuleUnload(kv.second.module);
         if (kv.second.imodule) (void)hipModuleUnload(kv.second.imodule);
         if (kv.second.module16) (void)hipModuleUnload(kv.second.module16);

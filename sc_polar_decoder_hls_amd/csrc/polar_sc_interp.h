@@ -42,6 +42,9 @@ typedef unsigned short uint16_t;
 typedef signed char int8_t;
 typedef unsigned char uint8_t;
 typedef __SIZE_TYPE__ size_t;
+// LDS words through address-space-3 pointers: ds_read / ds_write, never flat accesses (which
+// also count against vmcnt and wait behind outstanding HBM stores)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 
 enum : int {
@@ -49,7 +52,11 @@ enum : int {
     OP_H = 8, OP_H0 = 9, OP_END = 10,
     OP_WOPEN = 11, OP_WFLUSH = 12,  // HBM-scratch plans: partial-sum window of a 128-word subtree
     OP_SUB = 13,                    // hybrid plans: generated subtree decoder `fb` at node (level, pos)
-    OP_PLEAF = 14                   // PAR > 16: PRUNING_LEVEL 1 leaf decoder (fb kind) of the PAR word at (level, pos)
+    OP_PLEAF = 14,                  // PAR > 16: PRUNING_LEVEL 1 leaf decoder (fb kind) of the PAR word at (level, pos)
+    // grid-tier plans (polar_sc_host.cpp tier_schedule): the schedule runs as segments between
+    // grid-wide F / G launches; a segment ends with OP_SEGEND (no output) or OP_END (the last)
+    // and every segment but the first starts with OP_SEGCONT (the partial sums persist)
+    OP_SEGEND = 15, OP_SEGCONT = 16
 };
 // op.fb fields besides the leaf frozen pattern (bits 0..15) and PR1 leaf kind (16..18)
 constexpr uint32_t FB_EXACT = 1u << 19;   // G / GLEAF inside a PAR-word leaf: G_extended (no clamp)
@@ -90,7 +97,7 @@ template <bool GMEM>
 struct Ctx {
     slot_t *hs;            // HBM scratch (GMEM): slots [0, lds0), 8-bit pairs (128 B rows)
     uint32_t *hbit;        // HBM scratch (GMEM): bit dwords (256 B rows)
-    uint32_t *lb;          // LDS: slots [lds0, nslot) (GMEM) / slots + bit dwords (!GMEM)
+    lds_u32 *lb;           // LDS: slots [lds0, nslot) (GMEM) / slots + bit dwords (!GMEM)
     int lds0;              // first slot held in LDS (0 when !GMEM)
     int wd0;               // GMEM: first bit dword of the open partial-sum window, -1 = none
     uint32_t nslot;        // G - 1
@@ -119,11 +126,15 @@ struct Ctx {
         else sth(slot, v);
     }
     // bit dword d: LDS window (ops inside a windowed subtree), HBM bits, or LDS (!GMEM)
-    __device__ __forceinline__ uint32_t *wl(int d) const { return lb + ((int)nslot - lds0 + d - wd0) * 64; }
+    __device__ __forceinline__ lds_u32 *wl(int d) const { return lb + ((int)nslot - lds0 + d - wd0) * 64; }
     __device__ __forceinline__ uint32_t bld(int d) const
     {
-        if constexpr (GMEM) return wd0 >= 0 ? *wl(d) : hbit[d * 64];
-        else return lb[(nslot + d) * 64];
+        if constexpr (GMEM) {
+            if (wd0 >= 0) return *wl(d);   // wave-uniform branch: a ds_read or a global load
+            return hbit[d * 64];
+        } else {
+            return lb[(nslot + d) * 64];
+        }
     }
     // bit dword of an op that is never windowed (its node is wider than the window): a plain
     // load, not a flat one through a selected pointer (which would also wait for the LDS)
@@ -708,11 +719,12 @@ __device__ __forceinline__ void decode_body(
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int lane = threadIdx.x & 63;
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar loop control
-    const int wi = wib % wpg;                       // wave index in its group
+    const int lw = __builtin_ctz((unsigned)wpg);    // wpg is a power of two
+    const int wi = wib & (wpg - 1);                 // wave index in its group
     // the wave that runs the unsplit ops: rotated over the groups so that the lead waves of
     // the groups sharing a CU do not all sit on the same SIMD
-    const int lead = wpg > 1 ? (int)(blockIdx.x % (unsigned)wpg) : 0;
-    const int gib = wib / wpg;                      // group index in the block
+    const int lead = wpg > 1 ? (int)(blockIdx.x & (unsigned)(wpg - 1)) : 0;
+    const int gib = wib >> lw;                      // group index in the block
     const long group = (long)blockIdx.x * gpb + gib;
     const int G = N >> 4;
     const int row = lane >> 4;
@@ -723,7 +735,7 @@ __device__ __forceinline__ void decode_body(
     c.nslot = (uint32_t)(G - 1);
     c.lds0 = GMEM ? lds0 : 0;
     c.wd0 = -1;
-    c.lb = smem + (size_t)gib * (size_t)lds_dwords + lane;
+    c.lb = (lds_u32 *)smem + (size_t)gib * (size_t)lds_dwords + lane;
     // HBM part of the group: lds0 slots of 64 u16 (SM8 pairs), then the bit dwords
     uint32_t *const gbase = GMEM ? scratch + (size_t)group * (size_t)group_dwords : nullptr;
     c.hs = GMEM ? (slot_t *)gbase + lane : nullptr;
@@ -738,9 +750,11 @@ __device__ __forceinline__ void decode_body(
     // an idle group is a whole block when wpg > 1 (gpb == 1), so no barrier is stranded
     if (group * 8 >= batch) return;
 
-    // clear partial-sum memory (H0 may read words the H0 route never wrote)
+    // clear partial-sum memory (H0 may read words the H0 route never wrote), unless this is a
+    // continuation segment of a grid-tier plan
     const int nbd = (G + 15) >> 4;
-    if (wi == lead)
+    const bool fresh = __builtin_amdgcn_readfirstlane(ops[0].code) != OP_SEGCONT;
+    if (wi == lead && fresh)
         for (int d = 0; d < nbd; d++) c.bst(d, 0u);
 
     const bool tracer = TRACE && group == 0 && wi == lead && lane == 0;
@@ -752,6 +766,7 @@ __device__ __forceinline__ void decode_body(
     Op cur = ops[0];
     for (int oi = 0;; oi++) {
         const int code = __builtin_amdgcn_readfirstlane(cur.code);
+        if (code == OP_SEGEND) return;   // grid-tier segment: the next launch continues
         if (code == OP_END) {
             if (tracer) {
                 trace[2 + oi] = __builtin_readcyclecounter();
@@ -776,9 +791,16 @@ __device__ __forceinline__ void decode_body(
                 // open: clear the window (bits start at 0); flush: copy it to the HBM bits
                 if (wi == lead) {
                     c.wd0 = pos >> 4;
-                    for (int j = 0; j < WIN_DWORDS; j++) {
-                        if (code == OP_WOPEN) *c.wl(c.wd0 + j) = 0u;
-                        else c.hbit[(c.wd0 + j) * 64] = *c.wl(c.wd0 + j);
+                    lds_u32 *const w = c.wl(c.wd0);
+                    if (code == OP_WOPEN) {
+#pragma unroll
+                        for (int j = 0; j < WIN_DWORDS; j++) w[j * 64] = 0u;
+                    } else {
+                        uint32_t t[WIN_DWORDS];   // all LDS reads in flight, then the HBM stores
+#pragma unroll
+                        for (int j = 0; j < WIN_DWORDS; j++) t[j] = w[j * 64];
+#pragma unroll
+                        for (int j = 0; j < WIN_DWORDS; j++) c.hbit[(c.wd0 + j) * 64] = t[j];
                     }
                 }
                 win_d0 = code == OP_WOPEN ? (pos >> 4) : -1;
@@ -788,8 +810,8 @@ __device__ __forceinline__ void decode_body(
         }
         if (!split && wi != lead) continue;
         // this wave's share of a split op (whole op otherwise)
-        const int i0 = split ? (int)(((long)n * wi) / wpg) : 0;
-        const int i1 = split ? (int)(((long)n * (wi + 1)) / wpg) : n;
+        const int i0 = split ? (n * wi) >> lw : 0;
+        const int i1 = split ? (n * (wi + 1)) >> lw : n;
         switch (code) {
         case OP_F: op_fg<false>(c, k, n, -1, i0, i1, fb); break;
         case OP_G: op_fg<true>(c, k, n, upos, i0, i1, fb); break;
@@ -805,7 +827,7 @@ __device__ __forceinline__ void decode_body(
         case OP_SUB:
             // a whole subtree as generated straight-line code (hybrid plans, polar_sc_jit.cpp):
             // its root words are in the level-k stage slot in LDS, its bits go to `pos`
-            polar_sub_call(c, (int)fb, (int)(c.lb - smem) + (c.lvl_off(k) - c.lds0) * 64, pos);
+            polar_sub_call(c, (int)fb, (int)(c.lb - (lds_u32 *)smem) + (c.lvl_off(k) - c.lds0) * 64, pos);
             break;
 #endif
         default: break;
@@ -830,6 +852,51 @@ __device__ __forceinline__ void decode_body(
     for (int w = G + pl; w < out_stride; w += 16) {   // pad words (N = 32 with u64 output)
         if (st_lo) o_lo[w] = 0;
         if (st_hi) o_hi[w] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Grid tier (large N, hybrid plans): one F or G record of an upper-level node for every frame
+// group at once. Wave w of the grid takes words [cw*j, cw*j + cw) of group w / chunks (j =
+// w % chunks), so one group's wide op spans many CUs instead of the 8 waves of its block; the
+// segments of the schedule between these launches run in the hybrid kernel (OP_SEGEND /
+// OP_SEGCONT). Sources and destinations are HBM levels (nodes wider than the LDS region).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void tier_body(const chan_t *__restrict__ llr, uint32_t *__restrict__ scratch, int N,
+                                          int batch, int group_dwords, int lds0, int code, int k, int n, int upos,
+                                          uint32_t fb, int cw)
+{
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    const int chunks = (n + cw - 1) / cw;
+    const long group = wave / chunks;
+    const int j = wave - (int)group * chunks;
+    if (group * 8 >= batch) return;
+    const int G = N >> 4;
+    const int row = lane >> 4;
+    Ctx<true> c;
+    c.G = G;
+    c.nslot = (uint32_t)(G - 1);
+    c.lds0 = lds0;
+    c.wd0 = -1;
+    c.lb = nullptr;
+    uint32_t *const gbase = scratch + (size_t)group * (size_t)group_dwords;
+    c.hs = (slot_t *)gbase + lane;
+    c.hbit = gbase + (size_t)lds0 * (SLOT16 ? 64 : 32) + lane;
+    const long f_lo = group * 8 + row, f_hi = group * 8 + 4 + row;
+    const long f_lo_c = f_lo < batch ? f_lo : (long)batch - 1;
+    const long f_hi_c = f_hi < batch ? f_hi : (long)batch - 1;
+    c.ln.init((uint32_t)(lane & 15));
+    c.llr_lo = llr + (size_t)f_lo_c * (size_t)N + c.ln.pos;
+    c.llr_hi = llr + (size_t)f_hi_c * (size_t)N + c.ln.pos;
+    const int i0 = j * cw, i1 = i0 + cw < n ? i0 + cw : n;
+    const int w = fb_width(fb);
+    if (code == OP_G) {
+        if (k == 0) fg_words<true, true, false, false, false>(c, k, n, upos, i0, i1, w);
+        else fg_words<true, false, false, false, false>(c, k, n, upos, i0, i1, w);
+    } else {
+        if (k == 0) fg_words<false, true, false, false, false>(c, k, n, -1, i0, i1, w);
+        else fg_words<false, false, false, false, false>(c, k, n, -1, i0, i1, w);
     }
 }
 

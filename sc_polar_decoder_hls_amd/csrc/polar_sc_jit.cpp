@@ -376,7 +376,7 @@ struct Gen {
         const char *ctx = gmem ? "Ctx<true>" : "Ctx<false>";
         o << "__device__ __noinline__ void polar_sub_" << id << "(const " << ctx << " &c, int ldo, int pos)\n{\n"
           << "  extern __shared__ __attribute__((aligned(16))) u32 smem[];\n"
-          << "  const u32 *cin_ = smem + ldo;\n"
+          << "  const lds_u32 *cin_ = (const lds_u32 *)smem + ldo;\n"
           << "  const Lanes ln = c.ln;\n"
           << "  u32 bw[" << (words >= 16 ? words / 16 : 1) << "] = {};\n";
         stage_arrays(root_split_needed());
@@ -499,6 +499,11 @@ std::string hybrid_source(const polar_sc_plan &p, bool with_subs = true, bool ch
       << "    int lds_dwords, int lds0, unsigned long long *__restrict__ trace)\n{\n"
       << "  polar::decode_body<" << (gm ? "true" : "false")
       << ", true>(llr, out, ops, scratch, N, batch, out_stride, wpg, gpb, group_dwords, lds_dwords, lds0, trace);\n}\n";
+    if (gm && with_subs)   // grid tier: upper-level F / G over all frame groups (polar_sc_interp.h tier_body)
+        o << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_tier_kernel(\n"
+          << "    const polar::chan_t *__restrict__ llr, unsigned int *__restrict__ scratch, int N, int batch,\n"
+          << "    int group_dwords, int lds0, int code, int k, int n, int upos, unsigned int fb, int cw)\n{\n"
+          << "  polar::tier_body(llr, scratch, N, batch, group_dwords, lds0, code, k, n, upos, fb, cw);\n}\n";
     return o.str();
 }
 
@@ -655,6 +660,8 @@ int jit_load(const polar_sc_plan &p, DevState &st)
         return -EIO;
     if (p.hybrid && hipModuleGetFunction(&st.fn_trace, st.module, "polar_sc_hybrid_trace_kernel") != hipSuccess)
         return -EIO;
+    if (!p.tier.empty() && hipModuleGetFunction(&st.fn_tier, st.module, "polar_sc_tier_kernel") != hipSuccess)
+        return -EIO;
     return 0;
 }
 
@@ -687,9 +694,47 @@ int launch_interp_fn(hipFunction_t fn, const polar_sc_plan &p, const DevState &s
     return e == hipSuccess ? 0 : -EIO;
 }
 
+// Grid-tier plans: one launch per tier step, in schedule order on the caller's stream. Grid
+// steps run the F / G record over all frame groups, TIER_CW words per wave (256-thread
+// blocks); segment steps run the hybrid kernel on the segment's records.
+constexpr int TIER_CW = 64;
+
+int launch_tier(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
+                int out_stride, int wpg, void *stream)
+{
+    const long groups = (batch + 7) / 8;
+    const unsigned lds = (unsigned)p.lds_group_dwords * 4u;
+    void *scratch = st.scratch;
+    int N = (int)p.N, b = (int)batch, gpb = 1, gd = p.hbm_group_dwords, ld = p.lds_group_dwords, l0 = p.lds0;
+    int cw = TIER_CW;
+    unsigned long long *no_trace = nullptr;
+    for (const TierStep &t : p.tier) {
+        hipError_t e;
+        if (t.grid) {
+            int code = t.op.code, k = t.op.level, n = t.op.n, upos = t.op.upos;
+            unsigned fb = t.op.fb;
+            const long waves = groups * (long)((n + cw - 1) / cw);
+            void *args[] = {(void *)&llr, (void *)&scratch, (void *)&N, (void *)&b, (void *)&gd, (void *)&l0,
+                            (void *)&code, (void *)&k, (void *)&n, (void *)&upos, (void *)&fb, (void *)&cw};
+            e = hipModuleLaunchKernel(st.fn_tier, (unsigned)((waves + 3) / 4), 1, 1, 256, 1, 1, 0,
+                                      (hipStream_t)stream, args, nullptr);
+        } else {
+            const void *ops = (const polar_sc_op *)st.seg_ops + t.off;
+            void *args[] = {(void *)&llr, (void *)&out, (void *)&ops, (void *)&scratch, (void *)&N, (void *)&b,
+                            (void *)&out_stride, (void *)&wpg, (void *)&gpb, (void *)&gd, (void *)&ld, (void *)&l0,
+                            (void *)&no_trace};
+            e = hipModuleLaunchKernel(st.fn, (unsigned)groups, 1, 1, (unsigned)(64 * wpg), 1, 1, lds,
+                                      (hipStream_t)stream, args, nullptr);
+        }
+        if (e != hipSuccess) return -EIO;
+    }
+    return 0;
+}
+
 int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
                       int out_stride, int wpg, void *stream, unsigned long long *trace)
 {
+    if (!trace && !p.tier.empty()) return launch_tier(p, st, llr, out, batch, out_stride, wpg, stream);
     return launch_interp_fn(trace ? st.fn_trace : st.fn, p, st, llr, out, batch, out_stride, wpg, stream, trace);
 }
 

@@ -21,6 +21,8 @@ struct DevState {
     hipModule_t module = nullptr; // per-mask kernel
     hipFunction_t fn = nullptr;
     hipFunction_t fn_trace = nullptr;   // hybrid plans: the per-op monitor variant
+    hipFunction_t fn_tier = nullptr;    // grid-tier plans: upper-level F / G over all groups
+    void *seg_ops = nullptr;            // grid-tier plans: the segment schedules
     hipModule_t imodule = nullptr;      // per-mask plans with llr_bits != 6: hipRTC interpreter
     hipFunction_t ifn_trace = nullptr;  //   (per-op monitor only)
     hipModule_t module16 = nullptr;     // interpreter on the int16 channel (polar_sc_decode_i16)
@@ -39,7 +41,17 @@ struct HostBufs {
 
 // device-internal schedule records (never exported): the partial-sum window of HBM-scratch
 // plans, and the generated-subtree call of hybrid plans
-enum { POLAR_OP_WOPEN = 11, POLAR_OP_WFLUSH = 12, POLAR_OP_SUB = 13, POLAR_OP_PLEAF = 14 };
+enum { POLAR_OP_WOPEN = 11, POLAR_OP_WFLUSH = 12, POLAR_OP_SUB = 13, POLAR_OP_PLEAF = 14,
+       POLAR_OP_SEGEND = 15, POLAR_OP_SEGCONT = 16 };
+
+// grid tier of a hybrid HBM-scratch plan: the decode as a sequence of launches -- F / G
+// records of the upper-level nodes over all frame groups at once (grid), and the schedule
+// segments between them (the hybrid kernel, one block per group)
+struct TierStep {
+    int grid = 0;          // 1: grid F / G launch of record `op`; 0: segment at seg_ops[off]
+    polar_sc_op op{};
+    int off = 0;
+};
 // polar_sc_op.fb of G / GLEAF records inside a PAR-word leaf (PAR > 16): G_extended (no
 // clamp); bits 20..23: operand width above LLR_BITS (polar_sc_interp.h)
 constexpr uint32_t FB_EXACT = 1u << 19;
@@ -76,6 +88,11 @@ struct polar_sc_plan {
     int hybrid_waves = 8;            // waves per group cap = launch bound / 64 of the hybrid kernel
     int sub_words = 0;
     std::vector<std::vector<polar_sc_op>> subs;
+    // grid tier (hybrid HBM plans, polar_sc_host.cpp tier_schedule): F / G records with
+    // n >= tier_words output words run as grid-wide launches; empty = single-kernel decode
+    int tier_words = 0;
+    std::vector<polar_host::TierStep> tier;
+    std::vector<polar_sc_op> seg_ops;
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;
     mutable std::mutex host_mu;                             // polar_sc_decode_host staging

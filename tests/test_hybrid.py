@@ -14,8 +14,9 @@ import pytest
 import util
 
 
-def make(pkg, mask, jit="1", sub_words=None):
-    keys = {"POLAR_SC_JIT": jit, "POLAR_SC_SUB_WORDS": None if sub_words is None else str(sub_words)}
+def make(pkg, mask, jit="1", sub_words=None, tier_words=None):
+    keys = {"POLAR_SC_JIT": jit, "POLAR_SC_SUB_WORDS": None if sub_words is None else str(sub_words),
+            "POLAR_SC_TIER_WORDS": None if tier_words is None else str(tier_words)}
     old = {k: os.environ.get(k) for k in keys}
     try:
         for k, v in keys.items():
@@ -50,6 +51,21 @@ def test_hybrid_plan_stats(pkg):
     assert s["kernel"] == 0 and s["n_sub_calls"] == 0
     s = make(pkg, util.mask("frozen_n_8192_k_4096"), sub_words=8).stats
     assert s["kernel"] == 2 and s["sub_words"] == 8 and s["n_sub_calls"] >= s["n_sub_kinds"] > 0
+
+
+def test_grid_tier_plan(pkg):
+    """Grid tier: C3 / C5 plans cut their schedule at the F / G records of >= 1024 words (2 / 4
+    upper levels); POLAR_SC_TIER_WORDS moves the cut (0 = single kernel); plans too small for
+    an HBM level above the LDS region have none."""
+    s = make(pkg, util.mask("frozen_n_65536_k_32768")).stats
+    assert (s["tier_words"], s["tier_steps"]) == (1024, 10)
+    s = make(pkg, util.mask("frozen_n_262144_k_131072")).stats
+    assert s["tier_words"] == 1024 and s["tier_steps"] > 30
+    assert make(pkg, util.mask("frozen_n_65536_k_32768"), tier_words=0).stats["tier_steps"] == 0
+    assert make(pkg, util.mask("frozen_n_65536_k_32768"), tier_words=2048).stats["tier_steps"] == 4
+    assert make(pkg, util.mask("frozen_n_32768_k_29492")).stats["tier_steps"] == 0
+    assert make(pkg, util.mask("frozen_n_32768_k_29492"), tier_words=512).stats["tier_steps"] > 0
+    assert make(pkg, util.mask("frozen_n_65536_k_32768"), jit="0").stats["tier_steps"] == 0
 
 
 def test_hybrid_schedule_export_unchanged(pkg):
@@ -123,5 +139,39 @@ def test_hybrid_equals_interpreter_full_c3(pkg, cuda):
     mask = util.mask("frozen_n_65536_k_32768")
     llr, _ = bench.gen_frames_torch(cuda, mask, 4096, 2.0, 3, cuda.device("cuda"))
     outs = [make(pkg, mask, jit=j).decode(llr) for j in ("1", "0")]
+    cuda.cuda.synchronize()
+    assert cuda.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [13, 64])
+def test_grid_tier_parity_forced(pkg, cuda, oracle_mod, batch):
+    """A grid tier forced onto N = 32768 (F / G of >= 512 words grid-wide, the rest in
+    segments): bit-exact against the oracle, ragged batch included, and equal to the single
+    kernel decode of the same plan shape."""
+    mask = util.mask("frozen_n_32768_k_29492")
+    awgn, _ = util.synth_frames(mask, batch, ebn0_db=3.0, seed=batch)
+    llr = np.clip(awgn.astype(np.int32), -31, 31).astype(np.int8)
+    dec = make(pkg, mask, tier_words=512)
+    assert dec.stats["tier_steps"] > 0
+    t = cuda.from_numpy(llr).cuda()
+    out = dec.decode(t)
+    one = make(pkg, mask, tier_words=0).decode(t)
+    cuda.cuda.synchronize()
+    assert cuda.equal(out, one)
+    np.testing.assert_array_equal(pkg.unpack_bits(out.cpu().numpy(), mask.size), oracle_mod.decode_fsm(mask, llr))
+
+
+@pytest.mark.gpu
+def test_grid_tier_equals_single_kernel_c5(pkg, cuda):
+    """C5 (N = 262144) at its 8-GPU share of 64 frames: the grid-tier decode equals the single
+    hybrid kernel bit for bit (both are checked against the oracle on sampled frames by
+    test_gpu_parity.py::test_parity_c5_mask_sample)."""
+    import bench
+    mask = util.mask("frozen_n_262144_k_131072")
+    llr, _ = bench.gen_frames_torch(cuda, mask, 64, 2.0, 5, cuda.device("cuda"))
+    a = make(pkg, mask)
+    assert a.stats["tier_steps"] > 0
+    outs = [a.decode(llr), make(pkg, mask, tier_words=0).decode(llr)]
     cuda.cuda.synchronize()
     assert cuda.equal(outs[0], outs[1])
