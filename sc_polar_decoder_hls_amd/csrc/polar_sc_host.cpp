@@ -34,7 +34,7 @@ constexpr uint32_t NODE_R0 = 0x00, NODE_R1 = 0x0F, NODE_REP = 0x02, NODE_SPC = 0
 
 // largest per-wave LDS footprint kept on chip; above it stages go to HBM scratch
 constexpr uint32_t LDS_WAVE_LIMIT = 80u * 1024u;   // all-LDS interpreter limit per 8-frame group
-constexpr int LDS_LOW_SLOTS = 256;                  // HBM mode: the levels of nodes <= 128 words stay in LDS (WIN_DWORDS = this / 16)
+constexpr int LDS_LOW_SLOTS = 256;                  // HBM mode: default LDS region W (slots; the levels of nodes <= W / 2 words)
 
 }  // namespace
 
@@ -126,7 +126,7 @@ struct SubCtx {
 // schedule (polar_sc_plan_get_schedule) stays the plain one.
 void window_schedule(polar_sc_plan &p, const std::vector<polar_sc_op> &ops)
 {
-    const int W = LDS_LOW_SLOTS;
+    const int W = p.lds_slots;
     p.dev_ops.clear();
     int cur = -1;
     auto mark = [&](int code, int pos) {
@@ -617,10 +617,24 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     if (p->gmem) {
         // upper levels + bit dwords in HBM scratch; the levels of nodes <= 128 words in LDS,
         // plus an LDS window for the partial sums of the current 128-word subtree
-        p->lds0 = (int)p->G - LDS_LOW_SLOTS;
+        // the LDS region W: 256 slots, 512 from N = 32768 and 1024 from N = 131072 when the
+        // LDS slots hold 8-bit pairs (PAR 16, LLR_BITS <= 8: 78 KB per group = two groups per
+        // CU at W = 512, 150 KB = one at 1024); POLAR_SC_LDS_SLOTS overrides
+        const bool lds8 = c.par == 16 && c.llr_bits <= 8;
+        int W = LDS_LOW_SLOTS;
+        if (lds8 && p->G >= 8192) W = 1024;
+        else if (lds8 && p->G >= 2048) W = 512;
+        if (const char *e = std::getenv("POLAR_SC_LDS_SLOTS")) {
+            const int w = *e ? std::atoi(e) : 0;
+            if ((w == 256 || (lds8 && (w == 512 || w == 1024))) && (uint32_t)w <= p->G / 2) W = w;
+        }
+        p->lds_slots = W;
+        p->lds0 = (int)p->G - W;
         // 8-bit-pair slots (16-bit values for 9-bit LLRs) + bit dwords
         p->hbm_group_dwords = p->lds0 * (c.llr_bits > 8 ? 64 : 32) + (int)nbd * 64;
-        p->lds_group_dwords = ((int)nslot - p->lds0 + LDS_LOW_SLOTS / 16) * 64;
+        // + the partial-sum window + the SPC exchange area (polar_sc_interp.h SPC_XWAVES)
+        const int es = lds8 ? 2 : 4;   // bytes per LDS slot element (polar_sc_interp.h lslot_t)
+        p->lds_group_dwords = ((W - 1) * 64 * es) / 4 + (W / 16 + 3 * 8) * 64;
     } else {
         p->lds0 = 0;
         p->hbm_group_dwords = 0;
@@ -679,7 +693,7 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         if (const char *e = std::getenv("POLAR_SC_TIER_WORDS")) {
             if (*e) tw = std::atoi(e);
         }
-        if (tw > LDS_LOW_SLOTS && (uint32_t)tw <= p->G / 2) tier_schedule(*p, tw);
+        if (tw >= p->lds_slots && (uint32_t)tw <= p->G / 2) tier_schedule(*p, tw);
     }
     s.tier_steps = (uint32_t)p->tier.size();
     s.tier_words = (uint32_t)p->tier_words;

@@ -61,7 +61,12 @@ enum : int {
 // op.fb fields besides the leaf frozen pattern (bits 0..15) and PR1 leaf kind (16..18)
 constexpr uint32_t FB_EXACT = 1u << 19;   // G / GLEAF inside a PAR-word leaf: G_extended (no clamp)
 __device__ __forceinline__ int fb_width(uint32_t fb) { return QB + (int)((fb >> 20) & 15u); }   // operand width
-constexpr int WIN_DWORDS = 16;      // 256 words of partial sums (polar_sc_host.cpp LDS_LOW_SLOTS / 16)
+// HBM-scratch plans keep the levels of the nodes of at most W words (W = G - lds0, the plan's
+// LDS region, polar_sc_host.cpp lds_slots) in LDS, and the partial sums of the current W-word
+// subtree in an LDS window of W / 16 dwords
+constexpr int SPC_XWAVES = 8;       // HBM-scratch plans: an SPC op splits over at most this many waves
+                                    // (their parity / min-key partials meet in an LDS exchange area
+                                    // of 3 x 64 dwords per wave after the window)
 
 struct Op {            // == polar_sc_op (include/polar_sc.h)
     int32_t code, level, n, pos, upos;
@@ -87,6 +92,11 @@ template <bool GMEM> struct GMEM_OF<Ctx<GMEM>> { static constexpr bool value = G
 template <bool B> struct SlotT { typedef uint16_t T; };
 template <> struct SlotT<true> { typedef uint32_t T; };
 typedef SlotT<SLOT16>::T slot_t;
+// LDS stage slots of HBM-scratch plans: the HBM element (8-bit pairs) when the values fit it,
+// i.e. not inside PAR-word leaves (PAR > 16, whose exact G widens the operands)
+constexpr bool LDS8 = !SLOT16 && P16 == 1;
+typedef SlotT<!LDS8>::T lslot_t;
+typedef __attribute__((address_space(3))) lslot_t lds_slot;
 #if POLAR_CHAN16
 typedef short chan_t;          // int16 channel stream (polar_sc_decode_i16)
 #else
@@ -97,7 +107,10 @@ template <bool GMEM>
 struct Ctx {
     slot_t *hs;            // HBM scratch (GMEM): slots [0, lds0), 8-bit pairs (128 B rows)
     uint32_t *hbit;        // HBM scratch (GMEM): bit dwords (256 B rows)
-    lds_u32 *lb;           // LDS: slots [lds0, nslot) (GMEM) / slots + bit dwords (!GMEM)
+    lds_u32 *lb;           // !GMEM: LDS slots + bit dwords (u32 per lane)
+    lds_slot *ls;          // GMEM: LDS slots [lds0, nslot) (lslot_t per lane)
+    lds_u32 *lw;           // GMEM: the partial-sum window (win dwords), then the SPC exchange area
+    int win;               // GMEM: window dwords (W / 16)
     int lds0;              // first slot held in LDS (0 when !GMEM)
     int wd0;               // GMEM: first bit dword of the open partial-sum window, -1 = none
     uint32_t nslot;        // G - 1
@@ -105,13 +118,23 @@ struct Ctx {
     const chan_t *llr_lo, *llr_hi;   // frame rows (lane offset included)
     Lanes ln;
     __device__ __forceinline__ bool in_lds(int slot) const { return !GMEM || slot >= lds0; }
-    __device__ __forceinline__ uint32_t ldl(int slot) const { return lb[(slot - lds0) * 64]; }
+    __device__ __forceinline__ uint32_t ldl(int slot) const
+    {
+        if constexpr (GMEM && LDS8) return slot_unpack(ls[(slot - lds0) * 64]);
+        else if constexpr (GMEM) return ls[(slot - lds0) * 64];
+        else return lb[slot * 64];
+    }
     __device__ __forceinline__ uint32_t ldh(int slot) const
     {
         if constexpr (SLOT16) return hs[slot * 64];
         else return slot_unpack(hs[slot * 64]);
     }
-    __device__ __forceinline__ void stl(int slot, uint32_t v) const { lb[(slot - lds0) * 64] = v; }
+    __device__ __forceinline__ void stl(int slot, uint32_t v) const
+    {
+        if constexpr (GMEM && LDS8) ls[(slot - lds0) * 64] = (lslot_t)slot_pack(v);
+        else if constexpr (GMEM) ls[(slot - lds0) * 64] = v;
+        else lb[slot * 64] = v;
+    }
     __device__ __forceinline__ void sth(int slot, uint32_t v) const
     {
         if constexpr (SLOT16) hs[slot * 64] = v;
@@ -126,7 +149,9 @@ struct Ctx {
         else sth(slot, v);
     }
     // bit dword d: LDS window (ops inside a windowed subtree), HBM bits, or LDS (!GMEM)
-    __device__ __forceinline__ lds_u32 *wl(int d) const { return lb + ((int)nslot - lds0 + d - wd0) * 64; }
+    __device__ __forceinline__ lds_u32 *wl(int d) const { return lw + (d - wd0) * 64; }
+    // GMEM: the SPC exchange area after the window (SPC_XWAVES x 3 dwords per lane)
+    __device__ __forceinline__ lds_u32 *xs() const { return lw + win * 64; }
     __device__ __forceinline__ uint32_t bld(int d) const
     {
         if constexpr (GMEM) {
@@ -163,6 +188,10 @@ struct Ctx {
         return (k == 0) ? chan(i) : ld(lvl_off(k) + i);
     }
 };
+
+// a root word of a generated subtree decoder from its LDS stage slot (8-bit pairs or SM16)
+__device__ __forceinline__ uint32_t ch_load(uint32_t v) { return v; }
+__device__ __forceinline__ uint32_t ch_load(uint16_t v) { return slot_unpack(v); }
 
 #if POLAR_SC_SUBS
 // defined by the generated source of a hybrid plan: subtree decoder `id` reads its root
@@ -220,7 +249,7 @@ __device__ __forceinline__ void fg_words(const C &c, int k, int n, int upos, int
             if (upos >= 0) {
                 // ops wider than the partial-sum window (2n > 16 * WIN_DWORDS words) are never
                 // windowed (polar_sc_host.cpp window_schedule)
-                if (GMEM_OF<C>::value && n > 8 * WIN_DWORDS) {
+                if (GMEM_OF<C>::value && n > 8 * c.win) {
                     u0 = c.bld_nowin((upos + i) >> 4);
                     u1 = c.bld_nowin((upos + i + CH - 1) >> 4);
                 } else {
@@ -497,8 +526,12 @@ __device__ __forceinline__ uint32_t spc_mag(uint32_t lam)
 // minimum-|lambda| position (lexicographic (|l|, PAR word, bitrev(position)) == Min_Mask
 // tournament + strict '<' across PAR words) when the parity of x is odd.
 // [i0, i1): the words of this wave (R1 split in whole 16-word chunks; SPC is never split).
+// xw > 1 (SPC split over xw waves of an HBM-scratch group, wave index xi): every wave
+// reduces its words' parity and min keys, the partials meet in the LDS exchange area, and wave
+// 0 of the split applies the flip (after the barrier, so every wave's decisions are stored).
 template <bool SPC, bool L, class C>
-__device__ __forceinline__ void r1spc_body(const C &c, int s0, int n, int upos, int pos, int i0, int i1)
+__device__ __forceinline__ void r1spc_body(const C &c, int s0, int n, int upos, int pos, int i0, int i1, int xw = 1,
+                                           int xi = 0)
 {
     uint32_t ud = 0, acc = 0, par = 0;
     uint32_t key_lo = 0xFFFFFFFFu, key_hi = 0xFFFFFFFFu;
@@ -541,6 +574,21 @@ __device__ __forceinline__ void r1spc_body(const C &c, int s0, int n, int upos, 
         const uint32_t lk = c.ln.br << (LPAR - 4);
         key_lo = row_min_u32(key_lo | lk);
         key_hi = row_min_u32(key_hi | lk);
+        if constexpr (GMEM_OF<C>::value) {
+            if (xw > 1) {
+                lds_u32 *const x = c.xs();
+                x[(3 * xi) * 64] = par;
+                x[(3 * xi + 1) * 64] = key_lo;
+                x[(3 * xi + 2) * 64] = key_hi;
+                __syncthreads();
+                if (xi != 0) return;
+                for (int w = 1; w < xw; w++) {
+                    par ^= x[(3 * w) * 64];
+                    key_lo = __builtin_elementwise_min(key_lo, (uint32_t)x[(3 * w + 1) * 64]);
+                    key_hi = __builtin_elementwise_min(key_hi, (uint32_t)x[(3 * w + 2) * 64]);
+                }
+            }
+        }
         const uint32_t bm = 15u << (LPAR - 4);
         uint32_t flip_lo = ((par & 0x8000u) && (key_lo & bm) == lk) ? 1u : 0u;
         uint32_t flip_hi = ((par & 0x80000000u) && (key_hi & bm) == lk) ? 1u : 0u;
@@ -556,11 +604,12 @@ __device__ __forceinline__ void r1spc_body(const C &c, int s0, int n, int upos, 
 }
 
 template <bool SPC, class C>
-__device__ __forceinline__ void op_r1spc(const C &c, int k, int n, int upos, int pos, int i0, int i1)
+__device__ __forceinline__ void op_r1spc(const C &c, int k, int n, int upos, int pos, int i0, int i1, int xw = 1,
+                                         int xi = 0)
 {
     const int s0 = c.lvl_off(k);
-    if (c.in_lds(s0)) r1spc_body<SPC, true>(c, s0, n, upos, pos, i0, i1);
-    else r1spc_body<SPC, false>(c, s0, n, upos, pos, i0, i1);
+    if (c.in_lds(s0)) r1spc_body<SPC, true>(c, s0, n, upos, pos, i0, i1, xw, xi);
+    else r1spc_body<SPC, false>(c, s0, n, upos, pos, i0, i1, xw, xi);
 }
 
 // PAR > 16: the PRUNING_LEVEL 1 leaf decoders (R_STATE, my_module.h:566-593; library.h:
@@ -693,7 +742,7 @@ __device__ __forceinline__ void op_h(const C &c, int pos, int n, int j0, int j1)
 // the same barriers.
 //   llr:  [batch][N] int8;   out: [batch][out_stride] uint16 (bit_mem_1 words, END order)
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ bool op_split(int code, int n, int wpg)
+__device__ __forceinline__ bool op_split(int code, int n, int wpg, bool gmem)
 {
     if (wpg <= 1) return false;
     switch (code) {
@@ -702,6 +751,7 @@ __device__ __forceinline__ bool op_split(int code, int n, int wpg)
     case OP_H:
     case OP_H0:
     case OP_R1: return n >= 16 * wpg;
+    case OP_SPC: return gmem && n >= 16 * (wpg < SPC_XWAVES ? wpg : SPC_XWAVES);   // whole dwords per wave
     default: return false;
     }
 }
@@ -735,7 +785,12 @@ __device__ __forceinline__ void decode_body(
     c.nslot = (uint32_t)(G - 1);
     c.lds0 = GMEM ? lds0 : 0;
     c.wd0 = -1;
-    c.lb = (lds_u32 *)smem + (size_t)gib * (size_t)lds_dwords + lane;
+    lds_u32 *const gl = (lds_u32 *)smem + (size_t)gib * (size_t)lds_dwords;
+    c.lb = gl + lane;
+    // GMEM: W - 1 slots of lslot_t per lane, then the window and the SPC exchange area (dwords)
+    c.win = (G - c.lds0) >> 4;
+    c.ls = (lds_slot *)gl + lane;
+    c.lw = gl + (size_t)(G - 1 - c.lds0) * (size_t)(64 * sizeof(lslot_t) / 4) + lane;
     // HBM part of the group: lds0 slots of 64 u16 (SM8 pairs), then the bit dwords
     uint32_t *const gbase = GMEM ? scratch + (size_t)group * (size_t)group_dwords : nullptr;
     c.hs = GMEM ? (slot_t *)gbase + lane : nullptr;
@@ -782,7 +837,7 @@ __device__ __forceinline__ void decode_body(
         const uint32_t fb = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur.fb);
         const int flag = __builtin_amdgcn_readfirstlane(cur.r0);
         cur = nxt;
-        const bool split = op_split(code, n, wpg);
+        const bool split = op_split(code, n, wpg, GMEM);
         if (wpg > 1 && (split || prev_split)) __syncthreads();
         if (tracer) trace[2 + oi] = __builtin_readcyclecounter();
         prev_split = split;
@@ -794,13 +849,15 @@ __device__ __forceinline__ void decode_body(
                     lds_u32 *const w = c.wl(c.wd0);
                     if (code == OP_WOPEN) {
 #pragma unroll
-                        for (int j = 0; j < WIN_DWORDS; j++) w[j * 64] = 0u;
+                        for (int j = 0; j < c.win; j++) w[j * 64] = 0u;
                     } else {
-                        uint32_t t[WIN_DWORDS];   // all LDS reads in flight, then the HBM stores
+                        for (int j0 = 0; j0 < c.win; j0 += 16) {
+                            uint32_t t[16];   // 16 LDS reads in flight, then the HBM stores
 #pragma unroll
-                        for (int j = 0; j < WIN_DWORDS; j++) t[j] = w[j * 64];
+                            for (int j = 0; j < 16; j++) t[j] = w[(j0 + j) * 64];
 #pragma unroll
-                        for (int j = 0; j < WIN_DWORDS; j++) c.hbit[(c.wd0 + j) * 64] = t[j];
+                            for (int j = 0; j < 16; j++) c.hbit[(c.wd0 + j0 + j) * 64] = t[j];
+                        }
                     }
                 }
                 win_d0 = code == OP_WOPEN ? (pos >> 4) : -1;
@@ -819,7 +876,17 @@ __device__ __forceinline__ void decode_body(
         case OP_GLEAF: op_leaf<true>(c, k, pos, upos, fb); break;
         case OP_REP: op_rep(c, k, n, pos); break;
         case OP_R1: op_r1spc<false>(c, k, n, upos, pos, i0, i1); break;
-        case OP_SPC: op_r1spc<true>(c, k, n, upos, pos, 0, n); break;
+        case OP_SPC:
+            if (split) {
+                // at most SPC_XWAVES waves (0 .. xw-1 counted from the lead) take n / xw words each
+                const int xw = wpg < SPC_XWAVES ? wpg : SPC_XWAVES;
+                const int xi = (wi - lead) & (wpg - 1);
+                if (xi < xw) op_r1spc<true>(c, k, n, upos, pos, (n / xw) * xi, (n / xw) * (xi + 1), xw, xi);
+                else __syncthreads();   // the exchange barrier of the split
+            } else {
+                op_r1spc<true>(c, k, n, upos, pos, 0, n);
+            }
+            break;
         case OP_H: op_h<false>(c, pos, n, i0 >> 4, i1 >> 4); break;
         case OP_H0: op_h<true>(c, pos, n, i0 >> 4, i1 >> 4); break;
         case OP_PLEAF: op_pleaf(c, k, pos, (fb >> 16) & 7u); break;
@@ -827,7 +894,11 @@ __device__ __forceinline__ void decode_body(
         case OP_SUB:
             // a whole subtree as generated straight-line code (hybrid plans, polar_sc_jit.cpp):
             // its root words are in the level-k stage slot in LDS, its bits go to `pos`
-            polar_sub_call(c, (int)fb, (int)(c.lb - (lds_u32 *)smem) + (c.lvl_off(k) - c.lds0) * 64, pos);
+            // (in lslot_t units for GMEM plans, dwords otherwise)
+            if constexpr (GMEM)
+                polar_sub_call(c, (int)fb, (int)(c.ls - (lds_slot *)smem) + (c.lvl_off(k) - c.lds0) * 64, pos);
+            else
+                polar_sub_call(c, (int)fb, (int)(c.lb - (lds_u32 *)smem) + c.lvl_off(k) * 64, pos);
             break;
 #endif
         default: break;
@@ -880,6 +951,9 @@ __device__ __forceinline__ void tier_body(const chan_t *__restrict__ llr, uint32
     c.lds0 = lds0;
     c.wd0 = -1;
     c.lb = nullptr;
+    c.ls = nullptr;
+    c.lw = nullptr;
+    c.win = (G - lds0) >> 4;
     uint32_t *const gbase = scratch + (size_t)group * (size_t)group_dwords;
     c.hs = (slot_t *)gbase + lane;
     c.hbit = gbase + (size_t)lds0 * (SLOT16 ? 64 : 32) + lane;

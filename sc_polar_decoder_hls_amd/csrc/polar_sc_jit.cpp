@@ -27,6 +27,17 @@
 #include <sstream>
 
 namespace {
+// per-mask kernels: POLAR_SC_MASK_MIN_WAVES (2..8) adds a minimum-waves-per-SIMD launch bound
+// (the register allocator then targets that occupancy, spilling if it must)
+std::string mask_min_waves()
+{
+    const char *e = std::getenv("POLAR_SC_MASK_MIN_WAVES");
+    const int w = (e && *e) ? std::atoi(e) : 0;
+    return (w >= 2 && w <= 8) ? ", " + std::to_string(w) : std::string();
+}
+}  // namespace
+
+namespace {
 #include "polar_sc_device_src.inc"   // kPolarDeviceSrc: polar_sc_device.h as a string
 #include "polar_sc_interp_src.inc"   // kPolarInterpSrc: polar_sc_interp.h as a string
 }
@@ -44,6 +55,11 @@ struct Gen {
     // per-mask kernels: the channel words are split once (root_presplit) into m<LG> / s<LG>,
     // so the root ops run on split words like every other level
     bool presplit = false;
+    // per-mask kernels: the root words are dropped after the root F-type op and split again
+    // from the LDS-staged channel for the root G-type op (fewer live registers across the
+    // left half: higher occupancy for about 3 VALU more per root word)
+    bool resplit = false;
+    bool root_f_done = false;
     Gen(const std::vector<polar_sc_op> &ops_, int lg) : ops(ops_), LG(lg) {}
 
     // Partial sums: u32 bw[max(1, G / 16)], dword j = groups 16 j .. 16 j + 15, low frame in
@@ -118,7 +134,7 @@ struct Gen {
     // registers held across the whole left subtree.
     void clobber_parent(int sd, int n)
     {
-        if (sd == LG && !presplit) return;   // root: channel words are re-read from LDS
+        if (sd == LG && (!presplit || resplit)) return;   // root: channel words are re-read from LDS
         for (int i = 0; i < 2 * n; i++) o << "  asm volatile(\"\" : \"+v\"(" << M(sd, i) << "));\n";
         for (int k = 0; k < planes(2 * n); k++) o << "  asm volatile(\"\" : \"+v\"(s" << sd << "[" << k << "]));\n";
     }
@@ -181,6 +197,12 @@ struct Gen {
         const int sd = LG - op.level, cd = sd - 1, n = op.n, np = planes(n);
         const bool root = sd == LG && !presplit;
         fence();
+        if (resplit && sd == LG) {
+            const bool gtype = op.code == POLAR_OP_G || op.code == POLAR_OP_GLEAF || op.code == POLAR_OP_R1 ||
+                               op.code == POLAR_OP_SPC;
+            if (gtype && root_f_done) root_presplit(2 * n);
+            if (!gtype) root_f_done = true;
+        }
         if (root && (op.code == POLAR_OP_REP || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC)) root_split(2 * n);
         switch (op.code) {
         case POLAR_OP_F:
@@ -376,7 +398,8 @@ struct Gen {
         const char *ctx = gmem ? "Ctx<true>" : "Ctx<false>";
         o << "__device__ __noinline__ void polar_sub_" << id << "(const " << ctx << " &c, int ldo, int pos)\n{\n"
           << "  extern __shared__ __attribute__((aligned(16))) u32 smem[];\n"
-          << "  const lds_u32 *cin_ = (const lds_u32 *)smem + ldo;\n"
+          << (gmem ? "  const lds_slot *cin_ = (const lds_slot *)smem + ldo;\n"
+                   : "  const lds_u32 *cin_ = (const lds_u32 *)smem + ldo;\n")
           << "  const Lanes ln = c.ln;\n"
           << "  u32 bw[" << (words >= 16 ? words / 16 : 1) << "] = {};\n";
         stage_arrays(root_split_needed());
@@ -403,7 +426,7 @@ struct Gen {
         const int FS = N + 16, chunks = N / 2;   // 16-byte chunks per wave
         o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
           << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
-          << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_mask_kernel(\n"
+          << "extern \"C\" __global__ void __launch_bounds__(256" << mask_min_waves() << ") polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
           << "  __shared__ uint4 stage_[4 * 8 * " << FS / 16 << "];\n"
           << "  __shared__ unsigned char tabm_[256], tabs_[256];   // channel byte -> |LLR|, sign (qconv_format)\n"
@@ -437,6 +460,10 @@ struct Gen {
           << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
         stage_arrays(true);
         presplit = true;
+        {
+            const char *e = std::getenv("POLAR_SC_ROOT_RESPLIT");
+            resplit = e && e[0] == '1';
+        }
         root_presplit(G);
         all_ops();
         // END (my_module.h:1848-1869) + wrapper_out: x^ words in natural order
@@ -471,7 +498,7 @@ std::string hybrid_source(const polar_sc_plan &p, bool with_subs = true, bool ch
       << (p.cfg.extended ? 1 : 0) << "\n#define POLAR_LPAR " << 4 + lpar << "\n#define POLAR_CHAN16 " << (chan16 ? 1 : 0)
       << "\n#include \"polar_sc_interp.h\"\n";
     if (with_subs) {
-        o << "namespace polar {\n#define CH(w) cin_[(w) * 64]\n";
+        o << "namespace polar {\n#define CH(w) ch_load(cin_[(w) * 64])\n";
         int lg = 0;
         while ((1 << lg) < p.sub_words) lg++;
         for (size_t id = 0; id < p.subs.size(); id++) {

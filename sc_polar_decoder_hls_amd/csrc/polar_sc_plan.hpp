@@ -80,6 +80,7 @@ struct polar_sc_plan {
     // interpreter storage of one 8-frame group (dwords): HBM scratch part, LDS part, and the
     // first stage slot held in LDS (polar_sc_kernels.hip, Ctx)
     int hbm_group_dwords = 0, lds_group_dwords = 0, lds0 = 0;
+    int lds_slots = 256;             // HBM-scratch plans: LDS region W (slots [G - W, G - 1))
     int jit = 0;                     // 1: decode with the per-mask kernel
     // hybrid plans (N > 1024): the device schedule stops at every mixed node of sub_words
     // words with a POLAR_OP_SUB record; subs[id] is that subtree's own schedule (levels and
