@@ -164,22 +164,20 @@ void window_schedule(polar_sc_plan &p, const std::vector<polar_sc_op> &ops)
 // by the END record) and opened by POLAR_OP_SEGCONT after the first. The H / H0 records of
 // the cut nodes stay in the segments, in schedule order, so every launch sees the partial
 // sums of the launches before it (kernel boundaries order the HBM traffic).
-void tier_schedule(polar_sc_plan &p, int tw)
+polar_host::TierPlan tier_schedule(const polar_sc_plan &p, int tw)
 {
-    p.tier.clear();
-    p.seg_ops.clear();
-    p.tier_words = 0;
+    polar_host::TierPlan t;
     const std::vector<polar_sc_op> &ops = p.dev_ops;
     bool any = false;
     for (const polar_sc_op &o : ops)
         if ((o.code == POLAR_OP_F || o.code == POLAR_OP_G) && o.n >= tw) any = true;
-    if (!any) return;
+    if (!any) return t;
     bool open = false;
     auto mark = [&](int code) {
         polar_sc_op o{};
         o.code = code;
         o.upos = -1;
-        p.seg_ops.push_back(o);
+        t.seg_ops.push_back(o);
     };
     for (const polar_sc_op &o : ops) {
         if (o.code == POLAR_OP_END) break;
@@ -191,27 +189,28 @@ void tier_schedule(polar_sc_plan &p, int tw)
             polar_host::TierStep st;
             st.grid = 1;
             st.op = o;
-            p.tier.push_back(st);
+            t.steps.push_back(st);
             continue;
         }
         if (!open) {
             polar_host::TierStep st;
-            st.off = (int)p.seg_ops.size();
-            p.tier.push_back(st);
+            st.off = (int)t.seg_ops.size();
+            t.steps.push_back(st);
             if (st.off > 0) mark(polar_host::POLAR_OP_SEGCONT);
             open = true;
         }
-        p.seg_ops.push_back(o);
+        t.seg_ops.push_back(o);
     }
     if (!open) {   // the schedule ended on a grid record: an empty last segment writes the output
         polar_host::TierStep st;
-        st.off = (int)p.seg_ops.size();
-        p.tier.push_back(st);
+        st.off = (int)t.seg_ops.size();
+        t.steps.push_back(st);
         mark(polar_host::POLAR_OP_SEGCONT);
     }
     mark(POLAR_OP_END);
-    p.seg_ops.push_back(p.seg_ops.back());   // spare END: the kernel loads record i + 1 early
-    p.tier_words = tw;
+    t.seg_ops.push_back(t.seg_ops.back());   // spare END: the kernel loads record i + 1 early
+    t.tw = tw;
+    return t;
 }
 
 // PAR > 16: decode the PAR-word leaf (Spec_PolarDec_{PAR}, library.h:149-172 ->
@@ -388,10 +387,12 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool int
         if (hipMalloc(&st.ops, bytes) != hipSuccess) return -ENOMEM;
         if (hipMemcpy(st.ops, dops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
     }
-    if (!p->tier.empty() && !st.seg_ops) {
-        const size_t bytes = p->seg_ops.size() * sizeof(polar_sc_op);
-        if (hipMalloc(&st.seg_ops, bytes) != hipSuccess) return -ENOMEM;
-        if (hipMemcpy(st.seg_ops, p->seg_ops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+    for (size_t t = 0; t < p->tiers.size() && t < 2; t++) {
+        if (st.seg_ops[t]) continue;
+        const size_t bytes = p->tiers[t].seg_ops.size() * sizeof(polar_sc_op);
+        if (hipMalloc(&st.seg_ops[t], bytes) != hipSuccess) return -ENOMEM;
+        if (hipMemcpy(st.seg_ops[t], p->tiers[t].seg_ops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
+            return -EIO;
     }
     if (p->gmem) {
         size_t waves = (batch + 7) / 8;
@@ -686,17 +687,26 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     }
     if (p->gmem) window_schedule(*p, dev_sched);
     else if (p->hybrid) p->dev_ops = dev_sched;
-    // grid tier for the upper levels of large hybrid plans: F / G of at least 1024 output
-    // words (nodes of 32768+ LLRs). POLAR_SC_TIER_WORDS overrides (0 = off).
+    // grid tier for the upper levels of large hybrid plans (N >= 65536): the deep cut at F / G
+    // records of >= 1024 output words (nodes of 32768+ LLRs), and the root alone. Measured on
+    // one box: C5 (64 groups) 4.68 ms deep vs 4.90 root-only; C3 (512 groups, every CU busy
+    // either way) 1.53 ms root-only vs 1.59 deep. POLAR_SC_TIER_WORDS fixes one cut (0 = off).
     if (p->gmem && p->hybrid && p->sub_words > 0) {
-        int tw = p->G >= 4096 ? 1024 : 0;   // N >= 65536: the two or more levels above 16384-LLR nodes
-        if (const char *e = std::getenv("POLAR_SC_TIER_WORDS")) {
-            if (*e) tw = std::atoi(e);
+        std::vector<int> cuts;
+        if (const char *e = std::getenv("POLAR_SC_TIER_WORDS"); e && *e) {
+            cuts.push_back(std::atoi(e));
+        } else if (p->G >= 4096) {
+            cuts.push_back(1024);
+            if ((int)p->G / 2 != 1024) cuts.push_back((int)p->G / 2);
         }
-        if (tw >= p->lds_slots && (uint32_t)tw <= p->G / 2) tier_schedule(*p, tw);
+        for (int tw : cuts) {
+            if (tw < p->lds_slots || (uint32_t)tw > p->G / 2) continue;
+            polar_host::TierPlan t = tier_schedule(*p, tw);
+            if (!t.steps.empty()) p->tiers.push_back(std::move(t));
+        }
     }
-    s.tier_steps = (uint32_t)p->tier.size();
-    s.tier_words = (uint32_t)p->tier_words;
+    s.tier_steps = p->tiers.empty() ? 0u : (uint32_t)p->tiers[0].steps.size();
+    s.tier_words = p->tiers.empty() ? 0u : (uint32_t)p->tiers[0].tw;
     s.kernel = p->jit ? 1u : (p->hybrid ? 2u : 0u);
     s.storage = p->jit ? 2u : (uint32_t)p->gmem;
     s.lds_bytes_per_wave = p->jit ? 8u * (N + 16u) : (uint32_t)p->lds_group_dwords * 4u;
@@ -717,7 +727,8 @@ int polar_sc_plan_destroy(polar_sc_plan *p)
     for (auto &kv : p->dev) {
         if (have_dev) (void)hipSetDevice(kv.first);
         if (kv.second.ops) (void)hipFree(kv.second.ops);
-        if (kv.second.seg_ops) (void)hipFree(kv.second.seg_ops);
+        for (void *so : kv.second.seg_ops)
+            if (so) (void)hipFree(so);
         if (kv.second.module) (void)hipModuleUnload(kv.second.module);
         if (kv.second.imodule) (void)hipModuleUnload(kv.second.imodule);
         if (kv.second.module16) (void)hipModuleUnload(kv.second.module16);

@@ -687,7 +687,7 @@ int jit_load(const polar_sc_plan &p, DevState &st)
         return -EIO;
     if (p.hybrid && hipModuleGetFunction(&st.fn_trace, st.module, "polar_sc_hybrid_trace_kernel") != hipSuccess)
         return -EIO;
-    if (!p.tier.empty() && hipModuleGetFunction(&st.fn_tier, st.module, "polar_sc_tier_kernel") != hipSuccess)
+    if (!p.tiers.empty() && hipModuleGetFunction(&st.fn_tier, st.module, "polar_sc_tier_kernel") != hipSuccess)
         return -EIO;
     return 0;
 }
@@ -735,7 +735,12 @@ int launch_tier(const polar_sc_plan &p, const DevState &st, const int8_t *llr, u
     int N = (int)p.N, b = (int)batch, gpb = 1, gd = p.hbm_group_dwords, ld = p.lds_group_dwords, l0 = p.lds0;
     int cw = TIER_CW;
     unsigned long long *no_trace = nullptr;
-    for (const TierStep &t : p.tier) {
+    // batches with at least one frame group per CU keep every CU busy inside the hybrid
+    // kernel: they take the root-only cut (tiers[1]) when the plan has one
+    const long cus = st.simds > 0 ? st.simds / 4 : 256;
+    const size_t ti = (p.tiers.size() > 1 && groups >= cus) ? 1 : 0;
+    const TierPlan &tp = p.tiers[ti];
+    for (const TierStep &t : tp.steps) {
         hipError_t e;
         if (t.grid) {
             int code = t.op.code, k = t.op.level, n = t.op.n, upos = t.op.upos;
@@ -746,7 +751,7 @@ int launch_tier(const polar_sc_plan &p, const DevState &st, const int8_t *llr, u
             e = hipModuleLaunchKernel(st.fn_tier, (unsigned)((waves + 3) / 4), 1, 1, 256, 1, 1, 0,
                                       (hipStream_t)stream, args, nullptr);
         } else {
-            const void *ops = (const polar_sc_op *)st.seg_ops + t.off;
+            const void *ops = (const polar_sc_op *)st.seg_ops[ti] + t.off;
             void *args[] = {(void *)&llr, (void *)&out, (void *)&ops, (void *)&scratch, (void *)&N, (void *)&b,
                             (void *)&out_stride, (void *)&wpg, (void *)&gpb, (void *)&gd, (void *)&ld, (void *)&l0,
                             (void *)&no_trace};
@@ -761,7 +766,7 @@ int launch_tier(const polar_sc_plan &p, const DevState &st, const int8_t *llr, u
 int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
                       int out_stride, int wpg, void *stream, unsigned long long *trace)
 {
-    if (!trace && !p.tier.empty()) return launch_tier(p, st, llr, out, batch, out_stride, wpg, stream);
+    if (!trace && !p.tiers.empty()) return launch_tier(p, st, llr, out, batch, out_stride, wpg, stream);
     return launch_interp_fn(trace ? st.fn_trace : st.fn, p, st, llr, out, batch, out_stride, wpg, stream, trace);
 }
 

@@ -22,7 +22,7 @@ struct DevState {
     hipFunction_t fn = nullptr;
     hipFunction_t fn_trace = nullptr;   // hybrid plans: the per-op monitor variant
     hipFunction_t fn_tier = nullptr;    // grid-tier plans: upper-level F / G over all groups
-    void *seg_ops = nullptr;            // grid-tier plans: the segment schedules
+    void *seg_ops[2] = {nullptr, nullptr};   // grid-tier plans: the segment schedules per tier plan
     hipModule_t imodule = nullptr;      // per-mask plans with llr_bits != 6: hipRTC interpreter
     hipFunction_t ifn_trace = nullptr;  //   (per-op monitor only)
     hipModule_t module16 = nullptr;     // interpreter on the int16 channel (polar_sc_decode_i16)
@@ -51,6 +51,11 @@ struct TierStep {
     int grid = 0;          // 1: grid F / G launch of record `op`; 0: segment at seg_ops[off]
     polar_sc_op op{};
     int off = 0;
+};
+struct TierPlan {
+    int tw = 0;                        // F / G records of >= tw output words run grid-wide
+    std::vector<TierStep> steps;
+    std::vector<polar_sc_op> seg_ops;  // the segment schedules, concatenated
 };
 // polar_sc_op.fb of G / GLEAF records inside a PAR-word leaf (PAR > 16): G_extended (no
 // clamp); bits 20..23: operand width above LLR_BITS (polar_sc_interp.h)
@@ -89,11 +94,11 @@ struct polar_sc_plan {
     int hybrid_waves = 8;            // waves per group cap = launch bound / 64 of the hybrid kernel
     int sub_words = 0;
     std::vector<std::vector<polar_sc_op>> subs;
-    // grid tier (hybrid HBM plans, polar_sc_host.cpp tier_schedule): F / G records with
-    // n >= tier_words output words run as grid-wide launches; empty = single-kernel decode
-    int tier_words = 0;
-    std::vector<polar_host::TierStep> tier;
-    std::vector<polar_sc_op> seg_ops;
+    // grid tier (hybrid HBM plans, polar_sc_host.cpp tier_schedule): F / G records of at
+    // least tw output words run as grid-wide launches. tiers[0]: the deep cut; tiers[1]
+    // (when it differs): the root only, taken by batches with a frame group per CU or more
+    // (polar_sc_jit.cpp launch_tier). Empty: single-kernel decode.
+    std::vector<polar_host::TierPlan> tiers;
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;
     mutable std::mutex host_mu;                             // polar_sc_decode_host staging

@@ -63,6 +63,8 @@ def test_grid_tier_plan(pkg):
     assert s["tier_words"] == 1024 and s["tier_steps"] > 30
     assert make(pkg, util.mask("frozen_n_65536_k_32768"), tier_words=0).stats["tier_steps"] == 0
     assert make(pkg, util.mask("frozen_n_65536_k_32768"), tier_words=2048).stats["tier_steps"] == 4
+    # (batches with a frame group per CU take the root-only cut at launch: polar_sc_jit.cpp
+    # launch_tier; test_hybrid_equals_interpreter_full_c3 runs it at 512 groups)
     assert make(pkg, util.mask("frozen_n_32768_k_29492")).stats["tier_steps"] == 0
     assert make(pkg, util.mask("frozen_n_32768_k_29492"), tier_words=512).stats["tier_steps"] > 0
     assert make(pkg, util.mask("frozen_n_65536_k_32768"), jit="0").stats["tier_steps"] == 0
