@@ -41,11 +41,15 @@ TRAFFIC_PROFILES = {
 # (MI355X_MICROARCH.md) that would hold one C2 batch (67 MB).
 ROTATE_BYTES = 300 << 20
 EBN0_SWEEP = (1.0, 2.5, 4.0)   # throughput depends weakly on the SNR
-# VALU issue cost on gfx950 measured by tools/valu_microbench.hip (profiles/
-# r01_valu_microbench.log): 4.2-4.7 cycles per wave64 instruction for the packed-16 / logic /
-# DPP classes the decoder issues (8 waves per SIMD, independent chains)
-VALU_CYCLES_PER_INST = 4.4
-NOMINAL_CLOCK_GHZ = 2.4
+# VALU issue cost on gfx950, timed in-kernel with the shader clock (s_memtime) by
+# tools/valu_microbench.hip (profiles/r02_valu_microbench.log): SIMD cycles per wave64
+# instruction of the packed-16 / DPP / v_perm classes the decoder issues, by waves per SIMD
+# (independent chains). 8 waves: 2.62 (32-bit ALU 1.45); 4: 3.25; 2: 4.45; 1: 5.20. The
+# roofline peak is the full-occupancy figure; the per-mask kernel runs at 3 waves per SIMD
+# (158 VGPRs), whose ceiling lies between the 2- and 4-wave figures.
+VALU_CYCLES_PER_INST = 2.62
+VALU_CYCLES_BY_WAVES = {1: 5.20, 2: 4.45, 4: 3.25, 8: 2.62}
+NOMINAL_CLOCK_GHZ = 2.4   # fallback when the PMC profile has no measured clock
 
 CONFIGS = {
     # name: (mask fixture, per-GPU frames at N=1 semantics, description)
@@ -387,12 +391,15 @@ def main():
                 simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
                 waves = (per_gpu + 7) // 8
                 rate = waves * prof["valu_insts_per_wave"] / (kern_ms * 1e-3)
-                peak = simds * NOMINAL_CLOCK_GHZ * 1e9 / VALU_CYCLES_PER_INST
+                ghz = prof.get("effective_clock_ghz") or NOMINAL_CLOCK_GHZ
+                peak = simds * ghz * 1e9 / VALU_CYCLES_PER_INST
                 valu = {"insts_per_wave": prof["valu_insts_per_wave"], "waves_per_launch": waves,
                         "achieved": rate, "peak": peak, "unit": "wave-instructions/s", "frac": rate / peak,
-                        "peak_basis": "%d SIMDs x %.1f GHz / %.1f cycles per wave64 VALU instruction "
-                                      "(profiles/r01_valu_microbench.log)" % (simds, NOMINAL_CLOCK_GHZ,
-                                                                             VALU_CYCLES_PER_INST),
+                        "peak_basis": "%d SIMDs x %.2f GHz (PMC clock) / %.2f SIMD cycles per wave64 packed-16 "
+                                      "VALU instruction at 8 waves/SIMD (profiles/r02_valu_microbench.log)"
+                                      % (simds, ghz, VALU_CYCLES_PER_INST),
+                        "peak_at_3_waves_per_simd": simds * ghz * 1e9 / (0.5 * (VALU_CYCLES_BY_WAVES[2]
+                                                                                + VALU_CYCLES_BY_WAVES[4])),
                         "source": os.path.relpath(prof_path, ROOT)}
         res = {
             "metric": "decoded info bits/sec + frames/sec, N=1024 K=512 batch, 1/2/4/8 MI355X",

@@ -3,7 +3,11 @@
 counter, kernel duration from the trace, and derived figures (issue rate, wait shares,
 effective clock, HBM bytes per launch with the gfx950 FETCH_SIZE correction).
 
-usage: tools/pmc_summary.py gpurun_out/prof_<tag> [--kernel REGEX] [--json out.json]
+usage: tools/pmc_summary.py gpurun_out/prof_<tag> [--kernel REGEX] [--json out.json] [--reps R]
+
+--reps R: the driver ran R decodes of a multi-launch plan (grid tier: grid F / G launches +
+segment launches per decode); counters and kernel time are then totals per decode (all
+matching dispatches / R) instead of per-dispatch averages.
 """
 import argparse
 import csv
@@ -14,7 +18,7 @@ import re
 from collections import defaultdict
 
 
-def load_counters(d, kre):
+def load_counters(d, kre, reps=0):
     per = defaultdict(lambda: defaultdict(float))   # counter -> dispatch -> value (sum over instances)
     for f in glob.glob(os.path.join(d, "*", "*_counter_collection.csv")):
         with open(f) as fh:
@@ -22,6 +26,8 @@ def load_counters(d, kre):
                 if not kre.search(r["Kernel_Name"]):
                     continue
                 per[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
+    if reps > 0:
+        return {k: sum(v.values()) / reps for k, v in per.items() if v}
     return {k: sum(v.values()) / len(v) for k, v in per.items() if v}
 
 
@@ -41,12 +47,19 @@ def main():
     ap.add_argument("--kernel", default="polar_sc")
     ap.add_argument("--json")
     ap.add_argument("--skip-first", type=int, default=1, help="trace dispatches to drop (warm-up)")
+    ap.add_argument("--reps", type=int, default=0, help="decodes per run of a multi-launch plan")
     a = ap.parse_args()
     kre = re.compile(a.kernel)
-    c = load_counters(a.dir, kre)
+    c = load_counters(a.dir, kre, a.reps)
     durs = load_trace(a.dir, kre)
-    d = durs[a.skip_first:] if len(durs) > a.skip_first else durs
+    if a.reps > 0 and durs:
+        durs = [sum(durs) / a.reps]   # kernel time per decode (all its launches)
+        d = durs
+    else:
+        d = durs[a.skip_first:] if len(durs) > a.skip_first else durs
     res = {"kernel_regex": a.kernel, "dispatches": len(durs), "counters": c}
+    if a.reps > 0:
+        res["per_decode_of_reps"] = a.reps
     if d:
         res["kernel_s_mean"] = sum(d) / len(d)
         res["kernel_s_min"] = min(d)
