@@ -411,6 +411,10 @@ __device__ __forceinline__ u32 leaf_ms(u32 M, u32 S, const Lanes &ln)
     }
 }
 
+// packed root magnitudes of the per-mask kernels: the low / high byte of each 16-bit half
+__device__ __forceinline__ u32 rlo(u32 p) { return p & 0x00FF00FFu; }
+__device__ __forceinline__ u32 rhi(u32 p) { return __builtin_amdgcn_perm(p, p, 0x0C030C01u); }
+
 // SM16 pair with magnitudes <= 31 -> two SM8 bytes (low frame in bits 0..7, high frame in
 // bits 8..15); inverse of sm8_pair
 __device__ __forceinline__ u32 sm16_to_sm8x2(u32 v)

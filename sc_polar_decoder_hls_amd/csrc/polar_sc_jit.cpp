@@ -59,6 +59,11 @@ struct Gen {
     // from the LDS-staged channel for the root G-type op (fewer live registers across the
     // left half: higher occupancy for about 3 VALU more per root word)
     bool resplit = false;
+    // per-mask kernels: the root magnitudes packed two words per register (bytes of word j
+    // and j + G/2 in each 16-bit half): half the root registers for 2 VALU more per root
+    // F / G word. C2: 158 -> 126 VGPRs, 3 -> 4 waves per SIMD, 76.7 -> 72.7 / 75.5 us on one
+    // box (POLAR_SC_ROOT_PACK=0 restores the unpacked root)
+    bool pack = false;
     bool root_f_done = false;
     Gen(const std::vector<polar_sc_op> &ops_, int lg) : ops(ops_), LG(lg) {}
 
@@ -108,10 +113,19 @@ struct Gen {
     // Stage words below the root are split (polar_sc_device.h): m<d>[i] magnitudes and
     // s<d>[k] sign planes of words 16k..16k+15. The root reads SM16 channel words CH(i).
     static int planes(int words) { return words >= 16 ? words / 16 : 1; }
-    static std::string M(int sd, int i)
+    std::string M(int sd, int i) const
     {
         std::ostringstream s;
-        s << "m" << sd << "[" << i << "]";
+        if (pack && sd == LG) {
+            // packed root: pr[j] holds words j (low bytes) and j + G/2 (high bytes)
+            const int h = 1 << (LG - 1);
+            // (opaque: the compiler would otherwise rebuild the unpacked words from the
+            // presplit and keep all of them live, 180 VGPRs instead of 126)
+            if (i < h) s << "rlo(opaque(pr[" << i << "]))";
+            else s << "rhi(opaque(pr[" << i - h << "]))";
+        } else {
+            s << "m" << sd << "[" << i << "]";
+        }
         return s.str();
     }
     // sign plane of depth sd shifted so that word i is at bit 0 (bits past the op's words are
@@ -135,7 +149,11 @@ struct Gen {
     void clobber_parent(int sd, int n)
     {
         if (sd == LG && (!presplit || resplit)) return;   // root: channel words are re-read from LDS
-        for (int i = 0; i < 2 * n; i++) o << "  asm volatile(\"\" : \"+v\"(" << M(sd, i) << "));\n";
+        if (pack && sd == LG) {
+            for (int i = 0; i < n; i++) o << "  asm volatile(\"\" : \"+v\"(pr[" << i << "]));\n";
+        } else {
+            for (int i = 0; i < 2 * n; i++) o << "  asm volatile(\"\" : \"+v\"(" << M(sd, i) << "));\n";
+        }
         for (int k = 0; k < planes(2 * n); k++) o << "  asm volatile(\"\" : \"+v\"(s" << sd << "[" << k << "]));\n";
     }
 
@@ -183,6 +201,20 @@ struct Gen {
     void root_presplit(int words)
     {
         for (int k = 0; k < planes(words); k++) o << "  s" << LG << "[" << k << "] = 0u;\n";
+        if (pack) {
+            const int h = words / 2;
+            for (int i = 0; i < h; i++) {
+                const int j = i + h;
+                o << "  { const u32 a0_ = chl[" << 16 * i << "], a1_ = chh[" << 16 * i << "], b0_ = chl[" << 16 * j
+                  << "], b1_ = chh[" << 16 * j << "];\n"
+                  << "    pr[" << i << "] = (u32)tabm_[a0_] | ((u32)tabm_[b0_] << 8) | ((u32)tabm_[a1_] << 16) | ((u32)tabm_[b1_] << 24);\n"
+                  << "    s" << LG << "[" << i / 16 << "] |= ((u32)tabs_[a0_] | ((u32)tabs_[a1_] << 16)) << " << i % 16 << ";\n"
+                  << "    s" << LG << "[" << j / 16 << "] |= ((u32)tabs_[b0_] | ((u32)tabs_[b1_] << 16)) << " << j % 16
+                  << "; }\n";
+                chunk_fence(i, h);
+            }
+            return;
+        }
         for (int i = 0; i < words; i++) {
             o << "  { const u32 bl_ = chl[" << 16 * i << "], bh_ = chh[" << 16 * i << "];\n"
               << "    " << M(LG, i) << " = (u32)tabm_[bl_] | ((u32)tabm_[bh_] << 16);\n"
@@ -379,7 +411,8 @@ struct Gen {
     {
         for (int d = 1; d < LG; d++)
             o << "  u32 m" << d << "[" << (1 << d) << "], s" << d << "[" << planes(1 << d) << "];\n";
-        if (with_root) o << "  u32 m" << LG << "[" << (1 << LG) << "], s" << LG << "[" << planes(1 << LG) << "];\n";
+        if (with_root && pack) o << "  u32 pr[" << (1 << (LG - 1)) << "], s" << LG << "[" << planes(1 << LG) << "];\n";
+        else if (with_root) o << "  u32 m" << LG << "[" << (1 << LG) << "], s" << LG << "[" << planes(1 << LG) << "];\n";
     }
     void all_ops()
     {
@@ -458,12 +491,14 @@ struct Gen {
           << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
           << " + ln.pos;\n"
           << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
-        stage_arrays(true);
         presplit = true;
         {
             const char *e = std::getenv("POLAR_SC_ROOT_RESPLIT");
             resplit = e && e[0] == '1';
+            const char *pe = std::getenv("POLAR_SC_ROOT_PACK");
+            pack = !resplit && G >= 2 && !(pe && pe[0] == '0');
         }
+        stage_arrays(true);
         root_presplit(G);
         all_ops();
         // END (my_module.h:1848-1869) + wrapper_out: x^ words in natural order
