@@ -24,8 +24,9 @@ constexpr u32 MAG = 0x7FFF7FFFu;   // magnitudes of both halves
 //   POLAR_CA2   1: two's complement datapath (config.h:11 CA2, functions.h:48-118), values
 //               are i16 per half; 0: SIGMAG (SM16: bit 15 sign, bits 0..14 magnitude)
 //   POLAR_EXT   EXTENDED (config.h:14): exact leaves (1) or saturating G inside leaves (0)
-//   POLAR_LPAR  log2 PAR (polar_parameters.h:8), 4..6 on the device: a PAR word is P16
-//               consecutive 16-LLR device words
+//   POLAR_LPAR  log2 PAR (polar_parameters.h:8), 2..6 on the device: a PAR word is P16
+//               consecutive 16-LLR device words (PAR >= 16), or PPW PAR words share one
+//               device word (PAR 4 / 8: a sub-row of 4 / 8 lanes)
 //   POLAR_CHAN16  channel stream of int16 LLRs instead of int8
 #ifndef POLAR_Q
 #define POLAR_Q 6
@@ -43,12 +44,13 @@ constexpr u32 MAG = 0x7FFF7FFFu;   // magnitudes of both halves
 #define POLAR_CHAN16 0
 #endif
 static_assert(POLAR_Q >= 5 && POLAR_Q <= 9, "LLR_BITS 5..9");
-static_assert(POLAR_LPAR >= 4 && POLAR_LPAR <= 6, "PAR 16..64 on the device");
+static_assert(POLAR_LPAR >= 2 && POLAR_LPAR <= 6, "PAR 4..64 on the device");
 constexpr int QB = POLAR_Q;
 constexpr bool CA2 = POLAR_CA2 != 0;
 constexpr bool EXT = POLAR_EXT != 0;
 constexpr int LPAR = POLAR_LPAR;
-constexpr int P16 = 1 << (LPAR - 4);            // device words per PAR word
+constexpr int P16 = LPAR >= 4 ? 1 << (LPAR - 4) : 1;   // device words per PAR word
+constexpr int PPW = LPAR < 4 ? 16 >> LPAR : 1;          // PAR words per device word
 constexpr bool SLOT16 = QB > 8;                 // HBM stage slots hold 16-bit values
 constexpr u32 QMAG = (1u << (QB - 1)) - 1u;     // channel / F magnitude bound (31 at 6 bits)
 // G clamp: SIGMAG qsat_sm<Q-1> (15 at Q 6, functions.h:186-194), CA2 qsat<Q> (31, :63-75)

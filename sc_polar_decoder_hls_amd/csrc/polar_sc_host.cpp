@@ -257,6 +257,31 @@ void leaf_ops(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int level, 
     else par_expand(p, out, level + 1, wpos, P, p.fbp[g], 0);
 }
 
+// PAR 4 / 8: the group classes of device word w for the device's word tree
+// (polar_sc_interp.h word_node): per group g of the word, bits 7g..7g+3 = class, 7g+4..7g+6 =
+// PR1 leaf kind; bit 28 = PRUNING_LEVEL 2
+uint32_t word_info(const polar_sc_plan &p, uint32_t w)
+{
+    uint32_t info = p.cfg.pruning_level == 2 ? 1u << 28 : 0u;
+    for (uint32_t j = 0; j < p.ppw; j++) {
+        const uint32_t g = w * p.ppw + j;
+        info |= (p.type[g] & 15u) << (7 * j);
+        info |= (leaf_kind(p, g) & 7u) << (7 * j + 4);
+    }
+    return info;
+}
+uint32_t word_fb(const polar_sc_plan &p, uint32_t w)
+{
+    uint32_t fb = 0;
+    for (uint32_t k = 0; k < 16; k++) fb |= (uint32_t)p.mask[16 * w + k] << k;
+    return fb;
+}
+void emit_word(std::vector<polar_sc_op> &out, const polar_sc_plan &p, int code, int level, uint32_t w, int upos)
+{
+    emit(out, code, level, 1, (int)w, upos, word_fb(p, w));
+    out.back().reserved[1] = (int32_t)word_info(p, w);
+}
+
 // Decode the children of the node at device `level` covering PAR groups [g0, g0+cnt)
 // (cnt >= 2) whose LLR words are in stage buffer `level`. Mirrors the
 // F/G/R/H/H0/F_REP/G_R1/G_SPC transitions of my_module::do_action:
@@ -294,6 +319,40 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
         return;
     }
     const uint32_t h = cnt / 2;
+    if (p.ppw > 1) {
+        // PAR 4 / 8: nodes of two or more device words as usual; a child of one word is an
+        // FLEAF / GLEAF record whose device side decodes the whole word (its PAR words, their
+        // pruning and leaves: polar_sc_interp.h word_node)
+        const uint32_t Q = p.ppw;
+        const int hw = (int)(h / Q), w0 = (int)(g0 / Q), w1 = (int)((g0 + h) / Q);
+        const bool prune = p.cfg.pruning_level == 2;
+        const uint32_t tl = (is_root || !prune) ? NODE_RN : node_class(p, g0, h);
+        const uint32_t tr = (is_root || !prune) ? NODE_RN : node_class(p, g0 + h, h);
+        bool left_zero = false;
+        if (tl == NODE_R0) {
+            left_zero = true;
+        } else if (tl == NODE_REP) {
+            emit(out, POLAR_OP_REP, level, hw, w0, -1, 0);
+        } else if (h == Q) {
+            emit_word(out, p, POLAR_OP_FLEAF, level, (uint32_t)w0, -1);
+        } else {
+            emit(out, POLAR_OP_F, level, hw, w0, -1, 0);
+            compile_node(p, out, level + 1, g0, h, false, sc);
+        }
+        const int upos = left_zero ? -1 : w0;
+        if (tr == NODE_R1) {
+            emit(out, POLAR_OP_R1, level, hw, w1, upos, 0);
+        } else if (tr == NODE_SPC) {
+            emit(out, POLAR_OP_SPC, level, hw, w1, upos, 0);
+        } else if (h == Q) {
+            emit_word(out, p, POLAR_OP_GLEAF, level, (uint32_t)w1, upos);
+        } else {
+            emit(out, POLAR_OP_G, level, hw, w1, upos, 0);
+            compile_node(p, out, level + 1, g0 + h, h, false, sc);
+        }
+        emit(out, left_zero ? POLAR_OP_H0 : POLAR_OP_H, level, hw, w0, -1, 0);
+        return;
+    }
     const int P = (int)p.p16, hw = (int)h * P, w0 = (int)g0 * P, w1 = (int)(g0 + h) * P;
     // node pruning only at PRUNING_LEVEL 2 (my_module.h:478-531, 623-652, 815-868, 965-993);
     // REP2 / SPC2 classes fall through to the plain F / G transitions there
@@ -329,12 +388,14 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
 // SPC2/H0 switches (script/script_tests.sh:103-122), LLR_BITS 5..9 (QUANT 6..9,
 // script/parser.sh:12, parser_comp.sh:12; 9-bit LLRs beyond the int8 range need the int16
 // channel of polar_sc_decode_i16), SIGMAG or CA2 (parser.sh:15,43), EXTENDED 0/1
-// (config.h:14) and PAR 16 / 32 / 64 (script_tests.sh:11,124 runs 16 and 64). ELAG_RARE = 1
-// does not compile in the reference (my_module.h:255 vs :1511); PAR below 16 is not built.
+// (config.h:14) and PAR 4 / 8 / 16 / 32 / 64 (script_tests.sh:11,124 runs 16 and 64,
+// script_RTL_sim.sh:97-330 PAR 4..64). ELAG_RARE = 1 does not compile in the reference
+// (my_module.h:255 vs :1511).
 bool config_supported(const polar_sc_config &c)
 {
     auto sw = [](int32_t v) { return v == 0 || v == 1; };
-    return c.llr_bits >= 5 && c.llr_bits <= 9 && (c.par == 16 || c.par == 32 || c.par == 64) && sw(c.sigmag) &&
+    return c.llr_bits >= 5 && c.llr_bits <= 9 &&
+           (c.par == 4 || c.par == 8 || c.par == 16 || c.par == 32 || c.par == 64) && sw(c.sigmag) &&
            sw(c.extended) && c.pruning_level >= 0 && c.pruning_level <= 2 && sw(c.elag_r1) && sw(c.elag_rep) &&
            sw(c.elag_spc) && sw(c.elag_rep2) && sw(c.elag_spc2) && c.elag_rare == 0 && sw(c.elag_h0) &&
            sw(c.strict_llr);
@@ -534,7 +595,7 @@ const char *polar_sc_strerror(int err)
     case 0: return "success";
     case -EINVAL: return "invalid argument";
     case -ENOMEM: return "out of memory";
-    case -ENOTSUP: return "configuration not supported (PAR other than 16/32/64, LLR_BITS outside 5..9, ELAG_RARE, "
+    case -ENOTSUP: return "configuration not supported (PAR other than 4/8/16/32/64, LLR_BITS outside 5..9, ELAG_RARE, "
                           "or a switch outside 0/1; see polar_sc_config in include/polar_sc.h)";
     case -ENOENT: return "file not found";
     case -EIO: return "HIP runtime error";
@@ -578,7 +639,8 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     p->N = N;
     p->G = N / 16;
     p->GP = N / (uint32_t)c.par;
-    p->p16 = (uint32_t)c.par / 16;
+    p->p16 = c.par >= 16 ? (uint32_t)c.par / 16 : 1u;
+    p->ppw = c.par < 16 ? 16u / (uint32_t)c.par : 1u;
     p->cfg = c;
     p->mask.resize(N);
     p->fbp.resize(p->GP);
@@ -621,7 +683,7 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         // the LDS region W: 256 slots, 512 from N = 32768 and 1024 from N = 131072 when the
         // LDS slots hold 8-bit pairs (PAR 16, LLR_BITS <= 8: 78 KB per group = two groups per
         // CU at W = 512, 150 KB = one at 1024); POLAR_SC_LDS_SLOTS overrides
-        const bool lds8 = c.par == 16 && c.llr_bits <= 8;
+        const bool lds8 = c.par <= 16 && c.llr_bits <= 8;
         int W = LDS_LOW_SLOTS;
         if (lds8 && p->G >= 8192) W = 1024;
         else if (lds8 && p->G >= 2048) W = 512;

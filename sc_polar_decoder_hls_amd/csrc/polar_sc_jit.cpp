@@ -526,11 +526,11 @@ std::string hybrid_source(const polar_sc_plan &p, bool with_subs = true, bool ch
     std::ostringstream o;
     const bool gm = p.gmem != 0;
     const int waves = with_subs ? p.hybrid_waves : HYBRID_MAX_WAVES;
-    int lpar = 0;
-    while ((16 << lpar) < p.cfg.par) lpar++;
+    int lpar = 0;   // log2 PAR
+    while ((1 << lpar) < p.cfg.par) lpar++;
     o << "#define POLAR_LANE_REMAP 1\n#define POLAR_SC_SUBS " << (with_subs ? 1 : 0) << "\n#define POLAR_Q "
       << p.cfg.llr_bits << "\n#define POLAR_CA2 " << (p.cfg.sigmag ? 0 : 1) << "\n#define POLAR_EXT "
-      << (p.cfg.extended ? 1 : 0) << "\n#define POLAR_LPAR " << 4 + lpar << "\n#define POLAR_CHAN16 " << (chan16 ? 1 : 0)
+      << (p.cfg.extended ? 1 : 0) << "\n#define POLAR_LPAR " << lpar << "\n#define POLAR_CHAN16 " << (chan16 ? 1 : 0)
       << "\n#include \"polar_sc_interp.h\"\n";
     if (with_subs) {
         o << "namespace polar {\n#define CH(w) ch_load(cin_[(w) * 64])\n";

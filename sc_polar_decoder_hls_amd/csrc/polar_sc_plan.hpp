@@ -72,7 +72,8 @@ constexpr int HYBRID_MAX_WAVES = 8;
 
 struct polar_sc_plan {
     uint32_t N = 0, G = 0, K = 0;    // G: 16-LLR device words (N / 16)
-    uint32_t GP = 0, p16 = 1;        // PAR groups (N / PAR), device words per group
+    uint32_t GP = 0, p16 = 1;        // PAR groups (N / PAR), device words per group (PAR >= 16)
+    uint32_t ppw = 1;                // PAR groups per device word (PAR 4 / 8: 4 / 2)
     int lg = 0;                      // log2(N/16)
     polar_sc_config cfg{};
     std::vector<uint8_t> mask;       // N, 1 = information

@@ -1,4 +1,4 @@
-"""GPU parity across the reference's swept datapath formats: PAR 16 / 32 / 64
+"""GPU parity across the reference's swept datapath formats: PAR 4 / 8 / 16 / 32 / 64
 (polar_parameters.h:8; script_tests.sh:11,124 sweeps 16 and 64), CA2 vs SIGMAG (config.h:11;
 script/parser.sh:15,43), EXTENDED 0/1 (config.h:14) and LLR_BITS up to 9 (parser_comp.sh:12;
 int16 channel). Every format runs the schedule interpreter compiled by hipRTC with its
@@ -18,6 +18,8 @@ FORMATS = [
     (16, 0, 1, 6), (16, 0, 1, 8), (16, 0, 0, 6), (16, 1, 0, 6), (16, 1, 1, 9), (16, 0, 1, 9),
     (32, 1, 1, 6), (32, 0, 1, 6), (64, 1, 1, 6), (64, 1, 1, 8), (64, 0, 1, 6), (64, 1, 0, 6), (64, 0, 0, 8),
     (64, 1, 1, 9),
+    # PAR 4 / 8 (script_RTL_sim.sh:97-330): PAR words as lane groups of a device word
+    (8, 1, 1, 6), (8, 0, 1, 6), (8, 1, 0, 8), (4, 1, 1, 6), (4, 0, 0, 8), (4, 1, 1, 9),
 ]
 CONFIGS = ((2, 1, 1, 1, 0, 0, 1), (1, 1, 1, 1, 1, 1, 0), (0, 0, 0, 0, 0, 0, 0), (2, 1, 1, 1, 1, 1, 0))
 

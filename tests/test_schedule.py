@@ -154,7 +154,7 @@ def test_sweep_configs_change_results(pkg, oracle_mod):
 
 def test_unsupported_configs(pkg):
     mask = util.mask("FB_N128_K64")
-    for field, val in (("elag_rare", 1), ("llr_bits", 10), ("llr_bits", 4), ("par", 8), ("par", 128), ("par", 48),
+    for field, val in (("elag_rare", 1), ("llr_bits", 10), ("llr_bits", 4), ("par", 2), ("par", 128), ("par", 48),
                        ("sigmag", 2), ("extended", 2), ("pruning_level", 3)):
         c = pkg.default_config()
         setattr(c, field, val)
@@ -165,7 +165,8 @@ def test_unsupported_configs(pkg):
     c.par = 64
     with pytest.raises(pkg.PolarError):
         pkg.Decoder(np.ones(64, np.uint8), config=c)
-    for field, val in (("llr_bits", 9), ("par", 64), ("par", 32), ("sigmag", 0), ("extended", 0)):
+    for field, val in (("llr_bits", 9), ("par", 64), ("par", 32), ("par", 8), ("par", 4), ("sigmag", 0),
+                       ("extended", 0)):
         c = pkg.default_config()
         setattr(c, field, val)
         dec = pkg.Decoder(mask, config=c)
