@@ -42,11 +42,10 @@ extern "C" {
  *   * sigmag 1 (SIGMAG) or 0 (CA2, the two's complement datapath of functions.h:48-118)
  *     (script/parser.sh:15,43);
  *   * extended 1/0 (config.h:14: exact or saturating leaves);
- *   * par 16, 32 or 64 (script_tests.sh:11 runs 16 and 64).
+ *   * par 4, 8, 16, 32 or 64 (script_tests.sh:11 runs 16 and 64, script_RTL_sim.sh 4..64).
  * The shipped datapath (sigmag 1, par 16, extended 1, llr_bits <= 8) runs the specialised
  * kernels; every other format runs the schedule interpreter compiled for it. elag_rare = 1
- * (does not compile in the reference, my_module.h:255 vs :1511) and par below 16 are rejected
- * with -ENOTSUP.
+ * (does not compile in the reference, my_module.h:255 vs :1511) is rejected with -ENOTSUP.
  */
 typedef struct polar_sc_config {
     int32_t llr_bits;       /* LLR_BITS            (config.h:2)      default 6  */
@@ -86,8 +85,11 @@ typedef struct polar_sc_op {
                        leaf decoder (POLAR_LEAF_*; non-plain only at pruning_level 1).
                        PAR > 16 leaves (expanded into F / G / FLEAF / GLEAF / H records):
                        bit 19 = G_extended (no clamp), bits 20..23 = operand width above
-                       llr_bits */
-    int32_t reserved[2];
+                       llr_bits. PAR 4 / 8: FLEAF / GLEAF decode the whole 16-LLR word
+                       (its PAR words); bits 0..15 its frozen pattern */
+    int32_t reserved[2];   /* [1], PAR 4 / 8 leaf records: per PAR word g of the word, bits
+                              7g..7g+3 its do_prunning class, 7g+4..7g+6 its PR1 leaf
+                              decoder; bit 28 = PRUNING_LEVEL 2 */
 } polar_sc_op;
 
 enum {

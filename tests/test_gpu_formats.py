@@ -19,7 +19,8 @@ FORMATS = [
     (32, 1, 1, 6), (32, 0, 1, 6), (64, 1, 1, 6), (64, 1, 1, 8), (64, 0, 1, 6), (64, 1, 0, 6), (64, 0, 0, 8),
     (64, 1, 1, 9),
     # PAR 4 / 8 (script_RTL_sim.sh:97-330): PAR words as lane groups of a device word
-    (8, 1, 1, 6), (8, 0, 1, 6), (8, 1, 0, 8), (4, 1, 1, 6), (4, 0, 0, 8), (4, 1, 1, 9),
+    (8, 1, 1, 6), (8, 0, 1, 6), (8, 1, 0, 8), (8, 1, 1, 8), (4, 1, 1, 6), (4, 0, 0, 8), (4, 1, 1, 8),
+    (4, 1, 1, 9),
 ]
 CONFIGS = ((2, 1, 1, 1, 0, 0, 1), (1, 1, 1, 1, 1, 1, 0), (0, 0, 0, 0, 0, 0, 0), (2, 1, 1, 1, 1, 1, 0))
 
@@ -106,10 +107,11 @@ def _sweep_cfg(pkg, c7, par):
     return c
 
 
-@pytest.mark.parametrize("par", [16, 64])
+@pytest.mark.parametrize("par", [16, 64, 8, 4])
 def test_script_tests_pruning_sweep(pkg, cuda, oracle_mod, par, monkeypatch):
     """script/script_tests.sh:103-213 as the reference runs it: the 11 pruning configurations
-    on frozen_n_32768_k_29492 (its lines 105-106) at QUANT 8, for PAR 16 and 64 (line 124).
+    on frozen_n_32768_k_29492 (its lines 105-106) at QUANT 8, for PAR 16 and 64 (line 124),
+    and the same sweep at PAR 8 and 4 (the PAR values of script_RTL_sim.sh).
     PAR 16 plans run on the schedule interpreter here (POLAR_SC_JIT=0, one code object for
     the format); the generated-subtree kernels are swept in test_gpu_configs.py."""
     monkeypatch.setenv("POLAR_SC_JIT", "0")
