@@ -705,7 +705,7 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     }
     while ((1u << p->lg) < p->G) p->lg++;
     // per-mask register kernel for N <= 1024; above, the hybrid kernel (interpreter + generated
-    // subtree decoders of POLAR_SC_SUB_WORDS words, default 64 = 1024 LLRs). POLAR_SC_JIT=0
+    // subtree decoders of POLAR_SC_SUB_WORDS words, default 64 / 128). POLAR_SC_JIT=0
     // selects the plain schedule interpreter for every N.
     const char *jit_env = std::getenv("POLAR_SC_JIT");
     const bool jit_on = !(jit_env && jit_env[0] == '0');
@@ -715,11 +715,16 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         if ((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && (o.fb >> 16)) kinds = true;
     const bool dflt = default_format(c);
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
-    int sub_words = 64;
+    // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR
+    // level's F / G / H then run inside the straight-line code instead of as interpreter ops
+    // (one box, same-box A/B: C5 4.68 -> 3.76 ms, C5 64-frame share 4.18 -> 3.13, C3 1.54 ->
+    // 1.48; 248 VGPRs, no spills, at most 2 waves per SIMD -- below N = 32768 the smaller
+    // subtrees keep 3)
+    int sub_words = p->G >= 2048 ? 128 : 64;
     if (const char *e = std::getenv("POLAR_SC_SUB_WORDS")) {
         if (*e) sub_words = std::atoi(e);
     }
-    const bool sub_ok = sub_words >= 2 && sub_words <= 64 && (sub_words & (sub_words - 1)) == 0;
+    const bool sub_ok = sub_words >= 2 && sub_words <= 128 && (sub_words & (sub_words - 1)) == 0;
     std::vector<polar_sc_op> dev_sched;
     if (!p->jit && jit_on && !kinds && dflt && sub_ok && (uint32_t)sub_words < p->G) {
         SubCtx sc;

@@ -43,6 +43,9 @@ def structured_mask(rng, N):
 
 def test_hybrid_plan_stats(pkg):
     s = make(pkg, util.mask("frozen_n_65536_k_32768")).stats
+    # N >= 32768: 128-word (2048-LLR) subtrees
+    assert (s["kernel"], s["sub_words"], s["n_sub_kinds"], s["n_sub_calls"]) == (2, 128, 27, 27)
+    s = make(pkg, util.mask("frozen_n_65536_k_32768"), sub_words=64).stats
     assert (s["kernel"], s["sub_words"], s["n_sub_kinds"], s["n_sub_calls"]) == (2, 64, 43, 47)
     assert s["storage"] == 1
     s = make(pkg, util.mask("FB_N1024_K512")).stats
