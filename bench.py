@@ -47,8 +47,8 @@ EBN0_SWEEP = (1.0, 2.5, 4.0)   # throughput depends weakly on the
 # tools/valu_microbench.hip (profiles/r02_valu_microbench.log): SIMD cycles per wave64
 # instruction of the packed-16 / DPP / v_perm classes the decoder issues, by waves per SIMD
 # (independent chains). 8 waves: 2.62 (32-bit ALU 1.45); 4: 3.25; 2: 4.45; 1: 5.20. The
-# roofline peak is the full-occupancy figure; the per-mask kernel runs at 3 waves per SIMD
-# (158 VGPRs), whose ceiling lies between the 2- and 4-wave figures.
+# roofline peak is the full-occupancy figure; the per-mask kernel runs at 4 waves per SIMD
+# (126 VGPRs with the packed root, 33 KB of LDS per 4-wave block).
 VALU_CYCLES_PER_INST = 2.62
 VALU_CYCLES_BY_WAVES = {1: 5.20, 2: 4.45, 4: 3.25, 8: 2.62}
 NOMINAL_CLOCK_GHZ = 2.4   # fallback when the PMC profile has no measured clock
@@ -405,8 +405,8 @@ def main():
                         "peak_basis": "%d SIMDs x %.2f GHz (PMC clock) / %.2f SIMD cycles per wave64 packed-16 "
                                       "VALU instruction at 8 waves/SIMD (profiles/r02_valu_microbench.log)"
                                       % (simds, ghz, VALU_CYCLES_PER_INST),
-                        "peak_at_3_waves_per_simd": simds * ghz * 1e9 / (0.5 * (VALU_CYCLES_BY_WAVES[2]
-                                                                                + VALU_CYCLES_BY_WAVES[4])),
+                        # the per-mask kernel's occupancy (126 VGPRs, 33 KB LDS per 4-wave block)
+                        "peak_at_4_waves_per_simd": simds * ghz * 1e9 / VALU_CYCLES_BY_WAVES[4],
                         "source": os.path.relpath(prof_path, ROOT)}
         res = {
             "metric": "decoded info bits/sec + frames/sec, N=1024 K=512 batch, 1/2/4/8 MI355X",
