@@ -27,13 +27,24 @@
 #include <sstream>
 
 namespace {
-// per-mask kernels: POLAR_SC_MASK_MIN_WAVES (2..8) adds a minimum-waves-per-SIMD launch bound
-// (the register allocator then targets that occupancy, spilling if it must)
+// per-mask kernels: minimum waves per SIMD of the launch bound (the register allocator then
+// targets that occupancy, spilling if it must). Default 4: the persistent batch loop needs
+// ~132 VGPRs at C2 unbounded, and the scheduler then relaxes to 151 (3 waves per SIMD);
+// bounded at 4 it keeps 128 VGPRs with one dword spilled per batch. POLAR_SC_MASK_MIN_WAVES
+// (2..8) overrides, 0 removes the bound.
 std::string mask_min_waves()
 {
     const char *e = std::getenv("POLAR_SC_MASK_MIN_WAVES");
-    const int w = (e && *e) ? std::atoi(e) : 0;
+    const int w = (e && *e) ? std::atoi(e) : 4;
     return (w >= 2 && w <= 8) ? ", " + std::to_string(w) : std::string();
+}
+// per-mask kernels: POLAR_SC_MASK_PERSIST=R (>= 1) builds the persistent batch loop and caps
+// the grid at R x the resident blocks; 0 / unset: one 8-frame batch per wave, no loop
+int mask_persist()
+{
+    const char *e = std::getenv("POLAR_SC_MASK_PERSIST");
+    const int r = (e && *e) ? std::atoi(e) : 0;
+    return r > 0 ? r : 0;
 }
 }  // namespace
 
@@ -456,9 +467,33 @@ struct Gen {
         // (position 16 w + pl of frames row / row + 4) from there once, into the split root
         // words (root_presplit). Frame stride N + 16 bytes keeps the four rows of a read in
         // different banks.
-        const int FS = N + 16, chunks = N / 2;   // 16-byte chunks per wave
+        //
+        // Persistent waves (jit_launch caps the grid at the blocks that fit on the device at
+        // once): each wave loops over 8-frame batches wave, wave + stride, ... The channel of
+        // the next batch is fetched HBM -> LDS by global_load_lds_dwordx4 (no VGPRs) as soon
+        // as the presplit has read the current one, so its latency hides behind the decode
+        // instead of stalling every wave of the next dispatch round at once.
+        const int FS = N + 16, LPF = N / 16;   // LDS frame stride, 16-byte chunks (lanes) per frame
+        presplit = true;
+        {
+            const char *e = std::getenv("POLAR_SC_ROOT_RESPLIT");
+            resplit = e && e[0] == '1';
+            const char *pe = std::getenv("POLAR_SC_ROOT_PACK");
+            pack = !resplit && G >= 2 && !(pe && pe[0] == '0');
+        }
+        // Prefetch in the middle of the decode only where a frame fills all 64 lanes of a load
+        // (N = 1024): shorter frames load under a lane mask, and that branch in the middle of
+        // the straight-line code costs ~40 VGPRs and spills (N = 512); they fetch at the top of
+        // each iteration instead. The resplit variant re-reads the channel, so it fetches at the end.
+        // Off by default (mask_persist): one batch per wave measured faster than the persistent
+        // loop with prefetch (C2 same box: 74.0 vs 79.5 us, tools/gpu_ab_persist.sh), and the
+        // loop alone costs ~10 VGPRs.
+        const bool persist = mask_persist();
+        const bool prefetch = persist && !resplit && LPF >= 64;
         o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
           << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
+          << "typedef const __attribute__((address_space(1))) void *gas_t;\n"
+          << "typedef __attribute__((address_space(3))) void *las_t;\n"
           << "extern \"C\" __global__ void __launch_bounds__(256" << mask_min_waves() << ") polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
           << "  __shared__ uint4 stage_[4 * 8 * " << FS / 16 << "];\n"
@@ -466,18 +501,46 @@ struct Gen {
           << "  { const u32 v_ = sm8_of_byte(threadIdx.x); tabm_[threadIdx.x] = (unsigned char)(v_ & QMAG);\n"
           << "    tabs_[threadIdx.x] = (unsigned char)(v_ >> 7); }\n"
           << "  __syncthreads();\n"
-          << "  const int lane = threadIdx.x & 63, row = lane >> 4, pl = lane & 15, wib = threadIdx.x >> 6;\n"
-          << "  const long wave = (long)blockIdx.x * 4 + wib;\n"
-          << "  if (wave * 8 >= batch) return;\n"
-          << "  const long f_lo = wave * 8 + row, f_hi = wave * 8 + 4 + row;\n"
+          << "  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR batch indices\n"
+          << "  const long nw_ = ((long)batch + 7) / 8, wstride_ = (long)gridDim.x * 4;\n"
+          << "  long wave = (long)blockIdx.x * 4 + wib;\n"
+          << "  if (wave >= nw_) return;\n"
           << "  unsigned char *st_ = (unsigned char *)stage_ + wib * " << 8 * FS << ";\n"
-          << "  if ((((unsigned long)llr) & 15u) == 0u) {\n"
-          << "    for (int q = lane; q < " << chunks << "; q += 64) {\n"
-          << "      const int f = q / " << N / 16 << ", off = (q % " << N / 16 << ") * 16;\n"
-          << "      const long fr = wave * 8 + f < batch ? wave * 8 + f : (long)batch - 1;\n"
-          << "      *(uint4 *)(st_ + f * " << FS << " + off) = *(const uint4 *)(llr + fr * " << N << " + off);\n"
-          << "    }\n"
-          << "  } else {   // input not 16-byte aligned: byte copy\n"
+          << "  const bool al_ = (((unsigned long)llr) & 15u) == 0u;\n"
+          << "  const unsigned char *lla_ = (const unsigned char *)((unsigned long)llr & ~15ul);   // 16-byte aligned\n"
+          // async HBM -> LDS copy of the 8 frames of batch w, frames past the batch clamped to
+          // the last one (w past the last batch: the last frame 8 times, one 1 KB row that
+          // stays in cache). Uniform frame base (SGPR) + lane offset: one VGPR for all eight
+          // loads, and branch-free -- a branch in the middle of the straight-line decode costs
+          // the register allocator ~100 VGPRs. lla_: the input rounded down to 16 bytes (an
+          // unaligned input is byte-copied instead and the async rows are overwritten).
+          << "  auto fetch_ = [&](long w, int lane) {\n"
+          << "    const long f0_ = w * 8;\n";
+        for (int f = 0; f < 8; f++)
+            for (int c = 0; c < (LPF + 63) / 64; c++) {
+                // the LDS row of lane i is base + 16 i whatever its global address, so a frame
+                // of fewer than 64 chunks (N < 1024) loads with the other lanes masked off
+                const std::string ch = "(" + std::to_string(c * 64) + " + lane)";
+                o << "    if (" << (LPF - c * 64 >= 64 ? std::string("true") : "lane < " + std::to_string(LPF - c * 64))
+                  << ") { const long fr_ = f0_ + " << f << " < batch ? f0_ + " << f << " : (long)batch - 1;\n"
+                  << "      __builtin_amdgcn_global_load_lds((gas_t)(lla_ + fr_ * " << N << " + " << ch
+                  << " * 16), (las_t)(st_ + " << f * FS + c * 1024 << "), 16, 0, 0); }\n";
+            }
+        // Lane-derived values are recomputed in every iteration (the empty asm makes the lane
+        // index loop-variant): hoisted out of the loop they would stay live across the whole
+        // decode (~30 VGPRs, 4 -> 3 waves per SIMD).
+        o << "  };\n"
+          << (prefetch || resplit ? "  fetch_(wave, threadIdx.x & 63);\n" : "")
+          << (persist ? "  for (; wave < nw_; wave += wstride_) {\n" : "  {\n")
+          << "  int lane = threadIdx.x & 63;\n"
+          << "  asm volatile(\"\" : \"+v\"(lane));\n"
+          << "  const int row = lane >> 4, pl = lane & 15;\n"
+          << "  Lanes ln; ln.init((u32)pl);\n"
+          << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
+          << " + ln.pos;\n"
+          << (prefetch || resplit ? "" : "  fetch_(wave, lane);\n")
+          << "  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this batch's channel is in LDS\n"
+          << "  if (!al_) {   // input not 16-byte aligned: byte copy\n"
           << "    for (int q = lane; q < " << 8 * N << "; q += 64) {\n"
           << "      const int f = q / " << N << ", off = q % " << N << ";\n"
           << "      const long fr = wave * 8 + f < batch ? wave * 8 + f : (long)batch - 1;\n"
@@ -487,22 +550,17 @@ struct Gen {
           << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
           << "  __builtin_amdgcn_wave_barrier();\n"
           << "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n"
-          << "  Lanes ln; ln.init((u32)pl);\n"
-          << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
-          << " + ln.pos;\n"
           << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
-        presplit = true;
-        {
-            const char *e = std::getenv("POLAR_SC_ROOT_RESPLIT");
-            resplit = e && e[0] == '1';
-            const char *pe = std::getenv("POLAR_SC_ROOT_PACK");
-            pack = !resplit && G >= 2 && !(pe && pe[0] == '0');
-        }
         stage_arrays(true);
         root_presplit(G);
+        if (prefetch)   // the staged channel is consumed: prefetch the next batch into it
+            o << "  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the presplit reads are done\n"
+              << "  __builtin_amdgcn_wave_barrier();\n"
+              << "  fetch_(wave + wstride_, lane);\n";
         all_ops();
         // END (my_module.h:1848-1869) + wrapper_out: x^ words in natural order
-        o << "  const bool st_lo = f_lo < batch, st_hi = f_hi < batch;\n"
+        o << "  const long f_lo = wave * 8 + (lane >> 4), f_hi = f_lo + 4;\n"
+          << "  const bool st_lo = f_lo < batch, st_hi = f_hi < batch;\n"
           << "  unsigned short *o_lo = out + (size_t)f_lo * out_stride, *o_hi = out + (size_t)f_hi * out_stride;\n";
         for (int c = 0; c < (G + 15) / 16; c++) {
             o << "  { const u32 t_ = row_transpose16(to_position_order(" << get16(16 * c) << ", ln), ln); const int w_ = " << 16 * c << " + pl;\n"
@@ -510,6 +568,9 @@ struct Gen {
               << "if (st_hi) o_hi[w_] = (unsigned short)(t_ >> 16); } }\n";
         }
         o << "  for (int w_ = " << G << " + pl; w_ < out_stride; w_ += 16) { if (st_lo) o_lo[w_] = 0; if (st_hi) o_hi[w_] = 0; }\n"
+          << (resplit ? "  if (al_ && wave + wstride_ < nw_) fetch_(wave + wstride_, lane);   // root G re-read the channel\n"
+                      : "")
+          << "  }\n"
           << "}\n";
         return o.str();
     }
@@ -724,6 +785,19 @@ int jit_load(const polar_sc_plan &p, DevState &st)
         return -EIO;
     if (!p.tiers.empty() && hipModuleGetFunction(&st.fn_tier, st.module, "polar_sc_tier_kernel") != hipSuccess)
         return -EIO;
+    if (!p.hybrid) {
+        // per-mask kernel, persistent variant (POLAR_SC_MASK_PERSIST=R): grid = R x the blocks
+        // resident on the device at once; every wave loops over its 8-frame batches with the
+        // next channel prefetched into LDS (run_mask). Default: one batch per wave.
+        const int rounds = mask_persist();
+        int per_cu = 0;
+        if (rounds > 0 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, st.fn, 256, 0) == hipSuccess &&
+            per_cu > 0)
+            st.mask_blocks = rounds * per_cu * (st.simds > 0 ? st.simds / 4 : 256);
+        if (std::getenv("POLAR_SC_VERBOSE"))
+            std::fprintf(stderr, "polar_sc: per-mask kernel N=%u: %d resident blocks per CU, grid cap %d blocks\n",
+                         p.N, per_cu, st.mask_blocks);
+    }
     return 0;
 }
 
@@ -732,7 +806,9 @@ int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, ui
 {
     (void)p;
     const long waves = (batch + 7) / 8;
-    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    long nb = (waves + 3) / 4;
+    if (st.mask_blocks > 0 && nb > st.mask_blocks) nb = st.mask_blocks;   // persistent waves
+    const unsigned blocks = (unsigned)nb;
     int b = (int)batch;
     void *args[] = {(void *)&llr, (void *)&out, (void *)&b, (void *)&out_stride};
     hipError_t e = hipModuleLaunchKernel(st.fn, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream, args, nullptr);

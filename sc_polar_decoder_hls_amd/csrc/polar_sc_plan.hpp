@@ -28,6 +28,7 @@ struct DevState {
     hipModule_t module16 = nullptr;     // interpreter on the int16 channel (polar_sc_decode_i16)
     hipFunction_t fn16 = nullptr;
     int simds = 0;                // SIMDs of the device (4 per CU), for launch sizing
+    int mask_blocks = 0;          // per-mask kernel: grid cap (persistent waves), 0 = one batch per wave
 };
 
 enum JitMode { JIT_OFF = 0, JIT_AUTO = 1 };
