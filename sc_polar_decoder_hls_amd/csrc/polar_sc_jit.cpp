@@ -40,6 +40,15 @@ std::string mask_min_waves()
 }
 // per-mask kernels: POLAR_SC_MASK_PERSIST=R (>= 1) builds the persistent batch loop and caps
 // the grid at R x the resident blocks; 0 / unset: one 8-frame batch per wave, no loop
+// per-mask kernels: waves per block (POLAR_SC_MASK_WPB 1 / 2 / 4 / 8, default 4); each wave
+// has its own 8-frame batch and LDS stage, so the block size only sets the granularity at
+// which LDS is allocated and released
+int mask_wpb()
+{
+    const char *e = std::getenv("POLAR_SC_MASK_WPB");
+    const int w = (e && *e) ? std::atoi(e) : 4;
+    return (w == 1 || w == 2 || w == 8) ? w : 4;
+}
 int mask_persist()
 {
     const char *e = std::getenv("POLAR_SC_MASK_PERSIST");
@@ -489,21 +498,22 @@ struct Gen {
         // loop with prefetch (C2 same box: 74.0 vs 79.5 us, tools/gpu_ab_persist.sh), and the
         // loop alone costs ~10 VGPRs.
         const bool persist = mask_persist();
+        const int wpb = mask_wpb();
         const bool prefetch = persist && !resplit && LPF >= 64;
         o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
           << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
           << "typedef const __attribute__((address_space(1))) void *gas_t;\n"
           << "typedef __attribute__((address_space(3))) void *las_t;\n"
-          << "extern \"C\" __global__ void __launch_bounds__(256" << mask_min_waves() << ") polar_sc_mask_kernel(\n"
+          << "extern \"C\" __global__ void __launch_bounds__(" << 64 * wpb << mask_min_waves() << ") polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
-          << "  __shared__ uint4 stage_[4 * 8 * " << FS / 16 << "];\n"
+          << "  __shared__ uint4 stage_[" << wpb << " * 8 * " << FS / 16 << "];\n"
           << "  __shared__ unsigned char tabm_[256], tabs_[256];   // channel byte -> |LLR|, sign (qconv_format)\n"
-          << "  { const u32 v_ = sm8_of_byte(threadIdx.x); tabm_[threadIdx.x] = (unsigned char)(v_ & QMAG);\n"
-          << "    tabs_[threadIdx.x] = (unsigned char)(v_ >> 7); }\n"
+          << "  for (u32 t_ = threadIdx.x; t_ < 256u; t_ += " << 64 * wpb << "u) { const u32 v_ = sm8_of_byte(t_);\n"
+          << "    tabm_[t_] = (unsigned char)(v_ & QMAG); tabs_[t_] = (unsigned char)(v_ >> 7); }\n"
           << "  __syncthreads();\n"
           << "  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR batch indices\n"
-          << "  const long nw_ = ((long)batch + 7) / 8, wstride_ = (long)gridDim.x * 4;\n"
-          << "  long wave = (long)blockIdx.x * 4 + wib;\n"
+          << "  const long nw_ = ((long)batch + 7) / 8, wstride_ = (long)gridDim.x * " << wpb << ";\n"
+          << "  long wave = (long)blockIdx.x * " << wpb << " + wib;\n"
           << "  if (wave >= nw_) return;\n"
           << "  unsigned char *st_ = (unsigned char *)stage_ + wib * " << 8 * FS << ";\n"
           << "  const bool al_ = (((unsigned long)llr) & 15u) == 0u;\n"
@@ -791,7 +801,7 @@ int jit_load(const polar_sc_plan &p, DevState &st)
         // next channel prefetched into LDS (run_mask). Default: one batch per wave.
         const int rounds = mask_persist();
         int per_cu = 0;
-        if (rounds > 0 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, st.fn, 256, 0) == hipSuccess &&
+        if (rounds > 0 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, st.fn, 64 * mask_wpb(), 0) == hipSuccess &&
             per_cu > 0)
             st.mask_blocks = rounds * per_cu * (st.simds > 0 ? st.simds / 4 : 256);
         if (std::getenv("POLAR_SC_VERBOSE"))
@@ -806,12 +816,13 @@ int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, ui
 {
     (void)p;
     const long waves = (batch + 7) / 8;
-    long nb = (waves + 3) / 4;
+    const int wpb = mask_wpb();
+    long nb = (waves + wpb - 1) / wpb;
     if (st.mask_blocks > 0 && nb > st.mask_blocks) nb = st.mask_blocks;   // persistent waves
     const unsigned blocks = (unsigned)nb;
     int b = (int)batch;
     void *args[] = {(void *)&llr, (void *)&out, (void *)&b, (void *)&out_stride};
-    hipError_t e = hipModuleLaunchKernel(st.fn, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream, args, nullptr);
+    hipError_t e = hipModuleLaunchKernel(st.fn, blocks, 1, 1, 64 * wpb, 1, 1, 0, (hipStream_t)stream, args, nullptr);
     return e == hipSuccess ? 0 : -EIO;
 }
 
