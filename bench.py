@@ -32,11 +32,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # bytes they report (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
 # roofline.traffic when the benchmarked (mask, frames per GPU) is the profiled one.
 TRAFFIC_PROFILES = {
-    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r02_v4_c2_pmc.json"),
+    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r02_v5_c2_pmc.json"),
     # grid-tier plans: totals per decode over all its launches (tools/pmc_summary.py --reps)
-    ("frozen_n_65536_k_32768", 4096): os.path.join(ROOT, "profiles", "r02_v4_c3_pmc.json"),
-    ("frozen_n_262144_k_131072", 512): os.path.join(ROOT, "profiles", "r02_v4_c5_pmc.json"),
-    ("frozen_n_262144_k_131072", 64): os.path.join(ROOT, "profiles", "r02_v4_c5_b64_pmc.json"),
+    ("frozen_n_65536_k_32768", 4096): os.path.join(ROOT, "profiles", "r02_v5_c3_pmc.json"),
+    ("frozen_n_262144_k_131072", 512): os.path.join(ROOT, "profiles", "r02_v5_c5_pmc.json"),
+    ("frozen_n_262144_k_131072", 64): os.path.join(ROOT, "profiles", "r02_v5_c5_b64_pmc.json"),
 }
 # Rotated input: the timed loop cycles through distinct resident batches of at least this
 # many bytes in total, so the LLR reads come from HBM and not from the 256 MB Infinity Cache
@@ -48,7 +48,7 @@ EBN0_SWEEP = (1.0, 2.5, 4.0)   # throughput depends weakly on the
 # instruction of the packed-16 / DPP / v_perm classes the decoder issues, by waves per SIMD
 # (independent chains). 8 waves: 2.62 (32-bit ALU 1.45); 4: 3.25; 2: 4.45; 1: 5.20. The
 # roofline peak is the full-occupancy figure; the per-mask kernel runs at 4 waves per SIMD
-# (126 VGPRs with the packed root, 33 KB of LDS per 4-wave block).
+# (123 VGPRs with the packed root and the LDS-DMA channel fetch, 33 KB of LDS per 4-wave block).
 VALU_CYCLES_PER_INST = 2.62
 VALU_CYCLES_BY_WAVES = {1: 5.20, 2: 4.45, 4: 3.25, 8: 2.62}
 NOMINAL_CLOCK_GHZ = 2.4   # fallback when the PMC profile has no measured clock
@@ -405,7 +405,7 @@ def main():
                         "peak_basis": "%d SIMDs x %.2f GHz (PMC clock) / %.2f SIMD cycles per wave64 packed-16 "
                                       "VALU instruction at 8 waves/SIMD (profiles/r02_valu_microbench.log)"
                                       % (simds, ghz, VALU_CYCLES_PER_INST),
-                        # the per-mask kernel's occupancy (126 VGPRs, 33 KB LDS per 4-wave block)
+                        # the per-mask kernel's occupancy (123 VGPRs, 33 KB LDS per 4-wave block)
                         "peak_at_4_waves_per_simd": simds * ghz * 1e9 / VALU_CYCLES_BY_WAVES[4],
                         "source": os.path.relpath(prof_path, ROOT)}
         res = {
