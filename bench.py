@@ -370,12 +370,20 @@ def main():
         check = {"frames": nchk, "bit_exact": bool((got == ref).all())}
 
     # error rates of the last decoded batch vs the transmitted codewords (informative)
+    errors_all = None
     if xref is not None:
         # sc_error_counter semantics on the device (per-frame count mod 1024), whole batch
         cnt = pkg.count_errors(out, xref, N)
         torch.cuda.synchronize()
         c = [float(v) for v in cnt.cpu().tolist()]
         fer, ber = c[1] / per_gpu, c[2] / (per_gpu * N)
+        if dist is not None:
+            # the job's error totals: device counts summed over the ranks (RCCL all-reduce)
+            sharding.sum_over_ranks(cnt, dist, coll_dev)
+            t = [int(v) for v in cnt.cpu().tolist()]
+            errors_all = {"frames": frames_all, "frame_errors": t[1], "bit_errors": t[2],
+                          "bit_errors_mod1024_sum": t[0], "frame_error_rate": t[1] / frames_all,
+                          "bit_error_rate": t[2] / (frames_all * N)}
     else:
         xhat = pkg.unpack_bits(out[: min(per_gpu, 4096)].cpu().numpy(), N)
         xs = x[: xhat.shape[0]].cpu().numpy()
@@ -438,6 +446,7 @@ def main():
             "ebn0_sweep": sweep,
             "frame_error_rate": fer,
             "bit_error_rate": ber,
+            "errors_all_ranks": errors_all,
             "parity_check": check,
         }
         if world == 1 and args.host_io:

@@ -46,6 +46,20 @@ def max_over_ranks(values, dist=None, device=None):
     return [float(v) for v in t.tolist()]
 
 
+def sum_over_ranks(counts, dist=None, device=None):
+    """Error accounting over the whole job (the optional all-reduce of error
+    counts; sc_error_counter.h:50-126 counts per stream): element-wise sum of an integer
+    counter tensor over all ranks, in place on `device` (RCCL with the nccl backend). The
+    per-frame sc_uint<10> wrap is applied before the sum, by polar_count_errors."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return counts
+    t = counts.to(device) if device is not None else counts
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    if t is not counts:
+        counts.copy_(t.to(counts.device))
+    return counts
+
+
 def scatter_shards(full, total, frame_shape, dtype, dist=None, device=None):
     """Scatter a [total, *frame_shape] batch held by rank 0 into the per-rank shards of
     shard_bounds (RCCL over xGMI with the nccl backend). `full` is ignored on the other ranks

@@ -45,6 +45,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _error_counts(xhat, x):
+    """sc_error_counter.h:68-125 over a batch: [sum of per-frame bit errors mod 1024 (the
+    sc_uint<10> counter), frames with a non-zero wrapped count, exact bit errors]
+    (polar_count_errors semantics, csrc/polar_sc_channel.hip)."""
+    per = (np.asarray(xhat) != np.asarray(x)).sum(axis=1) if len(x) else np.zeros(0, np.int64)
+    return [int((per % 1024).sum()), int((per % 1024 > 0).sum()), int(per.sum())]
+
+
 def _worker(rank, world, port, total, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -54,7 +62,7 @@ def _worker(rank, world, port, total, q):
         from oracle import oracle
         mask = util.mask("FB_N128_K64")
         # every rank builds the same global batch (same seed) and decodes only its shard
-        llr, _ = util.synth_frames(mask, total, ebn0_db=1.0, seed=2024)
+        llr, x = util.synth_frames(mask, total, ebn0_db=1.0, seed=2024)
         start, count = sharding.shard_bounds(total, world, rank)
         bits = oracle.decode_fsm(mask, llr[start:start + count]) if count else np.zeros((0, mask.size), np.uint8)
         words = torch.from_numpy(np.packbits(bits.astype(np.uint8), axis=1, bitorder="little").copy()
@@ -67,13 +75,17 @@ def _worker(rank, world, port, total, q):
         ok_all = torch.tensor([1 if scattered_ok else 0])
         dist.all_reduce(ok_all)
         t = sharding.max_over_ranks([0.5 + rank, 3.0 - rank], dist)
+        # job-wide error accounting: per-rank counts (sc_error_counter semantics) summed
+        cnt = torch.tensor(_error_counts(bits, x[start:start + count]), dtype=torch.int64)
+        sharding.sum_over_ranks(cnt, dist)
         if rank == 0:
             ref = oracle.decode_fsm(mask, llr)
             ref_words = np.packbits(ref.astype(np.uint8), axis=1, bitorder="little").view(np.int64)
             q.put(("ok", bool(np.array_equal(full.numpy(), ref_words)) and int(ok_all) == world, t,
-                   [sharding.shard_bounds(total, world, r) for r in range(world)]))
+                   [sharding.shard_bounds(total, world, r) for r in range(world)],
+                   (cnt.tolist(), _error_counts(ref, x))))
     except Exception as e:   # surface worker failures to the test
-        q.put(("err", repr(e), None, None))
+        q.put(("err", repr(e), None, None, None))
         raise
     finally:
         dist.barrier()
@@ -89,7 +101,7 @@ def test_two_rank_gloo_shard_decode_gather(oracle_mod, total):
     for p in procs:
         p.start()
     try:
-        status, same, t, spans = q.get(timeout=240)
+        status, same, t, spans, errs = q.get(timeout=240)
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -97,4 +109,5 @@ def test_two_rank_gloo_shard_decode_gather(oracle_mod, total):
     assert same, "gathered shard decode differs from the single-process decode"
     assert t == [1.5, 3.0]
     assert sum(c for _, c in spans) == total
+    assert errs[0] == errs[1], "error counts summed over ranks differ from the whole batch's"
     assert all(p.exitcode == 0 for p in procs)
