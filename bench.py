@@ -336,24 +336,6 @@ def main():
     llr, xref, x = batches[last]
     out = outs[last]
 
-    # Eb/N0 sweep (BASELINE.md 2): the same timed loop on frames at each SNR
-    sweep = None
-    if args.ebn0_sweep:
-        sweep = []
-        for e in EBN0_SWEEP:
-            bs = make_batches(pkg, torch, args, mask, per_gpu, frame0, sum(counts), dev, e, nb)
-            el, km = timed_decodes(torch, sharding, dist, coll_dev, dec, bs, outs, max(1, args.steps // 2),
-                                   max(1, args.warmup // 4), stream)
-            ent = {"ebn0_db": e, "value": frames_all * max(1, args.steps // 2) / el * K,
-                   "ms_per_step": el / max(1, args.steps // 2) * 1e3, "kernel_ms": km}
-            if bs[0][1] is not None:
-                cnt = pkg.count_errors(outs[(max(1, args.steps // 2) - 1) % nb], bs[(max(1, args.steps // 2) - 1) % nb][1], N)
-                torch.cuda.synchronize()
-                ent["frame_error_rate"] = float(cnt[1].item()) / per_gpu
-            sweep.append(ent)
-            del bs
-        torch.cuda.synchronize()
-
     scatter_res = None
     if args.io == "scatter" and dist is not None:
         scatter_res = time_scatter_gather(torch, pkg, sharding, dist, dec, mask, frames_all, rank, dev,
@@ -389,6 +371,25 @@ def main():
         xs = x[: xhat.shape[0]].cpu().numpy()
         fer = float((xhat != xs).any(axis=1).mean())
         ber = float((xhat != xs).mean())
+
+    # (after the parity check and the error counts: the sweep reuses the output buffers)
+    # Eb/N0 sweep (BASELINE.md 2): the same timed loop on frames at each SNR
+    sweep = None
+    if args.ebn0_sweep:
+        sweep = []
+        for e in EBN0_SWEEP:
+            bs = make_batches(pkg, torch, args, mask, per_gpu, frame0, sum(counts), dev, e, nb)
+            el, km = timed_decodes(torch, sharding, dist, coll_dev, dec, bs, outs, max(1, args.steps // 2),
+                                   max(1, args.warmup // 4), stream)
+            ent = {"ebn0_db": e, "value": frames_all * max(1, args.steps // 2) / el * K,
+                   "ms_per_step": el / max(1, args.steps // 2) * 1e3, "kernel_ms": km}
+            if bs[0][1] is not None:
+                cnt = pkg.count_errors(outs[(max(1, args.steps // 2) - 1) % nb], bs[(max(1, args.steps // 2) - 1) % nb][1], N)
+                torch.cuda.synchronize()
+                ent["frame_error_rate"] = float(cnt[1].item()) / per_gpu
+            sweep.append(ent)
+            del bs
+        torch.cuda.synchronize()
 
     if rank == 0:
         bytes_per_launch = 1.125 * N * per_gpu
