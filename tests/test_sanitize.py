@@ -64,7 +64,9 @@ def test_host_library_asan_ubsan(pkg, tmp_path):
                                                "-I" + os.path.join(ROOT, "include"), "-I" + _build.GEN_DIR]
                               + _build.SOURCES + ["-o", lib, "-lhiprtc"])
     if _stale(exe, [lib, os.path.join(SAN, "host_san.c")]):
-        subprocess.check_call([_build.hipcc(), "-x", "c", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"]
+        # host-only C driver (no device code): -fno-gpu-sanitize keeps the sanitizers off any GPU target
+        subprocess.check_call([_build.hipcc(), "-x", "c", "-fno-gpu-sanitize", "-fsanitize=address,undefined",
+                               "-fno-sanitize-recover=all"]
                               + FLAGS + ["-I" + os.path.join(ROOT, "include"), os.path.join(SAN, "host_san.c"),
                                          "-o", exe, "-L" + OUT, "-lpolar_sc_san", "-Wl,-rpath," + OUT])
     # table files in both reference formats, written from the repo's mask fixtures
