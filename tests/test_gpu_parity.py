@@ -244,3 +244,23 @@ def test_gpu_matches_committed_vectors(pkg, cuda, case, jit):
     """GPU decode of the committed regression vectors (tests/golden/decode_vectors.npz)."""
     name, llr, x = util.decode_vectors()[case]
     _assert_same(_decode(pkg, cuda, util.mask(name), llr, jit), x, case)
+
+@pytest.mark.parametrize("name,batch", [("FB_N1024_K512", 40003), ("FB_N256_K128", 60001)])
+def test_persistent_mask_kernel(pkg, cuda, oracle_mod, monkeypatch, name, batch):
+    """POLAR_SC_MASK_PERSIST=1: the per-mask kernel as a persistent batch loop (grid = the
+    resident blocks, N = 1024 prefetching the next channel into LDS mid-decode, N < 1024
+    fetching at the top of each iteration). Batches larger than one batch per resident wave,
+    ragged: equal to the default kernel on every frame, and to the oracle on a sample."""
+    mask = util.mask(name)
+    llr, _ = util.synth_frames(mask, batch, ebn0_db=1.5, seed=77)
+    dev = cuda.from_numpy(llr).cuda()
+    ref_dec = make_decoder(pkg, mask, True)
+    ref = ref_dec.decode(dev)
+    monkeypatch.setenv("POLAR_SC_MASK_PERSIST", "1")
+    dec = make_decoder(pkg, mask, True)
+    got = dec.decode(dev)
+    cuda.cuda.synchronize()
+    g = pkg.unpack_bits(got.cpu().numpy(), mask.size)
+    _assert_same(g, pkg.unpack_bits(ref.cpu().numpy(), mask.size), "persistent vs default " + name)
+    idx = np.r_[0:48, batch - 40:batch]
+    _assert_same(g[idx], oracle_mod.decode_fsm(mask, llr[idx]), "persistent vs oracle " + name)
