@@ -654,6 +654,22 @@ namespace {
 // once on the build host and the cache travels with the in-tree library.
 const char *const kRtcOpts[] = {"--gpu-architecture=gfx950", "-O3", "-std=c++17"};
 
+// POLAR_SC_RTC_EXTRA: extra hipRTC options, separated by spaces or commas (e.g.
+// "-mllvm,-amdgpu-sched-strategy=max-ilp"), for compiler A/Bs; part of the cache key
+std::vector<std::string> rtc_extra()
+{
+    std::vector<std::string> v;
+    const char *e = std::getenv("POLAR_SC_RTC_EXTRA");
+    if (!e) return v;
+    std::string t(e);
+    for (char &ch : t)
+        if (ch == ',') ch = ' ';   // commas separate too (shell-friendly)
+    std::istringstream in(t);
+    std::string w;
+    while (in >> w) v.push_back(w);
+    return v;
+}
+
 uint64_t fnv1a(uint64_t h, const char *s, size_t n)
 {
     for (size_t i = 0; i < n; i++) {
@@ -682,6 +698,7 @@ std::string cache_path(const std::string &src)
     h = fnv1a(h, kPolarDeviceSrc, sizeof kPolarDeviceSrc);
     h = fnv1a(h, kPolarInterpSrc, sizeof kPolarInterpSrc);
     for (const char *o : kRtcOpts) h = fnv1a(h, o, std::strlen(o) + 1);
+    for (const std::string &o : rtc_extra()) h = fnv1a(h, o.c_str(), o.size() + 1);
     int ver_major = 0, ver_minor = 0;
     hiprtcVersion(&ver_major, &ver_minor);
     h = fnv1a(h, (const char *)&ver_major, sizeof ver_major);
@@ -728,7 +745,10 @@ int rtc_compile(const std::string &src, std::vector<char> &code, std::string &lo
     const char *hdrs[] = {kPolarDeviceSrc, kPolarInterpSrc};
     const char *names[] = {"polar_sc_device.h", "polar_sc_interp.h"};
     if (hiprtcCreateProgram(&prog, src.c_str(), "polar_sc_mask.hip", 2, hdrs, names) != HIPRTC_SUCCESS) return -EIO;
-    hiprtcResult rc = hiprtcCompileProgram(prog, 3, const_cast<const char **>(kRtcOpts));
+    const std::vector<std::string> extra = rtc_extra();
+    std::vector<const char *> opts(std::begin(kRtcOpts), std::end(kRtcOpts));
+    for (const std::string &o : extra) opts.push_back(o.c_str());
+    hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     size_t log_size = 0;
     hiprtcGetProgramLogSize(prog, &log_size);
     if (log_size > 1) {
