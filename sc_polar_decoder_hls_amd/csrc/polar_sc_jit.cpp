@@ -499,6 +499,7 @@ struct Gen {
         // loop alone costs ~10 VGPRs.
         const bool persist = mask_persist();
         const int wpb = mask_wpb();
+        p.mask_wpb = wpb;   // the launch shape of this source (jit_load -> DevState)
         const bool prefetch = persist && !resplit && LPF >= 64;
         o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
           << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
@@ -816,12 +817,14 @@ int jit_load(const polar_sc_plan &p, DevState &st)
     if (!p.tiers.empty() && hipModuleGetFunction(&st.fn_tier, st.module, "polar_sc_tier_kernel") != hipSuccess)
         return -EIO;
     if (!p.hybrid) {
+        // waves per block as generated into this plan's kernel source (run_mask)
+        st.mask_wpb = p.mask_wpb;
         // per-mask kernel, persistent variant (POLAR_SC_MASK_PERSIST=R): grid = R x the blocks
         // resident on the device at once; every wave loops over its 8-frame batches with the
         // next channel prefetched into LDS (run_mask). Default: one batch per wave.
         const int rounds = mask_persist();
         int per_cu = 0;
-        if (rounds > 0 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, st.fn, 64 * mask_wpb(), 0) == hipSuccess &&
+        if (rounds > 0 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, st.fn, 64 * st.mask_wpb, 0) == hipSuccess &&
             per_cu > 0)
             st.mask_blocks = rounds * per_cu * (st.simds > 0 ? st.simds / 4 : 256);
         if (std::getenv("POLAR_SC_VERBOSE"))
@@ -836,7 +839,7 @@ int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, ui
 {
     (void)p;
     const long waves = (batch + 7) / 8;
-    const int wpb = mask_wpb();
+    const int wpb = st.mask_wpb;
     long nb = (waves + wpb - 1) / wpb;
     if (st.mask_blocks > 0 && nb > st.mask_blocks) nb = st.mask_blocks;   // persistent waves
     const unsigned blocks = (unsigned)nb;

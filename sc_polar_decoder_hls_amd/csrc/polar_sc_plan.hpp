@@ -29,6 +29,7 @@ struct DevState {
     hipFunction_t fn16 = nullptr;
     int simds = 0;                // SIMDs of the device (4 per CU), for launch sizing
     int mask_blocks = 0;          // per-mask kernel: grid cap (persistent waves), 0 = one batch per wave
+    int mask_wpb = 4;             // per-mask kernel: waves per block, from its compiled launch bound
 };
 
 enum JitMode { JIT_OFF = 0, JIT_AUTO = 1 };
@@ -109,6 +110,7 @@ struct polar_sc_plan {
     mutable std::vector<char> interp_code;   // per-mask plans, llr_bits != 6: traced interpreter
     mutable std::vector<char> code16;        // interpreter on the int16 channel (polar_sc_decode_i16)
     mutable std::string jit_log;
+    mutable int mask_wpb = 4;             // per-mask kernel: waves per block of the generated source
 };
 
 namespace polar_host {
