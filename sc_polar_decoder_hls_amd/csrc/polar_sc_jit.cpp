@@ -497,7 +497,9 @@ struct Gen {
         // Off by default (mask_persist): one batch per wave measured faster than the persistent
         // loop with prefetch (C2 same box: 74.0 vs 79.5 us, tools/gpu_ab_persist.sh), and the
         // loop alone costs ~10 VGPRs.
-        const bool persist = mask_persist();
+        const int rounds = mask_persist();
+        const bool persist = rounds > 0;
+        p.mask_rounds = rounds;   // the grid cap of this source (0: one batch per wave)
         const int wpb = mask_wpb();
         p.mask_wpb = wpb;   // the launch shape of this source (jit_load -> DevState)
         const bool prefetch = persist && !resplit && LPF >= 64;
@@ -822,7 +824,7 @@ int jit_load(const polar_sc_plan &p, DevState &st)
         // per-mask kernel, persistent variant (POLAR_SC_MASK_PERSIST=R): grid = R x the blocks
         // resident on the device at once; every wave loops over its 8-frame batches with the
         // next channel prefetched into LDS (run_mask). Default: one batch per wave.
-        const int rounds = mask_persist();
+        const int rounds = p.mask_rounds;   // as generated: a capped grid needs the batch loop
         int per_cu = 0;
         if (rounds > 0 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, st.fn, 64 * st.mask_wpb, 0) == hipSuccess &&
             per_cu > 0)

@@ -111,6 +111,7 @@ struct polar_sc_plan {
     mutable std::vector<char> code16;        // interpreter on the int16 channel (polar_sc_decode_i16)
     mutable std::string jit_log;
     mutable int mask_wpb = 4;             // per-mask kernel: waves per block of the generated source
+    mutable int mask_rounds = 0;          //   and its persistent-loop grid cap (0: no loop)
 };
 
 namespace polar_host {
