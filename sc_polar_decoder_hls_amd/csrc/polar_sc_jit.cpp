@@ -503,6 +503,14 @@ struct Gen {
         const int wpb = mask_wpb();
         p.mask_wpb = wpb;   // the launch shape of this source (jit_load -> DevState)
         const bool prefetch = persist && !resplit && LPF >= 64;
+        // Two batches per wave in straight-line code (POLAR_SC_MASK_DUAL=1, N = 1024): the grid
+        // holds half the waves, each decodes batch w and then w + (grid waves), the second
+        // batch's channel prefetched into LDS right after the first one's presplit -- the
+        // persistent loop's overlap without a loop (no loop-carried registers); every frame
+        // index past the batch is clamped and its stores suppressed, so there is no branch.
+        const char *de = std::getenv("POLAR_SC_MASK_DUAL");
+        const bool dual = !persist && !resplit && LPF >= 64 && de && de[0] == '1';
+        p.mask_dual = dual ? 1 : 0;
         o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
           << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
           << "typedef const __attribute__((address_space(1))) void *gas_t;\n"
@@ -543,48 +551,52 @@ struct Gen {
         // index loop-variant): hoisted out of the loop they would stay live across the whole
         // decode (~30 VGPRs, 4 -> 3 waves per SIMD).
         o << "  };\n"
-          << (prefetch || resplit ? "  fetch_(wave, threadIdx.x & 63);\n" : "")
-          << (persist ? "  for (; wave < nw_; wave += wstride_) {\n" : "  {\n")
-          << "  int lane = threadIdx.x & 63;\n"
-          << "  asm volatile(\"\" : \"+v\"(lane));\n"
-          << "  const int row = lane >> 4, pl = lane & 15;\n"
-          << "  Lanes ln; ln.init((u32)pl);\n"
-          << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
-          << " + ln.pos;\n"
-          << (prefetch || resplit ? "" : "  fetch_(wave, lane);\n")
-          << "  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this batch's channel is in LDS\n"
-          << "  if (!al_) {   // input not 16-byte aligned: byte copy\n"
-          << "    for (int q = lane; q < " << 8 * N << "; q += 64) {\n"
-          << "      const int f = q / " << N << ", off = q % " << N << ";\n"
-          << "      const long fr = wave * 8 + f < batch ? wave * 8 + f : (long)batch - 1;\n"
-          << "      st_[f * " << FS << " + off] = llr[fr * " << N << " + off];\n"
-          << "    }\n"
-          << "  }\n"
-          << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
-          << "  __builtin_amdgcn_wave_barrier();\n"
-          << "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n"
-          << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
-        stage_arrays(true);
-        root_presplit(G);
-        if (prefetch)   // the staged channel is consumed: prefetch the next batch into it
-            o << "  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the presplit reads are done\n"
+          << (prefetch || resplit || dual ? "  fetch_(wave, threadIdx.x & 63);\n" : "");
+        for (int k = 0; k < (dual ? 2 : 1); k++) {
+            root_f_done = false;
+            o << (persist ? "  for (; wave < nw_; wave += wstride_) {\n" : "  {\n")
+              << (k == 1 ? "  wave += wstride_;   // second batch of this wave (may be past the last: no stores)\n" : "")
+              << "  int lane = threadIdx.x & 63;\n"
+              << "  asm volatile(\"\" : \"+v\"(lane));\n"
+              << "  const int row = lane >> 4, pl = lane & 15;\n"
+              << "  Lanes ln; ln.init((u32)pl);\n"
+              << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
+              << " + ln.pos;\n"
+              << (prefetch || resplit || dual ? "" : "  fetch_(wave, lane);\n")
+              << "  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this batch's channel is in LDS\n"
+              << "  if (!al_) {   // input not 16-byte aligned: byte copy\n"
+              << "    for (int q = lane; q < " << 8 * N << "; q += 64) {\n"
+              << "      const int f = q / " << N << ", off = q % " << N << ";\n"
+              << "      const long fr = wave * 8 + f < batch ? wave * 8 + f : (long)batch - 1;\n"
+              << "      st_[f * " << FS << " + off] = llr[fr * " << N << " + off];\n"
+              << "    }\n"
+              << "  }\n"
+              << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
               << "  __builtin_amdgcn_wave_barrier();\n"
-              << "  fetch_(wave + wstride_, lane);\n";
-        all_ops();
-        // END (my_module.h:1848-1869) + wrapper_out: x^ words in natural order
-        o << "  const long f_lo = wave * 8 + (lane >> 4), f_hi = f_lo + 4;\n"
-          << "  const bool st_lo = f_lo < batch, st_hi = f_hi < batch;\n"
-          << "  unsigned short *o_lo = out + (size_t)f_lo * out_stride, *o_hi = out + (size_t)f_hi * out_stride;\n";
-        for (int c = 0; c < (G + 15) / 16; c++) {
-            o << "  { const u32 t_ = row_transpose16(to_position_order(" << get16(16 * c) << ", ln), ln); const int w_ = " << 16 * c << " + pl;\n"
-              << "    if (w_ < " << G << ") { if (st_lo) o_lo[w_] = (unsigned short)(t_ & 0xFFFFu); "
-              << "if (st_hi) o_hi[w_] = (unsigned short)(t_ >> 16); } }\n";
+              << "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n"
+              << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
+            stage_arrays(true);
+            root_presplit(G);
+            if (prefetch || (dual && k == 0))   // the staged channel is consumed: prefetch the next batch into it
+                o << "  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the presplit reads are done\n"
+                  << "  __builtin_amdgcn_wave_barrier();\n"
+                  << "  fetch_(wave + wstride_, lane);\n";
+            all_ops();
+            // END (my_module.h:1848-1869) + wrapper_out: x^ words in natural order
+            o << "  const long f_lo = wave * 8 + (lane >> 4), f_hi = f_lo + 4;\n"
+              << "  const bool st_lo = f_lo < batch, st_hi = f_hi < batch;\n"
+              << "  unsigned short *o_lo = out + (size_t)f_lo * out_stride, *o_hi = out + (size_t)f_hi * out_stride;\n";
+            for (int c = 0; c < (G + 15) / 16; c++) {
+                o << "  { const u32 t_ = row_transpose16(to_position_order(" << get16(16 * c) << ", ln), ln); const int w_ = " << 16 * c << " + pl;\n"
+                  << "    if (w_ < " << G << ") { if (st_lo) o_lo[w_] = (unsigned short)(t_ & 0xFFFFu); "
+                  << "if (st_hi) o_hi[w_] = (unsigned short)(t_ >> 16); } }\n";
+            }
+            o << "  for (int w_ = " << G << " + pl; w_ < out_stride; w_ += 16) { if (st_lo) o_lo[w_] = 0; if (st_hi) o_hi[w_] = 0; }\n"
+              << (resplit ? "  if (al_ && wave + wstride_ < nw_) fetch_(wave + wstride_, lane);   // root G re-read the channel\n"
+                          : "")
+              << "  }\n";
         }
-        o << "  for (int w_ = " << G << " + pl; w_ < out_stride; w_ += 16) { if (st_lo) o_lo[w_] = 0; if (st_hi) o_hi[w_] = 0; }\n"
-          << (resplit ? "  if (al_ && wave + wstride_ < nw_) fetch_(wave + wstride_, lane);   // root G re-read the channel\n"
-                      : "")
-          << "  }\n"
-          << "}\n";
+        o << "}\n";
         return o.str();
     }
 };
@@ -839,10 +851,10 @@ int jit_load(const polar_sc_plan &p, DevState &st)
 int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
                int out_stride, void *stream)
 {
-    (void)p;
     const long waves = (batch + 7) / 8;
     const int wpb = st.mask_wpb;
-    long nb = (waves + wpb - 1) / wpb;
+    const long gw = p.mask_dual ? (waves + 1) / 2 : waves;   // dual kernels: two batches per wave
+    long nb = (gw + wpb - 1) / wpb;
     if (st.mask_blocks > 0 && nb > st.mask_blocks) nb = st.mask_blocks;   // persistent waves
     const unsigned blocks = (unsigned)nb;
     int b = (int)batch;

@@ -112,6 +112,7 @@ struct polar_sc_plan {
     mutable std::string jit_log;
     mutable int mask_wpb = 4;             // per-mask kernel: waves per block of the generated source
     mutable int mask_rounds = 0;          //   and its persistent-loop grid cap (0: no loop)
+    mutable int mask_dual = 0;            //   1: two batches per wave (POLAR_SC_MASK_DUAL)
 };
 
 namespace polar_host {
