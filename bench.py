@@ -111,21 +111,20 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(mask, seconds, ebn0_db, threads=None, runs=5):
+def cpu_baseline(mask, seconds, ebn0_db, llr, threads=None, runs=5):
     """Time the CPU oracle (literal FSM restatement) on a bounded sample of the workload
-    (runs of >= 1 s, median of 5): one thread, then `threads` threads over
-    disjoint frame chunks (the ctypes call releases the GIL). Returns the multi-thread median
-    with the single-thread one beside it."""
+    (runs of >= 1 s, median of 5, the same LLR buffers as the GPU run):
+    `llr` is the head of the first resident batch the GPU decoded, copied to the host. One
+    thread, then `threads` threads over disjoint frame chunks (the ctypes call releases the
+    GIL). Returns the multi-thread median with the single-thread one beside it."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle
-    import util
     oracle.build()
     N, K = mask.size, int(mask.sum())
     if threads is None:
         # the GPU box grants 16 CPUs per GPU (os.cpu_count() shows the whole machine)
         threads = max(1, min(16, os.cpu_count() or 1))
-    sample = max(8, min(4096, int(2 ** 22 // N)))
-    llr, _ = util.synth_frames(mask, sample, ebn0_db=ebn0_db, seed=0xF0)
+    sample = llr.shape[0]
     oracle.decode_fsm(mask, llr[:2])   # warm
     per_run = max(1.0, seconds / (2 * runs))
 
@@ -149,9 +148,10 @@ def cpu_baseline(mask, seconds, ebn0_db, threads=None, runs=5):
             "kind": "port", "value_1thread": med1 * K, "runs": runs, "run_seconds": per_run,
             "values_nthreads": [v * K for v in fpsn], "values_1thread": [v * K for v in fps1],
             "nproc": os.cpu_count(), "cpu_model": cpu_model(),
-            "sample": "%d frames (N=%d K=%d, Eb/N0=%.1f dB) decoded repeatedly by oracle/polar_oracle.c "
-                      "orc_decode_fsm (literal my_module FSM): median of %d runs of %.1f s on 1 thread, then on "
-                      "%d threads (frame chunks)" % (sample, N, K, ebn0_db, runs, per_run, threads)}
+            "sample": "the first %d frames of the GPU run's first resident batch (N=%d K=%d, Eb/N0=%.1f dB, "
+                      "copied to the host) decoded repeatedly by oracle/polar_oracle.c orc_decode_fsm (literal "
+                      "my_module FSM): median of %d runs of %.1f s on 1 thread, then on %d threads (frame chunks)"
+                      % (sample, N, K, ebn0_db, runs, per_run, threads)}
 
 
 def make_batches(pkg, torch, args, mask, per_gpu, frame0, stride, dev, ebn0, nb):
@@ -176,12 +176,21 @@ def make_batches(pkg, torch, args, mask, per_gpu, frame0, stride, dev, ebn0, nb)
     return out
 
 
-def timed_decodes(torch, sharding, dist, coll_dev, dec, batches, outs, steps, warmup, stream):
+def timed_decodes(torch, sharding, dist, coll_dev, dec, batches, outs, steps, warmup, stream, settle_s=0.0):
     """Warm-up, then `steps` back-to-back decode launches on one stream cycling through the
     resident batches, bracketed by a barrier + synchronize and by one HIP event pair on the
     launch stream (per-step event records would add ~5 us of stream markers to every step).
+    settle_s: before the warm-up, untimed decodes for this long, so that the timed steps see
+    the GPU clock of a continuous stream of batches and not its ramp out of idle.
     Returns (wall seconds, mean ms per launch from the events), both max over ranks."""
     nb = len(batches)
+    t_end = time.perf_counter() + settle_s
+    i = 0
+    while time.perf_counter() < t_end:
+        for _ in range(8):
+            dec.decode(batches[i % nb][0], outs[i % nb], stream)
+            i += 1
+        torch.cuda.synchronize()
     for i in range(warmup):
         dec.decode(batches[i % nb][0], outs[i % nb], stream)
     torch.cuda.synchronize()
@@ -200,6 +209,80 @@ def timed_decodes(torch, sharding, dist, coll_dev, dec, batches, outs, steps, wa
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / steps
     return sharding.max_over_ranks([elapsed, kern_ms], dist, coll_dev)
+
+
+# Secondary entries of the same JSON line (BASELINE.json configs[2] and [4]): timed in the same
+# process after the headline C2 region, each with its own roofline and a 4-frame oracle check.
+# name: (mask, frames per GPU or None = the 512-frame C5 batch sharded over the ranks, note)
+SECONDARY = (
+    ("c3", "frozen_n_65536_k_32768", 4096, "BASELINE configs[2]: N=65536 K=32768, 4096-frame batch per GPU"),
+    ("c5", "frozen_n_262144_k_131072", None, "BASELINE configs[4]: N=262144 K=131072, 512 frames sharded over the GPUs"),
+    ("c5_share64", "frozen_n_262144_k_131072", 64,
+     "C5's 8-GPU share (64 frames) on one GPU: the per-GPU latency of configs[4] at 8 GPUs"),
+)
+
+
+def roofline_entry(name, N, per_gpu, kern_ms):
+    """HBM roofline of one decode launch sequence: algorithmic bytes (1.125 N per frame) over
+    the event-timed kernel time; traffic from the committed PMC summary of the same workload."""
+    bytes_per_launch = 1.125 * N * per_gpu
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src, prof = None, None, None
+    prof_path = TRAFFIC_PROFILES.get((name, per_gpu))
+    if prof_path and os.path.exists(prof_path):
+        with open(prof_path) as f:
+            prof = json.load(f)
+        if "hbm_read_bytes_corrected" in prof and "hbm_write_bytes" in prof:
+            traffic = prof["hbm_read_bytes_corrected"] + prof["hbm_write_bytes"]
+            traffic_src = os.path.relpath(prof_path, ROOT)
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+            "traffic_source": traffic_src, "kernel_ms": kern_ms,
+            "algorithmic_bytes_per_launch": bytes_per_launch}, prof
+
+
+def secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mask_name, per_gpu, note, rank, world, dev,
+                    stream):
+    """One secondary configuration: resident rotated C-sim batches, a short timed loop (same
+    barrier / synchronize / max-over-ranks bracket as the headline), roofline, and a 4-frame
+    bit-exact check against the oracle on rank 0."""
+    import util
+    mask = util.mask(mask_name)
+    N, K = mask.size, int(mask.sum())
+    if per_gpu is None:
+        per_gpu = sharding.shard_bounds(512, world, rank)[1]
+    counts = [per_gpu]
+    if dist is not None:
+        t = torch.zeros(world, dtype=torch.float64, device=coll_dev)
+        t[rank] = per_gpu
+        dist.all_reduce(t)
+        counts = [int(v) for v in t.tolist()]
+    frame0 = int(sum(counts[:rank]))
+    dec = pkg.Decoder(mask)
+    dec.prepare(per_gpu)
+    nb = max(1, min(8, -(-ROTATE_BYTES // (per_gpu * N))))
+    batches = make_batches(pkg, torch, args, mask, per_gpu, frame0, sum(counts), dev, args.ebn0, nb)
+    outs = [torch.empty((per_gpu, dec.words), dtype=torch.int64, device=dev) for _ in range(nb)]
+    steps = max(3, min(args.steps, 20))
+    warm = 3
+    elapsed, kern_ms = timed_decodes(torch, sharding, dist, coll_dev, dec, batches, outs, steps, warm, stream)
+    frames_all = int(sum(counts))
+    ent = {"workload": note, "mask": mask_name, "N": N, "K": K, "frames_per_gpu": per_gpu,
+           "frames_all_ranks": frames_all, "steps": steps, "warmup": warm, "rotated_batches": nb,
+           "ms_per_step": elapsed / steps * 1e3, "info_bits_per_s": frames_all * steps / elapsed * K,
+           "frames_per_sec": frames_all * steps / elapsed, "kernel": kernel_name(dec.stats)}
+    ent["roofline"], _ = roofline_entry(mask_name, N, per_gpu, kern_ms)
+    if rank == 0 and args.check > 0:
+        from oracle import oracle
+        last = (steps - 1) % nb
+        nchk = min(4, per_gpu)
+        got = pkg.unpack_bits(outs[last][:nchk].cpu().numpy(), N)
+        ref = oracle.decode_fsm(mask, batches[last][0][:nchk].cpu().numpy())
+        ent["parity_check"] = {"frames": nchk, "bit_exact": bool((got == ref).all())}
+    dec.close()
+    del batches, outs
+    torch.cuda.empty_cache()
+    return ent
 
 
 def time_scatter_gather(torch, pkg, sharding, dist, dec, mask, total, rank, dev, cdev, args):
@@ -259,6 +342,11 @@ def main():
                          "%d MB, so the inputs do not sit in the Infinity Cache)" % (ROTATE_BYTES >> 20))
     ap.add_argument("--no-ebn0-sweep", dest="ebn0_sweep", action="store_false",
                     help="skip the Eb/N0 {1, 2.5, 4} dB sweep of the timed loop")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false",
+                    help="skip the C3 / C5 / C5-share entries timed after the headline region")
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="untimed decodes before the warm-up so that the timed steps run at the clock of "
+                         "a continuous stream (reported as settle_ms)")
     ap.add_argument("--io", choices=["resident", "scatter"], default="resident",
                     help="scatter: also time the C4 flow -- rank 0 holds the whole batch in HBM, "
                          "RCCL scatters the LLR shards, every rank decodes, RCCL gathers x^ to rank 0 "
@@ -320,7 +408,9 @@ def main():
     torch.cuda.synchronize()
 
     elapsed, kern_ms = timed_decodes(torch, sharding, dist, coll_dev, dec, batches, outs, args.steps, args.warmup,
-                                     stream)
+                                     stream, settle_s=args.settle_ms * 1e-3)
+    # the CPU baseline decodes the head of the first resident batch (the GPU run's own LLRs)
+    cpu_llr = batches[0][0][: max(8, min(4096, int(2 ** 22 // N)))].cpu().numpy() if rank == 0 else None
     if dist is not None:   # frames decoded by all ranks (shards may differ by a few frames)
         cnt = torch.tensor([per_gpu], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(cnt)
@@ -391,17 +481,20 @@ def main():
             del bs
         torch.cuda.synchronize()
 
+    secondary = None
+    if args.secondary and args.config == "c2" and not args.batch:
+        secondary = {}
+        for key, mname, pg, note in SECONDARY:
+            if key == "c5_share64" and world != 1:
+                continue   # at 8 GPUs the c5 entry already is the 64-frame share
+            secondary[key] = secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mname, pg, note, rank,
+                                             world, dev, stream)
+
     if rank == 0:
-        bytes_per_launch = 1.125 * N * per_gpu
-        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src, valu = None, None, None
+        roof, prof = roofline_entry(name, N, per_gpu, kern_ms)
         prof_path = TRAFFIC_PROFILES.get((name, per_gpu))
-        if prof_path and os.path.exists(prof_path):
-            with open(prof_path) as f:
-                prof = json.load(f)
-            if "hbm_read_bytes_corrected" in prof and "hbm_write_bytes" in prof:
-                traffic = prof["hbm_read_bytes_corrected"] + prof["hbm_write_bytes"]
-                traffic_src = os.path.relpath(prof_path, ROOT)
+        valu = None
+        if prof is not None:
             if "valu_insts_per_wave" in prof:
                 # supplementary: the bound that actually limits this kernel
                 simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
@@ -437,12 +530,10 @@ def main():
             "config": {"workload": desc, "N": N, "K": K, "frames_per_gpu": per_gpu,
                        "mask": name, "parallelism": "frames sharded, dp%d" % world,
                        "rotated_batches": nb, "rotated_bytes": nb * per_gpu * N},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
-                         "traffic_source": traffic_src,
-                         "kernel": kernel_name(dec.stats), "kernel_ms": kern_ms,
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
+            "roofline": dict(roof, kernel=kernel_name(dec.stats)),
             "valu_roofline": valu,
+            "settle_ms": args.settle_ms,
+            "secondary": secondary,
             "scatter_gather": scatter_res,
             "ebn0_sweep": sweep,
             "frame_error_rate": fer,
@@ -466,7 +557,7 @@ def main():
                                       "(%.1f MB in, %.1f MB out), copies + decode, synchronous"
                                       % (per_gpu, per_gpu * N / 1e6, per_gpu * dec.words * 8 / 1e6)}
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(mask, args.cpu_seconds, args.ebn0)
+            res["cpu_baseline"] = cpu_baseline(mask, args.cpu_seconds, args.ebn0, cpu_llr)
         print(json.dumps(res))
     if dist is not None:
         dist.destroy_process_group()

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define POLAR_SC_ABI_VERSION 2
+#define POLAR_SC_ABI_VERSION 3
 #define POLAR_SC_PAR 16
 
 /*
@@ -65,6 +65,27 @@ typedef struct polar_sc_config {
                                rejects |llr| > 2^(llr_bits-1) - 1 with -EINVAL (the device
                                entry point never validates).               default 0 */
 } polar_sc_config;
+
+/* Kernel selection and launch shape of a plan (all zero = automatic, what
+ * polar_sc_plan_create uses). The decode result never depends on these; they exist for tests
+ * and measurements. The generated kernels depend only on the mask, the config and this
+ * struct (never on the environment). Out-of-range values -> -EINVAL. */
+typedef struct polar_sc_tuning {
+    int32_t kernel;           /* 0 = automatic; 1 = the schedule interpreter for every N
+                                 (no per-mask / generated-subtree code) */
+    int32_t waves_per_group;  /* interpreter / hybrid launches: waves per 8-frame group, 0 =
+                                 automatic (more when the batch cannot fill the GPU), else 1,
+                                 2, 4, 8 or 16 (capped at the hybrid kernel's bound) */
+    int32_t sub_words;        /* hybrid plans: generated subtree size in 16-LLR words, 0 =
+                                 automatic (64, 128 from N = 32768), else a power of two 2..128 */
+    int32_t tier_words;       /* hybrid HBM-scratch plans: F / G records of >= this many words
+                                 run as grid launches; 0 = automatic, -1 = no grid tier */
+    int32_t lds_slots;        /* HBM-scratch plans: stage slots held in LDS, 0 = automatic,
+                                 else 256, 512 or 1024 */
+    int32_t hybrid_waves;     /* hybrid plans: waves per group of the kernel's launch bound,
+                                 0 = automatic (8), else 4 or 8 */
+    int32_t reserved[2];      /* must be 0 */
+} polar_sc_tuning;
 
 /* Immutable decode plan: N, config, frozen mask, compiled decode schedule and its device
  * copy. Safe to share between threads. Decode calls on different streams may overlap for
@@ -158,6 +179,9 @@ int polar_sc_default_config(polar_sc_config *cfg);
  * touch the GPU (the schedule is uploaded on the first device decode). */
 int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_mask,
                          const polar_sc_config *cfg);
+/* Same with explicit kernel selection (tun == NULL: automatic, as polar_sc_plan_create). */
+int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *info_mask,
+                               const polar_sc_config *cfg, const polar_sc_tuning *tun);
 int polar_sc_plan_destroy(polar_sc_plan *plan);
 
 /* Decode `batch` frames already resident on the current HIP device.
@@ -215,8 +239,8 @@ int polar_sc_plan_get_schedule(const polar_sc_plan *plan, polar_sc_op *ops, uint
 
 /* Per-mask kernel (plans with stats.storage == 2, N <= 1024): generate its HIP source and
  * compile it for gfx950 with hipRTC now (host only, no GPU needed); otherwise it is built
- * on the first decode. -ENOTSUP for plans that use the schedule interpreter. The
- * environment variable POLAR_SC_JIT=0 at plan creation selects the interpreter. */
+ * on the first decode. -ENOTSUP for plans that use the hipcc-built schedule interpreter
+ * (polar_sc_tuning.kernel = 1). */
 int polar_sc_plan_compile(const polar_sc_plan *plan);
 
 /* The generated per-mask kernel source (NUL-terminated, truncated to cap); *len = full size. */

@@ -22,7 +22,7 @@ from . import _build
 
 __all__ = [
     "Decoder", "PolarError", "load_frozen_tab", "load_mask_file", "unpack_bits", "pack_bits",
-    "default_config", "lib", "selftest_lanes", "OPS", "build", "csim_sigma", "csim_states", "csim_frames",
+    "default_config", "make_tuning", "lib", "selftest_lanes", "OPS", "build", "csim_sigma", "csim_states", "csim_frames",
     "count_errors",
 ]
 
@@ -52,6 +52,27 @@ class polar_sc_config(ctypes.Structure):
         "elag_spc", "elag_rep2", "elag_spc2", "elag_rare", "elag_h0", "strict_llr")]
 
 
+class polar_sc_tuning(ctypes.Structure):
+    """Kernel selection / launch shape of a plan (include/polar_sc.h); all 0 = automatic."""
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "kernel", "waves_per_group", "sub_words", "tier_words", "lds_slots", "hybrid_waves")] + [
+        ("reserved", ctypes.c_int32 * 2)]
+
+
+def make_tuning(tuning):
+    """dict (field -> int; kernel may be "auto" / "interp") or polar_sc_tuning or None."""
+    if tuning is None or isinstance(tuning, polar_sc_tuning):
+        return tuning
+    t = polar_sc_tuning()
+    for k, v in dict(tuning).items():
+        if k == "kernel" and isinstance(v, str):
+            v = {"auto": 0, "interp": 1}[v]
+        if k not in [f for f, _ in polar_sc_tuning._fields_ if f != "reserved"]:
+            raise KeyError("unknown tuning field %r" % k)
+        setattr(t, k, int(v))
+    return t
+
+
 class polar_sc_op(ctypes.Structure):
     _fields_ = [("code", ctypes.c_int32), ("level", ctypes.c_int32), ("n", ctypes.c_int32),
                 ("pos", ctypes.c_int32), ("upos", ctypes.c_int32), ("fb", ctypes.c_uint32),
@@ -76,7 +97,8 @@ class polar_sc_plan_stats(ctypes.Structure):
 
 # exported symbols of include/polar_sc.h (tests check that the library exports all of them)
 EXPORTS = (
-    "polar_sc_default_config", "polar_sc_plan_create", "polar_sc_plan_destroy", "polar_sc_decode",
+    "polar_sc_default_config", "polar_sc_plan_create", "polar_sc_plan_create_tuned", "polar_sc_plan_destroy",
+    "polar_sc_decode",
     "polar_sc_decode_u16", "polar_sc_plan_prepare", "polar_sc_decode_host", "polar_load_frozen_tab",
     "polar_load_mask_file", "polar_codeword_to_info", "polar_sc_plan_get_stats",
     "polar_sc_plan_get_schedule", "polar_sc_selftest_lanes", "polar_sc_strerror",
@@ -102,6 +124,7 @@ def lib():
     sig = {
         "polar_sc_default_config": [p],
         "polar_sc_plan_create": [ctypes.POINTER(p), u32, p, p],
+        "polar_sc_plan_create_tuned": [ctypes.POINTER(p), u32, p, p, p],
         "polar_sc_plan_destroy": [p],
         "polar_sc_decode": [p, p, p, sz, p],
         "polar_sc_decode_u16": [p, p, p, sz, p],
@@ -238,24 +261,27 @@ class Decoder:
 
     info_mask: (N,) array, nonzero = information bit (frozen-table bit 1).
     config:    polar_sc_config or None (reference config.h); other configs -> ENOTSUP.
+    tuning:    polar_sc_tuning, a dict of its fields, or None (automatic kernel selection).
     """
 
-    def __init__(self, info_mask=None, config=None):
+    def __init__(self, info_mask=None, config=None, tuning=None):
         self._plan = ctypes.c_void_p(None)
         self.N = 0
         if info_mask is not None:
-            self.load_frozen_bits(info_mask, config)
+            self.load_frozen_bits(info_mask, config, tuning)
 
     # -- FB port ---------------------------------------------------------------------------
-    def load_frozen_bits(self, info_mask, config=None):
+    def load_frozen_bits(self, info_mask, config=None, tuning=None):
         mask = np.ascontiguousarray(np.asarray(info_mask).astype(np.uint8) != 0, dtype=np.uint8)
         if mask.ndim != 1:
             raise ValueError("info_mask must be 1-D")
         self.close()
         plan = ctypes.c_void_p(None)
         cfg = ctypes.byref(config) if config is not None else None
-        _check("polar_sc_plan_create",
-               lib().polar_sc_plan_create(ctypes.byref(plan), int(mask.size), _np_ptr(mask), cfg))
+        tun = make_tuning(tuning)
+        _check("polar_sc_plan_create_tuned",
+               lib().polar_sc_plan_create_tuned(ctypes.byref(plan), int(mask.size), _np_ptr(mask), cfg,
+                                                ctypes.byref(tun) if tun is not None else None))
         self._plan = plan
         self.mask = mask
         self.N = int(mask.size)

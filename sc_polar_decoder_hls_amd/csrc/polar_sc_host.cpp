@@ -124,17 +124,17 @@ struct SubCtx {
 // flush). The subtree's ops are contiguous in the schedule and touch only bits of their own
 // subtree; the ops of larger nodes run after the flush and use the HBM copy. The exported
 // schedule (polar_sc_plan_get_schedule) stays the plain one.
-void window_schedule(polar_sc_plan &p, const std::vector<polar_sc_op> &ops)
+void window_schedule(const polar_sc_plan &p, const std::vector<polar_sc_op> &ops, std::vector<polar_sc_op> &dev)
 {
     const int W = p.lds_slots;
-    p.dev_ops.clear();
+    dev.clear();
     int cur = -1;
     auto mark = [&](int code, int pos) {
         polar_sc_op o{};
         o.code = code;
         o.pos = pos;
         o.upos = -1;
-        p.dev_ops.push_back(o);
+        dev.push_back(o);
     };
     for (const polar_sc_op &op : ops) {
         int win = -1;
@@ -153,7 +153,7 @@ void window_schedule(polar_sc_plan &p, const std::vector<polar_sc_op> &ops)
         }
         polar_sc_op o = op;
         o.reserved[0] = win >= 0 ? 1 : 0;
-        p.dev_ops.push_back(o);
+        dev.push_back(o);
     }
 }
 
@@ -409,16 +409,30 @@ bool default_format(const polar_sc_config &c)
     return c.sigmag == 1 && c.par == 16 && c.extended == 1 && c.llr_bits <= 8;
 }
 
+bool tuning_valid(const polar_sc_tuning &t)
+{
+    auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+    return (t.kernel == 0 || t.kernel == 1) && (t.waves_per_group == 0 || (pow2(t.waves_per_group) && t.waves_per_group <= 16)) &&
+           (t.sub_words == 0 || (pow2(t.sub_words) && t.sub_words >= 2 && t.sub_words <= 128)) &&
+           t.tier_words >= -1 && (t.tier_words <= 0 || pow2(t.tier_words)) &&
+           (t.lds_slots == 0 || t.lds_slots == 256 || t.lds_slots == 512 || t.lds_slots == 1024) &&
+           (t.hybrid_waves == 0 || t.hybrid_waves == 4 || t.hybrid_waves == 8) && t.reserved[0] == 0 &&
+           t.reserved[1] == 0;
+}
+
 int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
 
 // device state for the current device: schedule upload (+ scratch for `batch` frames)
-// interp: also upload the interpreter schedule of a per-mask plan (the per-op monitor runs
-// the schedule interpreter for those)
+// mode DEV_DECODE: the plan's decode kernel; DEV_TRACE: also the interpreter schedule of a
+// per-mask plan (the per-op monitor runs the schedule interpreter for those); DEV_I16: only
+// what the int16-channel interpreter needs (schedule, scratch), no per-mask / hybrid module
 // held: if non-null, receives the plan lock (still held on success) so that the caller can
 // launch with the scratch pointer it was given before another thread may reallocate it
-int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool interp = false,
+enum DevMode { DEV_DECODE, DEV_TRACE, DEV_I16 };
+int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, DevMode mode = DEV_DECODE,
                   std::unique_lock<std::mutex> *held = nullptr)
 {
+    const bool interp = mode != DEV_DECODE;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -EIO;
     std::unique_lock<std::mutex> lk(p->mu);
@@ -428,7 +442,7 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool int
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
         st.simds = 4 * cus;
     }
-    if (p->jit || p->hybrid) {
+    if ((p->jit || p->hybrid) && mode != DEV_I16) {
         int rc = polar_host::jit_load(*p, st);
         if (rc) return rc;
         if (p->jit && !interp) {
@@ -447,6 +461,13 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool int
         size_t bytes = dops.size() * sizeof(polar_sc_op);
         if (hipMalloc(&st.ops, bytes) != hipSuccess) return -ENOMEM;
         if (hipMemcpy(st.ops, dops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+    }
+    if (mode == DEV_I16 && !p->ops16.empty() && !st.ops16) {
+        std::vector<polar_sc_op> dops = p->ops16;
+        dops.push_back(dops.back());
+        const size_t bytes = dops.size() * sizeof(polar_sc_op);
+        if (hipMalloc(&st.ops16, bytes) != hipSuccess) return -ENOMEM;
+        if (hipMemcpy(st.ops16, dops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
     }
     for (size_t t = 0; t < p->tiers.size() && t < 2; t++) {
         if (st.seg_ops[t]) continue;
@@ -476,14 +497,10 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, bool int
 
 // Interpreter launches: waves per 8-frame group. Large batches keep one wave per group;
 // when the groups cannot fill the GPU (about 2 waves per SIMD), a group gets up to 16 waves
-// that split its wide ops (polar_sc_kernels.hip). POLAR_SC_WAVES_PER_GROUP overrides.
+// that split its wide ops (polar_sc_kernels.hip). polar_sc_tuning.waves_per_group fixes it.
 int waves_per_group(const polar_sc_plan *p, size_t batch, int simds)
 {
-    const char *env = std::getenv("POLAR_SC_WAVES_PER_GROUP");
-    if (env && *env) {
-        int w = std::atoi(env);
-        if (w >= 1 && w <= 16 && (w & (w - 1)) == 0) return p->hybrid && w > p->hybrid_waves ? p->hybrid_waves : w;
-    }
+    if (const int w = p->tune.waves_per_group) return p->hybrid && w > p->hybrid_waves ? p->hybrid_waves : w;
     const int wmax = p->hybrid ? p->hybrid_waves : 16;
     const size_t groups = (batch + 7) / 8;
     const size_t target = 2u * (size_t)(simds > 0 ? simds : 1024);
@@ -503,7 +520,7 @@ int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size
     // another thread reallocates the scratch only after this launch has been queued (and
     // synchronises the device before freeing it)
     std::unique_lock<std::mutex> held;
-    int rc = ensure_device(p, batch, &st, false, p->gmem ? &held : nullptr);
+    int rc = ensure_device(p, batch, &st, DEV_DECODE, p->gmem ? &held : nullptr);
     if (rc) return rc;
     if (p->jit) return polar_host::jit_launch(*p, *st, llr, out, (long)batch, out_stride, stream);
     const int wpg = waves_per_group(p, batch, st->simds);
@@ -528,7 +545,7 @@ int trace_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size_
     if (!recs) return 0;
     DevState *st = nullptr;
     std::unique_lock<std::mutex> held;
-    int rc = ensure_device(p, batch, &st, true, &held);
+    int rc = ensure_device(p, batch, &st, DEV_TRACE, &held);
     if (rc) return rc;
     const size_t slots = dops.size() + 3;
     unsigned long long *dtrace = nullptr;
@@ -625,12 +642,21 @@ int polar_sc_default_config(polar_sc_config *cfg)
 int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_mask,
                          const polar_sc_config *cfg)
 {
+    return polar_sc_plan_create_tuned(out, N, info_mask, cfg, nullptr);
+}
+
+int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *info_mask,
+                               const polar_sc_config *cfg, const polar_sc_tuning *tun)
+{
     if (!out || !info_mask) return -EINVAL;
     *out = nullptr;
     if (N < 32 || N > (1u << 20) || (N & (N - 1)) != 0) return -EINVAL;
     polar_sc_config c;
     if (cfg) c = *cfg; else polar_sc_default_config(&c);
     if (!config_supported(c)) return -ENOTSUP;
+    polar_sc_tuning t{};
+    if (tun) t = *tun;
+    if (!tuning_valid(t)) return -EINVAL;
 
     if (N < 2u * (uint32_t)c.par) return -EINVAL;   // INIT needs N_DIV >= 2 (my_module.h:294-309)
 
@@ -642,6 +668,7 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     p->p16 = c.par >= 16 ? (uint32_t)c.par / 16 : 1u;
     p->ppw = c.par < 16 ? 16u / (uint32_t)c.par : 1u;
     p->cfg = c;
+    p->tune = t;
     p->mask.resize(N);
     p->fbp.resize(p->GP);
     p->type.resize(p->GP);
@@ -682,13 +709,12 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         // plus an LDS window for the partial sums of the current 128-word subtree
         // the LDS region W: 256 slots, 512 from N = 32768 and 1024 from N = 131072 when the
         // LDS slots hold 8-bit pairs (PAR 16, LLR_BITS <= 8: 78 KB per group = two groups per
-        // CU at W = 512, 150 KB = one at 1024); POLAR_SC_LDS_SLOTS overrides
+        // CU at W = 512, 150 KB = one at 1024); polar_sc_tuning.lds_slots overrides
         const bool lds8 = c.par <= 16 && c.llr_bits <= 8;
         int W = LDS_LOW_SLOTS;
         if (lds8 && p->G >= 8192) W = 1024;
         else if (lds8 && p->G >= 2048) W = 512;
-        if (const char *e = std::getenv("POLAR_SC_LDS_SLOTS")) {
-            const int w = *e ? std::atoi(e) : 0;
+        if (const int w = t.lds_slots) {
             if ((w == 256 || (lds8 && (w == 512 || w == 1024))) && (uint32_t)w <= p->G / 2) W = w;
         }
         p->lds_slots = W;
@@ -705,10 +731,9 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     }
     while ((1u << p->lg) < p->G) p->lg++;
     // per-mask register kernel for N <= 1024; above, the hybrid kernel (interpreter + generated
-    // subtree decoders of POLAR_SC_SUB_WORDS words, default 64 / 128). POLAR_SC_JIT=0
+    // subtree decoders of sub_words words, default 64 / 128). polar_sc_tuning.kernel = 1
     // selects the plain schedule interpreter for every N.
-    const char *jit_env = std::getenv("POLAR_SC_JIT");
-    const bool jit_on = !(jit_env && jit_env[0] == '0');
+    const bool jit_on = t.kernel != 1;
     // PRUNING_LEVEL 1 leaf decoders other than the plain leaf run on the interpreter only
     bool kinds = false;
     for (const polar_sc_op &o : p->ops)
@@ -721,9 +746,7 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
     // 1.48; 248 VGPRs, no spills, at most 2 waves per SIMD -- below N = 32768 the smaller
     // subtrees keep 3)
     int sub_words = p->G >= 2048 ? 128 : 64;
-    if (const char *e = std::getenv("POLAR_SC_SUB_WORDS")) {
-        if (*e) sub_words = std::atoi(e);
-    }
+    if (t.sub_words) sub_words = t.sub_words;
     const bool sub_ok = sub_words >= 2 && sub_words <= 128 && (sub_words & (sub_words - 1)) == 0;
     std::vector<polar_sc_op> dev_sched;
     if (!p->jit && jit_on && !kinds && dflt && sub_ok && (uint32_t)sub_words < p->G) {
@@ -732,11 +755,7 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
         compile_node(*p, dev_sched, 0, 0, p->GP, true, &sc);
         emit(dev_sched, POLAR_OP_END, 0, 0, 0, -1, 0);
         p->hybrid = 1;
-        p->hybrid_waves = polar_host::HYBRID_MAX_WAVES;
-        if (const char *e = std::getenv("POLAR_SC_HYBRID_WAVES")) {
-            const int w = std::atoi(e);
-            if (w == 4 || w == 8) p->hybrid_waves = w;
-        }
+        p->hybrid_waves = t.hybrid_waves ? t.hybrid_waves : polar_host::HYBRID_MAX_WAVES;
         p->sub_words = sub_words;
         p->subs = std::move(sc.lists);
         s.sub_words = (uint32_t)sub_words;
@@ -752,16 +771,23 @@ int polar_sc_plan_create(polar_sc_plan **out, uint32_t N, const uint8_t *info_ma
             p->hybrid_waves = polar_host::HYBRID_MAX_WAVES;
         }
     }
-    if (p->gmem) window_schedule(*p, dev_sched);
+    if (p->gmem) window_schedule(*p, dev_sched, p->dev_ops);
     else if (p->hybrid) p->dev_ops = dev_sched;
+    // int16 channel (polar_sc_decode_i16): the interpreter has no generated subtrees, so it
+    // runs the plan's schedule without OP_SUB records
+    if (!p->subs.empty()) {
+        if (p->gmem) window_schedule(*p, p->ops, p->ops16);
+        else p->ops16 = p->ops;
+    }
     // grid tier for the upper levels of large hybrid plans (N >= 65536): the deep cut at F / G
     // records of >= 1024 output words (nodes of 32768+ LLRs), and the root alone. Measured on
     // one box: C5 (64 groups) 4.68 ms deep vs 4.90 root-only; C3 (512 groups, every CU busy
-    // either way) 1.53 ms root-only vs 1.59 deep. POLAR_SC_TIER_WORDS fixes one cut (0 = off).
-    if (p->gmem && p->hybrid && p->sub_words > 0) {
+    // either way) 1.53 ms root-only vs 1.59 deep. polar_sc_tuning.tier_words fixes one cut
+    // (-1 = none).
+    if (p->gmem && p->hybrid && p->sub_words > 0 && t.tier_words >= 0) {
         std::vector<int> cuts;
-        if (const char *e = std::getenv("POLAR_SC_TIER_WORDS"); e && *e) {
-            cuts.push_back(std::atoi(e));
+        if (t.tier_words > 0) {
+            cuts.push_back(t.tier_words);
         } else if (p->G >= 4096) {
             cuts.push_back(1024);
             if ((int)p->G / 2 != 1024) cuts.push_back((int)p->G / 2);
@@ -799,6 +825,7 @@ int polar_sc_plan_destroy(polar_sc_plan *p)
         if (kv.second.module) (void)hipModuleUnload(kv.second.module);
         if (kv.second.imodule) (void)hipModuleUnload(kv.second.imodule);
         if (kv.second.module16) (void)hipModuleUnload(kv.second.module16);
+        if (kv.second.ops16) (void)hipFree(kv.second.ops16);
         if (kv.second.scratch) (void)hipFree(kv.second.scratch);
     }
     if (have_dev && !p->dev.empty()) (void)hipSetDevice(cur);
@@ -839,15 +866,17 @@ int polar_sc_decode_i16(const polar_sc_plan *p, const int16_t *llr_dev, uint64_t
     if (batch > (size_t)0x7FFFFFF8) return -EINVAL;
     DevState *st = nullptr;
     std::unique_lock<std::mutex> held;
-    int rc = ensure_device(p, batch, &st, true, &held);
+    int rc = ensure_device(p, batch, &st, DEV_I16, &held);
     if (rc) return rc;
     rc = polar_host::jit_load16(*p, *st);
     if (rc) return rc;
     int wpg = waves_per_group(p, batch, st->simds);
     if (wpg > polar_host::HYBRID_MAX_WAVES) wpg = polar_host::HYBRID_MAX_WAVES;
     const int stride16 = (int)(4 * ((p->G + 3) / 4));
+    // hybrid plans: the schedule without generated-subtree records (the int16 interpreter
+    // has none of the plan's subtree decoders)
     return polar_host::launch_interp_fn(st->fn16, *p, *st, (const int8_t *)llr_dev, (uint16_t *)hard_bits_dev,
-                                        (long)batch, stride16, wpg, stream, nullptr);
+                                        (long)batch, stride16, wpg, stream, nullptr, st->ops16 ? st->ops16 : st->ops);
 }
 
 int polar_sc_decode_u16(const polar_sc_plan *p, const int8_t *llr_dev, uint16_t *bits_dev,

@@ -19,6 +19,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -27,34 +28,13 @@
 #include <sstream>
 
 namespace {
-// per-mask kernels: minimum waves per SIMD of the launch bound (the register allocator then
-// targets that occupancy, spilling if it must). Default 4: the persistent batch loop needs
-// ~132 VGPRs at C2 unbounded, and the scheduler then relaxes to 151 (3 waves per SIMD);
-// bounded at 4 it keeps 128 VGPRs with one dword spilled per batch. POLAR_SC_MASK_MIN_WAVES
-// (2..8) overrides, 0 removes the bound.
-std::string mask_min_waves()
-{
-    const char *e = std::getenv("POLAR_SC_MASK_MIN_WAVES");
-    const int w = (e && *e) ? std::atoi(e) : 4;
-    return (w >= 2 && w <= 8) ? ", " + std::to_string(w) : std::string();
-}
-// per-mask kernels: POLAR_SC_MASK_PERSIST=R (>= 1) builds the persistent batch loop and caps
-// the grid at R x the resident blocks; 0 / unset: one 8-frame batch per wave, no loop
-// per-mask kernels: waves per block (POLAR_SC_MASK_WPB 1 / 2 / 4 / 8, default 4); each wave
-// has its own 8-frame batch and LDS stage, so the block size only sets the granularity at
-// which LDS is allocated and released
-int mask_wpb()
-{
-    const char *e = std::getenv("POLAR_SC_MASK_WPB");
-    const int w = (e && *e) ? std::atoi(e) : 4;
-    return (w == 1 || w == 2 || w == 8) ? w : 4;
-}
-int mask_persist()
-{
-    const char *e = std::getenv("POLAR_SC_MASK_PERSIST");
-    const int r = (e && *e) ? std::atoi(e) : 0;
-    return r > 0 ? r : 0;
-}
+// per-mask kernels: waves per block and the launch bound's minimum waves per SIMD. The
+// register allocator targets 4 waves per SIMD (123 VGPRs at C2). Measured alternatives, all
+// slower on the same box and removed: a persistent batch loop (78.9 vs 72.8 us), two batches
+// per wave in straight-line code (80.9 vs 73.6 us), 1 / 2 waves per block (74.2 / 74.7 vs
+// 73.7 us), re-splitting the root from LDS for the root G (77 vs 72 us) -- DESIGN.md 3.1.
+constexpr int MASK_WPB = 4;
+constexpr int MASK_MIN_WAVES = 4;
 }  // namespace
 
 namespace {
@@ -75,16 +55,11 @@ struct Gen {
     // per-mask kernels: the channel words are split once (root_presplit) into m<LG> / s<LG>,
     // so the root ops run on split words like every other level
     bool presplit = false;
-    // per-mask kernels: the root words are dropped after the root F-type op and split again
-    // from the LDS-staged channel for the root G-type op (fewer live registers across the
-    // left half: higher occupancy for about 3 VALU more per root word)
-    bool resplit = false;
     // per-mask kernels: the root magnitudes packed two words per register (bytes of word j
     // and j + G/2 in each 16-bit half): half the root registers for 2 VALU more per root
     // F / G word. C2: 158 -> 126 VGPRs, 3 -> 4 waves per SIMD, 76.7 -> 72.7 / 75.5 us on one
-    // box (POLAR_SC_ROOT_PACK=0 restores the unpacked root)
+    // box
     bool pack = false;
-    bool root_f_done = false;
     Gen(const std::vector<polar_sc_op> &ops_, int lg) : ops(ops_), LG(lg) {}
 
     // Partial sums: u32 bw[max(1, G / 16)], dword j = groups 16 j .. 16 j + 15, low frame in
@@ -168,7 +143,7 @@ struct Gen {
     // registers held across the whole left subtree.
     void clobber_parent(int sd, int n)
     {
-        if (sd == LG && (!presplit || resplit)) return;   // root: channel words are re-read from LDS
+        if (sd == LG && !presplit) return;   // root: channel words are re-read from LDS
         if (pack && sd == LG) {
             for (int i = 0; i < n; i++) o << "  asm volatile(\"\" : \"+v\"(pr[" << i << "]));\n";
         } else {
@@ -249,12 +224,6 @@ struct Gen {
         const int sd = LG - op.level, cd = sd - 1, n = op.n, np = planes(n);
         const bool root = sd == LG && !presplit;
         fence();
-        if (resplit && sd == LG) {
-            const bool gtype = op.code == POLAR_OP_G || op.code == POLAR_OP_GLEAF || op.code == POLAR_OP_R1 ||
-                               op.code == POLAR_OP_SPC;
-            if (gtype && root_f_done) root_presplit(2 * n);
-            if (!gtype) root_f_done = true;
-        }
         if (root && (op.code == POLAR_OP_REP || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC)) root_split(2 * n);
         switch (op.code) {
         case POLAR_OP_F:
@@ -472,50 +441,20 @@ struct Gen {
     {
         const int N = (int)p.N, G = (int)p.G;
         // Channel staging: each wave copies its 8 frames (8 x N bytes, contiguous rows of the
-        // [batch][N] input) into LDS with 16-byte loads, then reads the bytes of its lane
-        // (position 16 w + pl of frames row / row + 4) from there once, into the split root
-        // words (root_presplit). Frame stride N + 16 bytes keeps the four rows of a read in
-        // different banks.
-        //
-        // Persistent waves (jit_launch caps the grid at the blocks that fit on the device at
-        // once): each wave loops over 8-frame batches wave, wave + stride, ... The channel of
-        // the next batch is fetched HBM -> LDS by global_load_lds_dwordx4 (no VGPRs) as soon
-        // as the presplit has read the current one, so its latency hides behind the decode
-        // instead of stalling every wave of the next dispatch round at once.
+        // [batch][N] input) HBM -> LDS with global_load_lds_dwordx4, then reads the bytes of
+        // its lane (position 16 w + pl of frames row / row + 4) from there once, into the split
+        // root words (root_presplit). Frame stride N + 16 bytes keeps the four rows of a read
+        // in different banks. One 8-frame batch per wave; the launch is one wave per batch.
         const int FS = N + 16, LPF = N / 16;   // LDS frame stride, 16-byte chunks (lanes) per frame
+        const int wpb = MASK_WPB;
         presplit = true;
-        {
-            const char *e = std::getenv("POLAR_SC_ROOT_RESPLIT");
-            resplit = e && e[0] == '1';
-            const char *pe = std::getenv("POLAR_SC_ROOT_PACK");
-            pack = !resplit && G >= 2 && !(pe && pe[0] == '0');
-        }
-        // Prefetch in the middle of the decode only where a frame fills all 64 lanes of a load
-        // (N = 1024): shorter frames load under a lane mask, and that branch in the middle of
-        // the straight-line code costs ~40 VGPRs and spills (N = 512); they fetch at the top of
-        // each iteration instead. The resplit variant re-reads the channel, so it fetches at the end.
-        // Off by default (mask_persist): one batch per wave measured faster than the persistent
-        // loop with prefetch (C2 same box: 74.0 vs 79.5 us, tools/gpu_ab_persist.sh), and the
-        // loop alone costs ~10 VGPRs.
-        const int rounds = mask_persist();
-        const bool persist = rounds > 0;
-        p.mask_rounds = rounds;   // the grid cap of this source (0: one batch per wave)
-        const int wpb = mask_wpb();
-        p.mask_wpb = wpb;   // the launch shape of this source (jit_load -> DevState)
-        const bool prefetch = persist && !resplit && LPF >= 64;
-        // Two batches per wave in straight-line code (POLAR_SC_MASK_DUAL=1, N = 1024): the grid
-        // holds half the waves, each decodes batch w and then w + (grid waves), the second
-        // batch's channel prefetched into LDS right after the first one's presplit -- the
-        // persistent loop's overlap without a loop (no loop-carried registers); every frame
-        // index past the batch is clamped and its stores suppressed, so there is no branch.
-        const char *de = std::getenv("POLAR_SC_MASK_DUAL");
-        const bool dual = !persist && !resplit && LPF >= 64 && de && de[0] == '1';
-        p.mask_dual = dual ? 1 : 0;
+        pack = G >= 2;
         o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
           << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
           << "typedef const __attribute__((address_space(1))) void *gas_t;\n"
           << "typedef __attribute__((address_space(3))) void *las_t;\n"
-          << "extern \"C\" __global__ void __launch_bounds__(" << 64 * wpb << mask_min_waves() << ") polar_sc_mask_kernel(\n"
+          << "extern \"C\" __global__ void __launch_bounds__(" << 64 * wpb << ", " << MASK_MIN_WAVES
+          << ") polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
           << "  __shared__ uint4 stage_[" << wpb << " * 8 * " << FS / 16 << "];\n"
           << "  __shared__ unsigned char tabm_[256], tabs_[256];   // channel byte -> |LLR|, sign (qconv_format)\n"
@@ -523,15 +462,14 @@ struct Gen {
           << "    tabm_[t_] = (unsigned char)(v_ & QMAG); tabs_[t_] = (unsigned char)(v_ >> 7); }\n"
           << "  __syncthreads();\n"
           << "  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR batch indices\n"
-          << "  const long nw_ = ((long)batch + 7) / 8, wstride_ = (long)gridDim.x * " << wpb << ";\n"
+          << "  const long nw_ = ((long)batch + 7) / 8;\n"
           << "  long wave = (long)blockIdx.x * " << wpb << " + wib;\n"
           << "  if (wave >= nw_) return;\n"
           << "  unsigned char *st_ = (unsigned char *)stage_ + wib * " << 8 * FS << ";\n"
           << "  const bool al_ = (((unsigned long)llr) & 15u) == 0u;\n"
           << "  const unsigned char *lla_ = (const unsigned char *)((unsigned long)llr & ~15ul);   // 16-byte aligned\n"
           // async HBM -> LDS copy of the 8 frames of batch w, frames past the batch clamped to
-          // the last one (w past the last batch: the last frame 8 times, one 1 KB row that
-          // stays in cache). Uniform frame base (SGPR) + lane offset: one VGPR for all eight
+          // the last one. Uniform frame base (SGPR) + lane offset: one VGPR for all eight
           // loads, and branch-free -- a branch in the middle of the straight-line decode costs
           // the register allocator ~100 VGPRs. lla_: the input rounded down to 16 bytes (an
           // unaligned input is byte-copied instead and the async rows are overwritten).
@@ -547,55 +485,44 @@ struct Gen {
                   << "      __builtin_amdgcn_global_load_lds((gas_t)(lla_ + fr_ * " << N << " + " << ch
                   << " * 16), (las_t)(st_ + " << f * FS + c * 1024 << "), 16, 0, 0); }\n";
             }
-        // Lane-derived values are recomputed in every iteration (the empty asm makes the lane
-        // index loop-variant): hoisted out of the loop they would stay live across the whole
-        // decode (~30 VGPRs, 4 -> 3 waves per SIMD).
+        // Lane-derived values are recomputed after the fetch (the empty asm makes the lane
+        // index opaque): kept from the top they would stay live across the whole decode
+        // (~30 VGPRs, 4 -> 3 waves per SIMD).
         o << "  };\n"
-          << (prefetch || resplit || dual ? "  fetch_(wave, threadIdx.x & 63);\n" : "");
-        for (int k = 0; k < (dual ? 2 : 1); k++) {
-            root_f_done = false;
-            o << (persist ? "  for (; wave < nw_; wave += wstride_) {\n" : "  {\n")
-              << (k == 1 ? "  wave += wstride_;   // second batch of this wave (may be past the last: no stores)\n" : "")
-              << "  int lane = threadIdx.x & 63;\n"
-              << "  asm volatile(\"\" : \"+v\"(lane));\n"
-              << "  const int row = lane >> 4, pl = lane & 15;\n"
-              << "  Lanes ln; ln.init((u32)pl);\n"
-              << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
-              << " + ln.pos;\n"
-              << (prefetch || resplit || dual ? "" : "  fetch_(wave, lane);\n")
-              << "  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this batch's channel is in LDS\n"
-              << "  if (!al_) {   // input not 16-byte aligned: byte copy\n"
-              << "    for (int q = lane; q < " << 8 * N << "; q += 64) {\n"
-              << "      const int f = q / " << N << ", off = q % " << N << ";\n"
-              << "      const long fr = wave * 8 + f < batch ? wave * 8 + f : (long)batch - 1;\n"
-              << "      st_[f * " << FS << " + off] = llr[fr * " << N << " + off];\n"
-              << "    }\n"
-              << "  }\n"
-              << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
-              << "  __builtin_amdgcn_wave_barrier();\n"
-              << "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n"
-              << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
-            stage_arrays(true);
-            root_presplit(G);
-            if (prefetch || (dual && k == 0))   // the staged channel is consumed: prefetch the next batch into it
-                o << "  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the presplit reads are done\n"
-                  << "  __builtin_amdgcn_wave_barrier();\n"
-                  << "  fetch_(wave + wstride_, lane);\n";
-            all_ops();
-            // END (my_module.h:1848-1869) + wrapper_out: x^ words in natural order
-            o << "  const long f_lo = wave * 8 + (lane >> 4), f_hi = f_lo + 4;\n"
-              << "  const bool st_lo = f_lo < batch, st_hi = f_hi < batch;\n"
-              << "  unsigned short *o_lo = out + (size_t)f_lo * out_stride, *o_hi = out + (size_t)f_hi * out_stride;\n";
-            for (int c = 0; c < (G + 15) / 16; c++) {
-                o << "  { const u32 t_ = row_transpose16(to_position_order(" << get16(16 * c) << ", ln), ln); const int w_ = " << 16 * c << " + pl;\n"
-                  << "    if (w_ < " << G << ") { if (st_lo) o_lo[w_] = (unsigned short)(t_ & 0xFFFFu); "
-                  << "if (st_hi) o_hi[w_] = (unsigned short)(t_ >> 16); } }\n";
-            }
-            o << "  for (int w_ = " << G << " + pl; w_ < out_stride; w_ += 16) { if (st_lo) o_lo[w_] = 0; if (st_hi) o_hi[w_] = 0; }\n"
-              << (resplit ? "  if (al_ && wave + wstride_ < nw_) fetch_(wave + wstride_, lane);   // root G re-read the channel\n"
-                          : "")
-              << "  }\n";
+          << "  {\n"
+          << "  int lane = threadIdx.x & 63;\n"
+          << "  asm volatile(\"\" : \"+v\"(lane));\n"
+          << "  const int row = lane >> 4, pl = lane & 15;\n"
+          << "  Lanes ln; ln.init((u32)pl);\n"
+          << "  const unsigned char *chl = st_ + row * " << FS << " + ln.pos, *chh = st_ + (row + 4) * " << FS
+          << " + ln.pos;\n"
+          << "  fetch_(wave, lane);\n"
+          << "  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this batch's channel is in LDS\n"
+          << "  if (!al_) {   // input not 16-byte aligned: byte copy\n"
+          << "    for (int q = lane; q < " << 8 * N << "; q += 64) {\n"
+          << "      const int f = q / " << N << ", off = q % " << N << ";\n"
+          << "      const long fr = wave * 8 + f < batch ? wave * 8 + f : (long)batch - 1;\n"
+          << "      st_[f * " << FS << " + off] = llr[fr * " << N << " + off];\n"
+          << "    }\n"
+          << "  }\n"
+          << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
+          << "  __builtin_amdgcn_wave_barrier();\n"
+          << "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n"
+          << "  u32 bw[" << (G >= 16 ? G / 16 : 1) << "] = {};\n";
+        stage_arrays(true);
+        root_presplit(G);
+        all_ops();
+        // END (my_module.h:1848-1869) + wrapper_out: x^ words in natural order
+        o << "  const long f_lo = wave * 8 + (lane >> 4), f_hi = f_lo + 4;\n"
+          << "  const bool st_lo = f_lo < batch, st_hi = f_hi < batch;\n"
+          << "  unsigned short *o_lo = out + (size_t)f_lo * out_stride, *o_hi = out + (size_t)f_hi * out_stride;\n";
+        for (int c = 0; c < (G + 15) / 16; c++) {
+            o << "  { const u32 t_ = row_transpose16(to_position_order(" << get16(16 * c) << ", ln), ln); const int w_ = " << 16 * c << " + pl;\n"
+              << "    if (w_ < " << G << ") { if (st_lo) o_lo[w_] = (unsigned short)(t_ & 0xFFFFu); "
+              << "if (st_hi) o_hi[w_] = (unsigned short)(t_ >> 16); } }\n";
         }
+        o << "  for (int w_ = " << G << " + pl; w_ < out_stride; w_ += 16) { if (st_lo) o_lo[w_] = 0; if (st_hi) o_hi[w_] = 0; }\n"
+          << "  }\n";
         o << "}\n";
         return o.str();
     }
@@ -669,22 +596,6 @@ namespace {
 // once on the build host and the cache travels with the in-tree library.
 const char *const kRtcOpts[] = {"--gpu-architecture=gfx950", "-O3", "-std=c++17"};
 
-// POLAR_SC_RTC_EXTRA: extra hipRTC options, separated by spaces or commas (e.g.
-// "-mllvm,-amdgpu-sched-strategy=max-ilp"), for compiler A/Bs; part of the cache key
-std::vector<std::string> rtc_extra()
-{
-    std::vector<std::string> v;
-    const char *e = std::getenv("POLAR_SC_RTC_EXTRA");
-    if (!e) return v;
-    std::string t(e);
-    for (char &ch : t)
-        if (ch == ',') ch = ' ';   // commas separate too (shell-friendly)
-    std::istringstream in(t);
-    std::string w;
-    while (in >> w) v.push_back(w);
-    return v;
-}
-
 uint64_t fnv1a(uint64_t h, const char *s, size_t n)
 {
     for (size_t i = 0; i < n; i++) {
@@ -713,7 +624,6 @@ std::string cache_path(const std::string &src)
     h = fnv1a(h, kPolarDeviceSrc, sizeof kPolarDeviceSrc);
     h = fnv1a(h, kPolarInterpSrc, sizeof kPolarInterpSrc);
     for (const char *o : kRtcOpts) h = fnv1a(h, o, std::strlen(o) + 1);
-    for (const std::string &o : rtc_extra()) h = fnv1a(h, o.c_str(), o.size() + 1);
     int ver_major = 0, ver_minor = 0;
     hiprtcVersion(&ver_major, &ver_minor);
     h = fnv1a(h, (const char *)&ver_major, sizeof ver_major);
@@ -739,7 +649,10 @@ void cache_store(const std::string &path, const std::vector<char> &code)
     if (path.empty()) return;
     const size_t slash = path.rfind('/');
     (void)mkdir(path.substr(0, slash).c_str(), 0755);
-    const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
+    // unique per process and call: prewarm compiles from several threads, and two of them may
+    // store the same key
+    static std::atomic<unsigned> seq{0};
+    const std::string tmp = path + ".tmp." + std::to_string((long)getpid()) + "." + std::to_string(seq++);
     {
         std::ofstream f(tmp, std::ios::binary);
         if (!f) return;
@@ -760,10 +673,7 @@ int rtc_compile(const std::string &src, std::vector<char> &code, std::string &lo
     const char *hdrs[] = {kPolarDeviceSrc, kPolarInterpSrc};
     const char *names[] = {"polar_sc_device.h", "polar_sc_interp.h"};
     if (hiprtcCreateProgram(&prog, src.c_str(), "polar_sc_mask.hip", 2, hdrs, names) != HIPRTC_SUCCESS) return -EIO;
-    const std::vector<std::string> extra = rtc_extra();
-    std::vector<const char *> opts(std::begin(kRtcOpts), std::end(kRtcOpts));
-    for (const std::string &o : extra) opts.push_back(o.c_str());
-    hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
+    hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof kRtcOpts / sizeof kRtcOpts[0]), (const char **)kRtcOpts);
     size_t log_size = 0;
     hiprtcGetProgramLogSize(prog, &log_size);
     if (log_size > 1) {
@@ -830,46 +740,29 @@ int jit_load(const polar_sc_plan &p, DevState &st)
         return -EIO;
     if (!p.tiers.empty() && hipModuleGetFunction(&st.fn_tier, st.module, "polar_sc_tier_kernel") != hipSuccess)
         return -EIO;
-    if (!p.hybrid) {
-        // waves per block as generated into this plan's kernel source (run_mask)
-        st.mask_wpb = p.mask_wpb;
-        // per-mask kernel, persistent variant (POLAR_SC_MASK_PERSIST=R): grid = R x the blocks
-        // resident on the device at once; every wave loops over its 8-frame batches with the
-        // next channel prefetched into LDS (run_mask). Default: one batch per wave.
-        const int rounds = p.mask_rounds;   // as generated: a capped grid needs the batch loop
-        int per_cu = 0;
-        if (rounds > 0 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, st.fn, 64 * st.mask_wpb, 0) == hipSuccess &&
-            per_cu > 0)
-            st.mask_blocks = rounds * per_cu * (st.simds > 0 ? st.simds / 4 : 256);
-        if (std::getenv("POLAR_SC_VERBOSE"))
-            std::fprintf(stderr, "polar_sc: per-mask kernel N=%u: %d resident blocks per CU, grid cap %d blocks\n",
-                         p.N, per_cu, st.mask_blocks);
-    }
     return 0;
 }
 
 int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
                int out_stride, void *stream)
 {
-    const long waves = (batch + 7) / 8;
-    const int wpb = st.mask_wpb;
-    const long gw = p.mask_dual ? (waves + 1) / 2 : waves;   // dual kernels: two batches per wave
-    long nb = (gw + wpb - 1) / wpb;
-    if (st.mask_blocks > 0 && nb > st.mask_blocks) nb = st.mask_blocks;   // persistent waves
-    const unsigned blocks = (unsigned)nb;
+    (void)p;
+    const long waves = (batch + 7) / 8;   // one 8-frame batch per wave (run_mask)
+    const unsigned blocks = (unsigned)((waves + MASK_WPB - 1) / MASK_WPB);
     int b = (int)batch;
     void *args[] = {(void *)&llr, (void *)&out, (void *)&b, (void *)&out_stride};
-    hipError_t e = hipModuleLaunchKernel(st.fn, blocks, 1, 1, 64 * wpb, 1, 1, 0, (hipStream_t)stream, args, nullptr);
+    hipError_t e = hipModuleLaunchKernel(st.fn, blocks, 1, 1, 64 * MASK_WPB, 1, 1, 0, (hipStream_t)stream, args,
+                                         nullptr);
     return e == hipSuccess ? 0 : -EIO;
 }
 
 // hybrid kernel: the interpreter's launch shape (polar_sc_kernels.hip, polar_sc_launch_decode)
 int launch_interp_fn(hipFunction_t fn, const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out,
-                     long batch, int out_stride, int wpg, void *stream, unsigned long long *trace)
+                     long batch, int out_stride, int wpg, void *stream, unsigned long long *trace, const void *ops)
 {
     const long groups = (batch + 7) / 8;
     const unsigned lds = (unsigned)p.lds_group_dwords * 4u;
-    const void *ops = st.ops;
+    if (!ops) ops = st.ops;
     void *scratch = st.scratch;
     int N = (int)p.N, b = (int)batch, gpb = 1, gd = p.hbm_group_dwords, ld = p.lds_group_dwords, l0 = p.lds0;
     void *args[] = {(void *)&llr, (void *)&out, (void *)&ops, (void *)&scratch, (void *)&N, (void *)&b,

@@ -27,9 +27,8 @@ struct DevState {
     hipFunction_t ifn_trace = nullptr;  //   (per-op monitor only)
     hipModule_t module16 = nullptr;     // interpreter on the int16 channel (polar_sc_decode_i16)
     hipFunction_t fn16 = nullptr;
+    void *ops16 = nullptr;              //   and its schedule when it differs from `ops`
     int simds = 0;                // SIMDs of the device (4 per CU), for launch sizing
-    int mask_blocks = 0;          // per-mask kernel: grid cap (persistent waves), 0 = one batch per wave
-    int mask_wpb = 4;             // per-mask kernel: waves per block, from its compiled launch bound
 };
 
 enum JitMode { JIT_OFF = 0, JIT_AUTO = 1 };
@@ -78,11 +77,16 @@ struct polar_sc_plan {
     uint32_t ppw = 1;                // PAR groups per device word (PAR 4 / 8: 4 / 2)
     int lg = 0;                      // log2(N/16)
     polar_sc_config cfg{};
+    polar_sc_tuning tune{};          // kernel selection / launch shape (all 0 = automatic)
     std::vector<uint8_t> mask;       // N, 1 = information
     std::vector<uint64_t> fbp;       // GP, Bit_Frozen (bit k = mask[PAR g + k])
     std::vector<uint8_t> type;       // GP, Node_Type
     std::vector<polar_sc_op> ops;
     std::vector<polar_sc_op> dev_ops;   // device copy when it differs (HBM-scratch plans)
+    // the schedule interpreter's copy for the int16 channel (polar_sc_decode_i16): the plan's
+    // schedule without generated-subtree records (windowed for HBM-scratch plans); empty when
+    // it equals dev_ops (or ops)
+    std::vector<polar_sc_op> ops16;
     polar_sc_plan_stats stats{};
     int gmem = 0;
     // interpreter storage of one 8-frame group (dwords): HBM scratch part, LDS part, and the
@@ -110,9 +114,6 @@ struct polar_sc_plan {
     mutable std::vector<char> interp_code;   // per-mask plans, llr_bits != 6: traced interpreter
     mutable std::vector<char> code16;        // interpreter on the int16 channel (polar_sc_decode_i16)
     mutable std::string jit_log;
-    mutable int mask_wpb = 4;             // per-mask kernel: waves per block of the generated source
-    mutable int mask_rounds = 0;          //   and its persistent-loop grid cap (0: no loop)
-    mutable int mask_dual = 0;            //   1: two batches per wave (POLAR_SC_MASK_DUAL)
 };
 
 namespace polar_host {
@@ -128,6 +129,7 @@ int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *
 int jit_load_interp(const polar_sc_plan &p, DevState &st);
 int jit_load16(const polar_sc_plan &p, DevState &st);
 int launch_interp_fn(hipFunction_t fn, const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out,
-                     long batch, int out_stride, int wpg, void *stream, unsigned long long *trace);
+                     long batch, int out_stride, int wpg, void *stream, unsigned long long *trace,
+                     const void *ops = nullptr);   // schedule: nullptr = st.ops
 bool jit_supported(uint32_t N);
 }  // namespace polar_host

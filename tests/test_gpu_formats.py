@@ -84,6 +84,22 @@ def test_int16_channel_matches_int8(pkg, cuda, oracle_mod, q):
     _assert_same(pkg.unpack_bits(b.cpu().numpy(), mask.size), oracle_mod.decode_fsm(mask, llr, llr_bits=q), "i16")
 
 
+@pytest.mark.parametrize("name", ["frozen_n_2048_k_1024", "frozen_n_16384_k_8192", "frozen_n_65536_k_32768"])
+def test_int16_channel_hybrid_plans(pkg, cuda, oracle_mod, name):
+    """polar_sc_decode_i16 on plans whose int8 path is the hybrid kernel (generated subtree
+    decoders, grid tier at N = 65536): the int16 interpreter runs the plan's schedule without
+    subtree records and must give the int8 path's bits (it skipped the subtrees)."""
+    mask = util.mask(name)
+    llr, _ = util.synth_frames(mask, 11, ebn0_db=1.5, seed=1616)
+    dec = pkg.Decoder(mask)
+    assert dec.stats["kernel"] == 2 and dec.stats["n_sub_calls"] > 0
+    a = dec.decode(cuda.from_numpy(llr).cuda())
+    b = dec.decode(cuda.from_numpy(llr.astype(np.int16)).cuda())
+    cuda.cuda.synchronize()
+    assert (a.cpu().numpy() == b.cpu().numpy()).all()
+    _assert_same(pkg.unpack_bits(b.cpu().numpy(), mask.size), oracle_mod.decode_fsm(mask, llr), "i16 " + name)
+
+
 def test_formats_noiseless_full_size(pkg, cuda):
     """PAR 64 and CA2 at a full C2 batch (65536 frames): noiseless codewords decode exactly
     (size-independent property)."""
@@ -108,19 +124,18 @@ def _sweep_cfg(pkg, c7, par):
 
 
 @pytest.mark.parametrize("par", [16, 64, 8, 4])
-def test_script_tests_pruning_sweep(pkg, cuda, oracle_mod, par, monkeypatch):
+def test_script_tests_pruning_sweep(pkg, cuda, oracle_mod, par):
     """script/script_tests.sh:103-213 as the reference runs it: the 11 pruning configurations
     on frozen_n_32768_k_29492 (its lines 105-106) at QUANT 8, for PAR 16 and 64 (line 124),
     and the same sweep at PAR 8 and 4 (the PAR values of script_RTL_sim.sh).
-    PAR 16 plans run on the schedule interpreter here (POLAR_SC_JIT=0, one code object for
+    PAR 16 plans run on the schedule interpreter here (tuning kernel = 1, one code object for
     the format); the generated-subtree kernels are swept in test_gpu_configs.py."""
-    monkeypatch.setenv("POLAR_SC_JIT", "0")
     mask = util.mask("frozen_n_32768_k_29492")
     awgn, _ = util.synth_frames(mask, 8, ebn0_db=3.5, seed=par)
     llr = np.clip(awgn.astype(np.int32) * 4, -127, 127).astype(np.int8)
     t = cuda.from_numpy(llr).cuda()
     for c7 in oracle_mod.SWEEP_CONFIGS:
-        dec = pkg.Decoder(mask, config=_sweep_cfg(pkg, c7, par))
+        dec = pkg.Decoder(mask, config=_sweep_cfg(pkg, c7, par), tuning={"kernel": 1})
         out = dec.decode(t)
         cuda.cuda.synchronize()
         got = pkg.unpack_bits(out.cpu().numpy(), mask.size)

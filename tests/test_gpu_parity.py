@@ -1,7 +1,5 @@
 """GPU parity: the HIP decoder (through the C ABI) must be bit-exact with the CPU oracle
 (literal restatement of my_module::do_action) on the same LLR frames."""
-import os
-
 import numpy as np
 import pytest
 
@@ -10,18 +8,10 @@ import util
 pytestmark = pytest.mark.gpu
 
 
-def make_decoder(pkg, mask, jit=True):
+def make_decoder(pkg, mask, jit=True, **tuning):
     """jit=True: default plan (per-mask register kernel for N <= 1024); False: schedule
-    interpreter (POLAR_SC_JIT=0 at plan creation)."""
-    old = os.environ.get("POLAR_SC_JIT")
-    os.environ["POLAR_SC_JIT"] = "1" if jit else "0"
-    try:
-        return pkg.Decoder(mask)
-    finally:
-        if old is None:
-            del os.environ["POLAR_SC_JIT"]
-        else:
-            os.environ["POLAR_SC_JIT"] = old
+    interpreter (polar_sc_tuning.kernel = 1)."""
+    return pkg.Decoder(mask, tuning=dict(tuning, kernel=0 if jit else 1))
 
 
 def _decode(pkg, torch, mask, llr, jit=True):
@@ -158,6 +148,14 @@ def test_parity_c5_mask_sample(pkg, cuda, oracle_mod):
     _assert_same(_decode(pkg, cuda, mask, llr), oracle_mod.decode_fsm(mask, llr), "C5 sample")
 
 
+def test_parity_n524288_mask_sample(pkg, cuda, oracle_mod):
+    """The largest reference mask (Generated_Frozen_Bit/frozen_n_524288_k_262144.txt,
+    SURVEY.md 5): 2 frames vs the oracle (grid tier + HBM scratch at N = 2^19)."""
+    mask = util.mask("frozen_n_524288_k_262144")
+    llr, _ = util.synth_frames(mask, 2, ebn0_db=1.0, seed=524288)
+    _assert_same(_decode(pkg, cuda, mask, llr), oracle_mod.decode_fsm(mask, llr), "N=524288 sample")
+
+
 def test_full_size_c2_noiseless_roundtrip(pkg, cuda):
     """At BASELINE C2 size (65536 frames): noiseless LLRs must decode to the sent codeword
     (size-independent encode -> decode round trip)."""
@@ -226,15 +224,10 @@ def test_interpreter_waves_per_group(pkg, cuda, oracle_mod, name, batch, wpg):
     ops, leaves/REP/SPC on wave 0, barriers between differently split ops)."""
     mask = util.mask(name)
     llr, _ = util.synth_frames(mask, batch, ebn0_db=1.5, seed=wpg)
-    old = os.environ.get("POLAR_SC_WAVES_PER_GROUP")
-    os.environ["POLAR_SC_WAVES_PER_GROUP"] = str(wpg)
-    try:
-        got = _decode(pkg, cuda, mask, llr, jit=False)
-    finally:
-        if old is None:
-            del os.environ["POLAR_SC_WAVES_PER_GROUP"]
-        else:
-            os.environ["POLAR_SC_WAVES_PER_GROUP"] = old
+    dec = make_decoder(pkg, mask, False, waves_per_group=wpg)
+    out = dec.decode(cuda.from_numpy(np.ascontiguousarray(llr)).cuda())
+    cuda.cuda.synchronize()
+    got = pkg.unpack_bits(out.cpu().numpy(), mask.size)
     _assert_same(got, oracle_mod.decode_fsm(mask, llr), "%s wpg=%d" % (name, wpg))
 
 
@@ -246,21 +239,16 @@ def test_gpu_matches_committed_vectors(pkg, cuda, case, jit):
     _assert_same(_decode(pkg, cuda, util.mask(name), llr, jit), x, case)
 
 @pytest.mark.parametrize("name,batch", [("FB_N1024_K512", 40003), ("FB_N256_K128", 60001)])
-def test_persistent_mask_kernel(pkg, cuda, oracle_mod, monkeypatch, name, batch):
-    """POLAR_SC_MASK_PERSIST=1: the per-mask kernel as a persistent batch loop (grid = the
-    resident blocks, N = 1024 prefetching the next channel into LDS mid-decode, N < 1024
-    fetching at the top of each iteration). Batches larger than one batch per resident wave,
-    ragged: equal to the default kernel on every frame, and to the oracle on a sample."""
+def test_mask_kernel_large_ragged_batch(pkg, cuda, oracle_mod, name, batch):
+    """The per-mask kernel on a batch of several dispatch rounds with a ragged tail: equal to
+    the schedule interpreter on every frame, and to the oracle on a sample."""
     mask = util.mask(name)
     llr, _ = util.synth_frames(mask, batch, ebn0_db=1.5, seed=77)
     dev = cuda.from_numpy(llr).cuda()
-    ref_dec = make_decoder(pkg, mask, True)
-    ref = ref_dec.decode(dev)
-    monkeypatch.setenv("POLAR_SC_MASK_PERSIST", "1")
-    dec = make_decoder(pkg, mask, True)
-    got = dec.decode(dev)
+    ref = make_decoder(pkg, mask, False).decode(dev)
+    got = make_decoder(pkg, mask, True).decode(dev)
     cuda.cuda.synchronize()
     g = pkg.unpack_bits(got.cpu().numpy(), mask.size)
-    _assert_same(g, pkg.unpack_bits(ref.cpu().numpy(), mask.size), "persistent vs default " + name)
+    _assert_same(g, pkg.unpack_bits(ref.cpu().numpy(), mask.size), "per-mask vs interpreter " + name)
     idx = np.r_[0:48, batch - 40:batch]
-    _assert_same(g[idx], oracle_mod.decode_fsm(mask, llr[idx]), "persistent vs oracle " + name)
+    _assert_same(g[idx], oracle_mod.decode_fsm(mask, llr[idx]), "per-mask vs oracle " + name)

@@ -1,13 +1,11 @@
 """Hybrid plans (N > 1024): the schedule interpreter for the upper tree levels plus generated
-straight-line decoders for every mixed subtree of POLAR_SC_SUB_WORDS words
+straight-line decoders for every mixed subtree of polar_sc_tuning.sub_words words
 (polar_sc_interp.h OP_SUB, polar_sc_jit.cpp hybrid_source).
 
 CPU tests: plan statistics and hipRTC compilation of the generated source (no GPU needed).
 GPU tests: bit-exact against the oracle for every subtree size, including subtrees whose root
 children are REP / R1 / SPC nodes (the root-split path of the generator), and against the
 plain interpreter on a full C3 batch."""
-import os
-
 import numpy as np
 import pytest
 
@@ -15,22 +13,14 @@ import util
 
 
 def make(pkg, mask, jit="1", sub_words=None, tier_words=None):
-    keys = {"POLAR_SC_JIT": jit, "POLAR_SC_SUB_WORDS": None if sub_words is None else str(sub_words),
-            "POLAR_SC_TIER_WORDS": None if tier_words is None else str(tier_words)}
-    old = {k: os.environ.get(k) for k in keys}
-    try:
-        for k, v in keys.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-        return pkg.Decoder(mask)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    """Plan with explicit kernel selection (polar_sc_tuning): jit "0" = the schedule
+    interpreter; sub_words / tier_words as given (tier_words 0 = no grid tier)."""
+    t = {"kernel": 0 if jit == "1" else 1}
+    if sub_words is not None:
+        t["sub_words"] = sub_words
+    if tier_words is not None:
+        t["tier_words"] = tier_words if tier_words else -1
+    return pkg.Decoder(mask, tuning=t)
 
 
 def structured_mask(rng, N):
@@ -58,7 +48,7 @@ def test_hybrid_plan_stats(pkg):
 
 def test_grid_tier_plan(pkg):
     """Grid tier: C3 / C5 plans cut their schedule at the F / G records of >= 1024 words (2 / 4
-    upper levels); POLAR_SC_TIER_WORDS moves the cut (0 = single kernel); plans too small for
+    upper levels); polar_sc_tuning.tier_words moves the cut (-1 = single kernel); plans too small for
     an HBM level above the LDS region have none."""
     s = make(pkg, util.mask("frozen_n_65536_k_32768")).stats
     assert (s["tier_words"], s["tier_steps"]) == (1024, 10)
@@ -71,6 +61,19 @@ def test_grid_tier_plan(pkg):
     assert make(pkg, util.mask("frozen_n_32768_k_29492")).stats["tier_steps"] == 0
     assert make(pkg, util.mask("frozen_n_32768_k_29492"), tier_words=512).stats["tier_steps"] > 0
     assert make(pkg, util.mask("frozen_n_65536_k_32768"), jit="0").stats["tier_steps"] == 0
+
+
+def test_plan_n524288(pkg):
+    """The largest reference mask (N = 2^19): HBM-scratch storage with the 1024-slot LDS
+    region, grid tier at 1024 words, and scratch sized for the upper levels of one group."""
+    s = make(pkg, util.mask("frozen_n_524288_k_262144")).stats
+    assert (s["N"], s["K"], s["groups"]) == (524288, 262144, 32768)
+    assert (s["n_r0"], s["n_r1"], s["n_rep"], s["n_spc"], s["n_rn"]) == (14575, 13875, 662, 1341, 2315)
+    assert s["storage"] == 1 and s["kernel"] == 2 and s["tier_words"] == 1024 and s["tier_steps"] > 40
+    # LDS: 1023 slots of 8-bit pairs + the 64-dword partial-sum window + the SPC exchange area
+    assert s["lds_bytes_per_wave"] == (1023 * 64 * 2) + (64 + 24) * 256
+    # HBM: slots [0, G - 1024) as 128-byte rows + 2048 bit dwords of 256 bytes
+    assert s["scratch_bytes_per_wave"] == (32768 - 1024) * 128 + 2048 * 256
 
 
 def test_hybrid_schedule_export_unchanged(pkg):

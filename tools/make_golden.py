@@ -83,6 +83,8 @@ TABLES = [
     ("frozen_n_16384_k_14746", "mask", "Generated_Frozen_Bit/frozen_n_16384_k_14746.txt", 16384, 14746),
     ("frozen_n_65536_k_32768", "mask", "Generated_Frozen_Bit/frozen_n_65536_k_32768.txt", 65536, 32768),
     ("frozen_n_262144_k_131072", "mask", "Generated_Frozen_Bit/frozen_n_262144_k_131072.txt", 262144, 131072),
+    # the largest reference masks (N up to 524288)
+    ("frozen_n_524288_k_262144", "mask", "Generated_Frozen_Bit/frozen_n_524288_k_262144.txt", 524288, 262144),
 ]
 
 
