@@ -72,12 +72,16 @@ typedef struct polar_sc_config {
  * struct (never on the environment). Out-of-range values -> -EINVAL. */
 typedef struct polar_sc_tuning {
     int32_t kernel;           /* 0 = automatic; 1 = the schedule interpreter for every N
-                                 (no per-mask / generated-subtree code) */
+                                 (no per-mask / generated-subtree code); 2 = the hybrid
+                                 kernel (8-frame groups) for N > 1024; 3 = the pair kernel
+                                 (one frame pair per wave) for N >= 2048 */
     int32_t waves_per_group;  /* interpreter / hybrid launches: waves per 8-frame group, 0 =
                                  automatic (more when the batch cannot fill the GPU), else 1,
                                  2, 4, 8 or 16 (capped at the hybrid kernel's bound) */
-    int32_t sub_words;        /* hybrid plans: generated subtree size in 16-LLR words, 0 =
-                                 automatic (64, 128 from N = 32768), else a power of two 2..128 */
+    int32_t sub_words;        /* hybrid / pair plans: generated subtree size in 16-LLR words,
+                                 0 = automatic (hybrid: 64, 128 from N = 32768; pair:
+                                 min(256, N / 32)), else a power of two 2..128 (hybrid) or
+                                 16..256 and <= N / 32 (pair) */
     int32_t tier_words;       /* hybrid HBM-scratch plans: F / G records of >= this many words
                                  run as grid launches; 0 = automatic, -1 = no grid tier */
     int32_t lds_slots;        /* HBM-scratch plans: stage slots held in LDS, 0 = automatic,
@@ -321,10 +325,18 @@ int polar_write_parameters_h(const uint8_t *info_mask, uint32_t N, uint32_t par,
 int polar_parse_parameters_h(const char *path, uint8_t *mask_out, uint32_t cap, uint32_t *N_out,
                              uint32_t *par_out);
 
-/* GPU self-test of the cross-lane (DPP) exchange patterns the kernels rely on.
- * out_dev: 4*64 uint32 on the device; entry [h][lane] = source lane seen by `lane` for
- * partner distance 1<<h. Synchronous. */
+/* GPU self-test of the cross-lane exchange patterns the kernels rely on.
+ * out_dev: 8*64 uint32 on the device; entry [h][lane] (h = 0..3) = source lane seen by `lane`
+ * for DPP partner distance 1<<h; [4], [5] = the two results of v_permlane16_swap and [6], [7]
+ * those of v_permlane32_swap of the lane id with itself. Synchronous. */
 int polar_sc_selftest_lanes(uint32_t *out_dev);
+
+/* Test hook of pair plans (stats.kernel == 3): run generated subtree decoder `id` on one
+ * wave (one frame pair): in_dev = its root as stage-slot rows, [S/4 rows][64 lanes] uint16
+ * (SM8 pairs: low byte = frame 0, high byte = frame 1, lane 16 r + l = word 4 j + r, position
+ * of lane l of polar_sc_pair.h); out_dev = its partial sums, [max(1, S/64) dwords][64 lanes].
+ * Synchronous. -ENOTSUP for other plans. */
+int polar_sc_debug_subtree(const polar_sc_plan *plan, uint32_t id, const uint16_t *in_dev, uint32_t *out_dev);
 
 const char *polar_sc_strerror(int err);
 int polar_sc_abi_version(void);

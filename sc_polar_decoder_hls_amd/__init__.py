@@ -105,7 +105,7 @@ EXPORTS = (
     "polar_sc_abi_version", "polar_sc_plan_compile", "polar_sc_plan_kernel_source",
     "polar_csim_frames", "polar_csim_states", "polar_count_errors",
     "polar_mask_from_order", "polar_write_frozen_tab", "polar_write_parameters_h", "polar_parse_parameters_h",
-    "polar_sc_trace", "polar_sc_decode_i16",
+    "polar_sc_trace", "polar_sc_decode_i16", "polar_sc_debug_subtree",
 )
 
 _lib = None
@@ -137,6 +137,7 @@ def lib():
         "polar_sc_plan_get_stats": [p, p],
         "polar_sc_plan_get_schedule": [p, p, u32, ctypes.POINTER(u32)],
         "polar_sc_selftest_lanes": [p],
+        "polar_sc_debug_subtree": [p, u32, p, p],
         "polar_sc_plan_compile": [p],
         "polar_sc_plan_kernel_source": [p, ctypes.c_char_p, sz, ctypes.POINTER(sz)],
         "polar_sc_strerror": [i32],
@@ -425,6 +426,17 @@ class Decoder:
                 ctypes.c_void_p(s.cuda_stream)))
         return out
 
+    def debug_subtree(self, sid, rows):
+        """Test hook of pair plans: generated subtree decoder `sid` on root slot rows (uint16
+        [S/4, 64], SM8 pairs); returns its partial-sum dwords uint32 [max(1, S/64), 64]."""
+        torch = _torch()
+        S = self.stats["sub_words"]
+        inp = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.uint16).view(np.int16)).cuda()
+        out = torch.zeros((max(1, S // 64), 64), dtype=torch.int32, device="cuda")
+        _check("polar_sc_debug_subtree", lib().polar_sc_debug_subtree(self._plan, int(sid), ctypes.c_void_p(inp.data_ptr()),
+                                                                       ctypes.c_void_p(out.data_ptr())))
+        return out.cpu().numpy().view(np.uint32)
+
     def decode_host(self, llr):
         """Host arrays in/out (synchronous): int8 [B, N] -> uint64 [B, ceil(N/64)]."""
         a = np.ascontiguousarray(np.atleast_2d(llr), dtype=np.int8)
@@ -443,11 +455,12 @@ class Decoder:
 
 
 def selftest_lanes():
-    """Run the DPP row-exchange self-test on the current GPU; returns [4, 64] source lanes."""
+    """Run the cross-lane exchange self-test on the current GPU; returns [8, 64] source lanes
+    (DPP distances 1, 2, 4, 8; permlane16_swap results 0 / 1; permlane32_swap results 0 / 1)."""
     torch = _torch()
-    buf = torch.zeros(4 * 64, dtype=torch.int32, device="cuda")
+    buf = torch.zeros(8 * 64, dtype=torch.int32, device="cuda")
     _check("polar_sc_selftest_lanes", lib().polar_sc_selftest_lanes(ctypes.c_void_p(buf.data_ptr())))
-    return buf.view(4, 64).cpu().numpy()
+    return buf.view(8, 64).cpu().numpy()
 
 
 # ---------------------------------------------------------------------------------------

@@ -10,11 +10,13 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "lib", "libpolar_sc.so")
 SOURCES = [os.path.join(PKG, "csrc", "polar_sc_kernels.hip"), os.path.join(PKG, "csrc", "polar_sc_host.cpp"),
-           os.path.join(PKG, "csrc", "polar_sc_jit.cpp"), os.path.join(PKG, "csrc", "polar_sc_channel.hip"),
+           os.path.join(PKG, "csrc", "polar_sc_jit.cpp"), os.path.join(PKG, "csrc", "polar_sc_pairgen.cpp"),
+           os.path.join(PKG, "csrc", "polar_sc_channel.hip"),
            os.path.join(PKG, "csrc", "polar_sc_tables.cpp")]
 DEVICE_H = os.path.join(PKG, "csrc", "polar_sc_device.h")
 INTERP_H = os.path.join(PKG, "csrc", "polar_sc_interp.h")
-HEADERS = [os.path.join(ROOT, "include", "polar_sc.h"), DEVICE_H, INTERP_H, os.path.join(PKG, "csrc", "polar_sc_plan.hpp"),
+PAIR_H = os.path.join(PKG, "csrc", "polar_sc_pair.h")
+HEADERS = [os.path.join(ROOT, "include", "polar_sc.h"), DEVICE_H, INTERP_H, PAIR_H, os.path.join(PKG, "csrc", "polar_sc_plan.hpp"),
            os.path.join(PKG, "csrc", "polar_sc_glibcf.h")]
 GEN_DIR = os.path.join(PKG, "build")
 CLI_SRC = os.path.join(ROOT, "examples", "polar_decode_cli.c")
@@ -56,7 +58,8 @@ def build(force=False, verbose=False):
     os.makedirs(GEN_DIR, exist_ok=True)
     # embed the device headers for hipRTC (per-mask kernels are compiled at plan time)
     for path, inc, name in ((DEVICE_H, "polar_sc_device_src.inc", "kPolarDeviceSrc"),
-                            (INTERP_H, "polar_sc_interp_src.inc", "kPolarInterpSrc")):
+                            (INTERP_H, "polar_sc_interp_src.inc", "kPolarInterpSrc"),
+                            (PAIR_H, "polar_sc_pair_src.inc", "kPolarPairSrc")):
         with open(path) as f:
             src = f.read()
         assert ")POLARSRC\"" not in src
@@ -70,6 +73,28 @@ def build(force=False, verbose=False):
     subprocess.check_call(cmd)
     os.replace(tmp, LIB)
     return LIB
+
+
+def prewarm_plans(plans, threads=8, verbose=False):
+    """Compile the hipRTC kernels of [(name, info mask, tuning dict)] into the code-object cache
+    (host only, in parallel, largest first)."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+    import sc_polar_decoder_hls_amd as pkg
+
+    def one(item):
+        name, m, tun = item
+        t0 = time.time()
+        dec = pkg.Decoder(m, tuning=tun)
+        ok = dec.compile()
+        dec.close()
+        return name, tun, ok, time.time() - t0
+
+    items = sorted(plans, key=lambda it: -it[1].size)
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        for name, tun, ok, dt in ex.map(one, items):
+            if verbose:
+                print("prewarm %-28s %s %s %.1f s" % (name, tun, "compiled" if ok else "(no hipRTC kernel)", dt))
 
 
 def prewarm(masks, configs=(None,), threads=8, verbose=False):

@@ -213,6 +213,57 @@ polar_host::TierPlan tier_schedule(const polar_sc_plan &p, int tw)
     return t;
 }
 
+// Grid tier of a pair plan: the F / G records of at least `tw` output words become grid
+// launches over all frame pairs; the records between them are the cases of the segment kernel
+// (polar_sc_pairgen.cpp), separated by POLAR_OP_SEGEND. H / H0 of the cut nodes stay in the
+// segments, in schedule order.
+polar_host::PairTier pair_tier_schedule(const std::vector<polar_sc_op> &ops, int tw)
+{
+    polar_host::PairTier t;
+    bool any = false;
+    for (const polar_sc_op &o : ops)
+        if ((o.code == POLAR_OP_F || o.code == POLAR_OP_G) && o.n >= tw) any = true;
+    if (!any) return t;
+    int seg = 0;
+    bool open = false;
+    for (const polar_sc_op &o : ops) {
+        if (o.code == POLAR_OP_END) break;
+        if ((o.code == POLAR_OP_F || o.code == POLAR_OP_G) && o.n >= tw) {
+            if (open) {
+                polar_sc_op e{};
+                e.code = polar_host::POLAR_OP_SEGEND;
+                e.upos = -1;
+                t.seg_ops.push_back(e);
+                open = false;
+                seg++;
+            }
+            polar_host::TierStep st;
+            st.grid = 1;
+            st.op = o;
+            t.steps.push_back(st);
+            continue;
+        }
+        if (!open) {
+            polar_host::TierStep st;
+            st.off = seg;
+            t.steps.push_back(st);
+            open = true;
+        }
+        t.seg_ops.push_back(o);
+    }
+    if (!open) {   // the schedule ended on a grid record: an empty last segment writes the output
+        polar_host::TierStep st;
+        st.off = seg;
+        t.steps.push_back(st);
+    }
+    polar_sc_op e{};
+    e.code = POLAR_OP_END;
+    e.upos = -1;
+    t.seg_ops.push_back(e);
+    t.tw = tw;
+    return t;
+}
+
 // PAR > 16: decode the PAR-word leaf (Spec_PolarDec_{PAR}, library.h:149-172 ->
 // functions.h:766-866) whose LLRs are the node of `words` device words at (level, wpos) as
 // device ops: F, the left half, G (G_extended, flagged exact, when EXTENDED; the operands of
@@ -412,8 +463,8 @@ bool default_format(const polar_sc_config &c)
 bool tuning_valid(const polar_sc_tuning &t)
 {
     auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
-    return (t.kernel == 0 || t.kernel == 1) && (t.waves_per_group == 0 || (pow2(t.waves_per_group) && t.waves_per_group <= 16)) &&
-           (t.sub_words == 0 || (pow2(t.sub_words) && t.sub_words >= 2 && t.sub_words <= 128)) &&
+    return (t.kernel >= 0 && t.kernel <= 3) && (t.waves_per_group == 0 || (pow2(t.waves_per_group) && t.waves_per_group <= 16)) &&
+           (t.sub_words == 0 || (pow2(t.sub_words) && t.sub_words >= 2 && t.sub_words <= 256)) &&
            t.tier_words >= -1 && (t.tier_words <= 0 || pow2(t.tier_words)) &&
            (t.lds_slots == 0 || t.lds_slots == 256 || t.lds_slots == 512 || t.lds_slots == 1024) &&
            (t.hybrid_waves == 0 || t.hybrid_waves == 4 || t.hybrid_waves == 8) && t.reserved[0] == 0 &&
@@ -442,14 +493,14 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, DevMode 
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
         st.simds = 4 * cus;
     }
-    if ((p->jit || p->hybrid) && mode != DEV_I16) {
+    if ((p->jit || p->hybrid || p->pair) && mode != DEV_I16) {
         int rc = polar_host::jit_load(*p, st);
         if (rc) return rc;
         if (p->jit && !interp) {
             *out = &st;
             return 0;
         }
-        if (p->jit && p->cfg.llr_bits != 6) {   // traced per-mask plan: hipRTC interpreter at POLAR_Q
+        if ((p->jit || p->pair) && interp && p->cfg.llr_bits != 6) {   // traced plan: hipRTC interpreter at POLAR_Q
             rc = polar_host::jit_load_interp(*p, st);
             if (rc) return rc;
         }
@@ -476,9 +527,10 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, DevMode 
         if (hipMemcpy(st.seg_ops[t], p->tiers[t].seg_ops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
             return -EIO;
     }
-    if (p->gmem) {
+    if (p->gmem || p->pair) {
         size_t waves = (batch + 7) / 8;
-        size_t need = waves * (size_t)p->hbm_group_dwords * 4u;
+        size_t need = p->gmem ? waves * (size_t)p->hbm_group_dwords * 4u : 0u;
+        if (p->pair) need = std::max(need, (batch + 1) / 2 * (size_t)p->pair_dwords * 4u);
         if (need > st.scratch_bytes) {
             if (st.scratch) {
                 if (hipDeviceSynchronize() != hipSuccess) return -EIO;
@@ -520,9 +572,10 @@ int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size
     // another thread reallocates the scratch only after this launch has been queued (and
     // synchronises the device before freeing it)
     std::unique_lock<std::mutex> held;
-    int rc = ensure_device(p, batch, &st, DEV_DECODE, p->gmem ? &held : nullptr);
+    int rc = ensure_device(p, batch, &st, DEV_DECODE, (p->gmem || p->pair) ? &held : nullptr);
     if (rc) return rc;
     if (p->jit) return polar_host::jit_launch(*p, *st, llr, out, (long)batch, out_stride, stream);
+    if (p->pair) return polar_host::jit_launch_pair(*p, *st, llr, out, (long)batch, out_stride, stream);
     const int wpg = waves_per_group(p, batch, st->simds);
     if (p->hybrid) return polar_host::jit_launch_hybrid(*p, *st, llr, out, (long)batch, out_stride, wpg, stream);
     rc = polar_sc_launch_decode(p->gmem, llr, out, st->ops, (uint32_t *)st->scratch, (int)p->N, (long)batch,
@@ -556,7 +609,7 @@ int trace_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size_
     if (!rc) {
         if (p->hybrid) {
             rc = polar_host::jit_launch_hybrid(*p, *st, llr, out, (long)batch, out_stride, wpg, nullptr, dtrace);
-        } else if (p->jit && p->cfg.llr_bits != 6) {
+        } else if ((p->jit || p->pair) && p->cfg.llr_bits != 6) {
             // per-mask plan at another LLR_BITS: the hipRTC interpreter of its POLAR_Q
             if (wpg > polar_host::HYBRID_MAX_WAVES) wpg = polar_host::HYBRID_MAX_WAVES;
             rc = polar_host::launch_interp_fn(st->ifn_trace, *p, *st, llr, out, (long)batch, out_stride, wpg, nullptr,
@@ -749,7 +802,40 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     if (t.sub_words) sub_words = t.sub_words;
     const bool sub_ok = sub_words >= 2 && sub_words <= 128 && (sub_words & (sub_words - 1)) == 0;
     std::vector<polar_sc_op> dev_sched;
-    if (!p->jit && jit_on && !kinds && dflt && sub_ok && (uint32_t)sub_words < p->G) {
+    // pair plans (polar_sc_pair.h): one frame pair per wave, generated subtrees of up to 256
+    // words; polar_sc_tuning.kernel = 3 (2 = the hybrid kernel of 8-frame groups)
+    const bool want_pair = !p->jit && jit_on && !kinds && dflt && p->G >= 128 && t.kernel == 3;
+    if (want_pair) {
+        int S = std::min<int>(polar_host::PAIR_SUB_WORDS, (int)p->G / 2);
+        if (t.sub_words) {
+            if (t.sub_words < 16 || (uint32_t)t.sub_words > p->G / 2) {
+                delete p;
+                return -EINVAL;
+            }
+            S = t.sub_words;
+        }
+        SubCtx sc;
+        sc.words = (uint32_t)S;
+        compile_node(*p, p->pair_ops, 0, 0, p->GP, true, &sc);
+        emit(p->pair_ops, POLAR_OP_END, 0, 0, 0, -1, 0);
+        p->pair = 1;
+        p->sub_words = S;
+        p->subs = std::move(sc.lists);
+        s.sub_words = (uint32_t)S;
+        s.n_sub_kinds = (uint32_t)p->subs.size();
+        s.n_sub_calls = sc.calls;
+        p->pair_slot_rows = ((int)p->G - S) / 4;
+        p->pair_dwords = p->pair_slot_rows * 32 + (int)(p->G / 64) * 64;
+        if (t.tier_words > 0) {
+            if (t.tier_words <= S) {
+                delete p;
+                return -EINVAL;
+            }
+            p->pair_tier = pair_tier_schedule(p->pair_ops, t.tier_words);
+        }
+        // the schedule interpreter's copy (per-op monitor, int16 channel)
+        dev_sched = p->ops;
+    } else if (!p->jit && jit_on && !kinds && dflt && sub_ok && (uint32_t)sub_words < p->G) {
         SubCtx sc;
         sc.words = (uint32_t)sub_words;
         compile_node(*p, dev_sched, 0, 0, p->GP, true, &sc);
@@ -804,6 +890,15 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     s.storage = p->jit ? 2u : (uint32_t)p->gmem;
     s.lds_bytes_per_wave = p->jit ? 8u * (N + 16u) : (uint32_t)p->lds_group_dwords * 4u;
     s.scratch_bytes_per_wave = p->jit ? 0u : (uint64_t)p->hbm_group_dwords * 4u;
+    if (p->pair) {
+        // per frame pair: HBM slot rows + partial sums; LDS: the subtree-root level
+        s.kernel = 3u;
+        s.storage = 1u;
+        s.tier_steps = (uint32_t)p->pair_tier.steps.size();
+        s.tier_words = (uint32_t)p->pair_tier.tw;
+        s.lds_bytes_per_wave = (uint32_t)p->sub_words / 4u * 128u;
+        s.scratch_bytes_per_wave = (uint64_t)p->pair_dwords * 4u;
+    }
     *out = p;
     return 0;
 }
@@ -1016,7 +1111,7 @@ int polar_sc_plan_get_schedule(const polar_sc_plan *p, polar_sc_op *ops, uint32_
 int polar_sc_plan_compile(const polar_sc_plan *p)
 {
     if (!p) return -EINVAL;
-    if (!p->jit && !p->hybrid) return -ENOTSUP;
+    if (!p->jit && !p->hybrid && !p->pair) return -ENOTSUP;
     std::lock_guard<std::mutex> lk(p->mu);
     return polar_host::jit_compile(*p);
 }
@@ -1024,7 +1119,7 @@ int polar_sc_plan_compile(const polar_sc_plan *p)
 int polar_sc_plan_kernel_source(const polar_sc_plan *p, char *buf, size_t cap, size_t *len)
 {
     if (!p || !len) return -EINVAL;
-    if (!p->jit && !p->hybrid) return -ENOTSUP;
+    if (!p->jit && !p->hybrid && !p->pair) return -ENOTSUP;
     const std::string src = polar_host::jit_source(*p);
     *len = src.size();
     if (buf && cap) {
@@ -1033,6 +1128,21 @@ int polar_sc_plan_kernel_source(const polar_sc_plan *p, char *buf, size_t cap, s
         buf[n] = 0;
     }
     return 0;
+}
+
+int polar_sc_debug_subtree(const polar_sc_plan *p, uint32_t id, const uint16_t *in_dev, uint32_t *out_dev)
+{
+    if (!p || !in_dev || !out_dev) return -EINVAL;
+    if (!p->pair) return -ENOTSUP;
+    if (id >= p->subs.size()) return -EINVAL;
+    DevState *st = nullptr;
+    int rc = ensure_device(p, 1, &st);
+    if (rc) return rc;
+    int i = (int)id;
+    void *args[] = {(void *)&in_dev, (void *)&out_dev, (void *)&i};
+    if (hipModuleLaunchKernel(st->fn_subtest, 1, 1, 1, 64, 1, 1, 0, nullptr, args, nullptr) != hipSuccess)
+        return -EIO;
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -EIO;
 }
 
 int polar_sc_selftest_lanes(uint32_t *out_dev)

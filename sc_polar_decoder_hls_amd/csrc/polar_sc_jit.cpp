@@ -40,6 +40,7 @@ constexpr int MASK_MIN_WAVES = 4;
 namespace {
 #include "polar_sc_device_src.inc"   // kPolarDeviceSrc: polar_sc_device.h as a string
 #include "polar_sc_interp_src.inc"   // kPolarInterpSrc: polar_sc_interp.h as a string
+#include "polar_sc_pair_src.inc"     // kPolarPairSrc: polar_sc_pair.h as a string
 }
 
 namespace polar_host {
@@ -584,6 +585,7 @@ std::string hybrid_source(const polar_sc_plan &p, bool with_subs = true, bool ch
 
 std::string jit_source(const polar_sc_plan &p)
 {
+    if (p.pair) return pair_source(p);
     if (p.hybrid) return hybrid_source(p);
     return Gen(p.ops, p.lg).run_mask(p);
 }
@@ -623,6 +625,7 @@ std::string cache_path(const std::string &src)
     h = fnv1a(h, src.data(), src.size());
     h = fnv1a(h, kPolarDeviceSrc, sizeof kPolarDeviceSrc);
     h = fnv1a(h, kPolarInterpSrc, sizeof kPolarInterpSrc);
+    h = fnv1a(h, kPolarPairSrc, sizeof kPolarPairSrc);
     for (const char *o : kRtcOpts) h = fnv1a(h, o, std::strlen(o) + 1);
     int ver_major = 0, ver_minor = 0;
     hiprtcVersion(&ver_major, &ver_minor);
@@ -670,9 +673,9 @@ int rtc_compile(const std::string &src, std::vector<char> &code, std::string &lo
     const std::string cpath = cache_path(src);
     if (cache_load(cpath, code)) return 0;
     hiprtcProgram prog;
-    const char *hdrs[] = {kPolarDeviceSrc, kPolarInterpSrc};
-    const char *names[] = {"polar_sc_device.h", "polar_sc_interp.h"};
-    if (hiprtcCreateProgram(&prog, src.c_str(), "polar_sc_mask.hip", 2, hdrs, names) != HIPRTC_SUCCESS) return -EIO;
+    const char *hdrs[] = {kPolarDeviceSrc, kPolarInterpSrc, kPolarPairSrc};
+    const char *names[] = {"polar_sc_device.h", "polar_sc_interp.h", "polar_sc_pair.h"};
+    if (hiprtcCreateProgram(&prog, src.c_str(), "polar_sc_mask.hip", 3, hdrs, names) != HIPRTC_SUCCESS) return -EIO;
     hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof kRtcOpts / sizeof kRtcOpts[0]), (const char **)kRtcOpts);
     size_t log_size = 0;
     hiprtcGetProgramLogSize(prog, &log_size);
@@ -733,6 +736,16 @@ int jit_load(const polar_sc_plan &p, DevState &st)
     int rc = jit_compile(p);
     if (rc) return rc;
     if (hipModuleLoadData(&st.module, p.jit_code.data()) != hipSuccess) return -EIO;
+    if (p.pair) {
+        if (hipModuleGetFunction(&st.fn, st.module, "polar_sc_pair_kernel") != hipSuccess) return -EIO;
+        if (hipModuleGetFunction(&st.fn_subtest, st.module, "polar_sc_pair_subtest_kernel") != hipSuccess)
+            return -EIO;
+        if (!p.pair_tier.steps.empty() &&
+            (hipModuleGetFunction(&st.fn_seg, st.module, "polar_sc_pair_seg_kernel") != hipSuccess ||
+             hipModuleGetFunction(&st.fn_tier, st.module, "polar_sc_pair_tier_kernel") != hipSuccess))
+            return -EIO;
+        return 0;
+    }
     if (hipModuleGetFunction(&st.fn, st.module, p.hybrid ? "polar_sc_hybrid_kernel" : "polar_sc_mask_kernel") !=
         hipSuccess)
         return -EIO;
@@ -809,6 +822,62 @@ int launch_tier(const polar_sc_plan &p, const DevState &st, const int8_t *llr, u
                             (void *)&no_trace};
             e = hipModuleLaunchKernel(st.fn, (unsigned)groups, 1, 1, (unsigned)(64 * wpg), 1, 1, lds,
                                       (hipStream_t)stream, args, nullptr);
+        }
+        if (e != hipSuccess) return -EIO;
+    }
+    return 0;
+}
+
+// Pair plans (polar_sc_pair.h): one block of W waves per frame pair. W grows while the pairs
+// cannot give every SIMD two waves (C3's 2048 pairs: 1; C5's 256 or 32: 8). The stage slots of
+// the smallest levels go to LDS while they fit the share of a CU's 160 KB that one resident
+// pair gets (all-HBM otherwise); with a grid tier they stay below the tier's cut.
+int jit_launch_pair(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
+                    int out_stride, void *stream)
+{
+    const long pairs = (batch + 1) / 2;
+    const long cus = st.simds > 0 ? st.simds / 4 : 256;
+    int W = p.tune.waves_per_group;
+    if (W == 0) {
+        W = 1;
+        while (W < PAIR_WAVES_MAX && pairs * W < 2 * (st.simds > 0 ? st.simds : 1024)) W *= 2;
+    }
+    if (W > PAIR_WAVES_MAX) W = PAIR_WAVES_MAX;
+    const bool tier = !p.pair_tier.steps.empty();
+    // LDS: levels of nodes S .. L words (32 (2 L - S) bytes) + the SPC exchange (3 W rows of 256 B)
+    const long per_cu = (pairs + cus - 1) / cus;
+    const long budget = 160l * 1024l / (per_cu > 0 ? per_cu : 1) - 3l * W * 256l;
+    const int S = p.sub_words, G = (int)p.G;
+    int L = 0;
+    for (int w = S; w <= G / 2; w *= 2) {
+        if (tier && w >= p.pair_tier.tw) break;
+        if (32l * (2l * w - S) <= budget) L = w;
+    }
+    const int lds_rows = L ? (2 * L - S) / 4 : 0;
+    int lds_row0 = p.pair_slot_rows - lds_rows;
+    const unsigned lds = (unsigned)(lds_rows * 128 + 3 * W * 256);
+    int N = (int)p.N, b = (int)batch, pd = p.pair_dwords, sr = p.pair_slot_rows;
+    void *scratch = st.scratch;
+    auto segment = [&](hipFunction_t fn, int seg) {
+        void *args[] = {(void *)&llr, (void *)&out, (void *)&scratch, (void *)&N, (void *)&b, (void *)&out_stride,
+                        (void *)&pd, (void *)&sr, (void *)&lds_row0, (void *)&seg};
+        return hipModuleLaunchKernel(fn, (unsigned)pairs, 1, 1, (unsigned)(64 * W), 1, 1, lds, (hipStream_t)stream,
+                                     args, nullptr);
+    };
+    if (!tier) return segment(st.fn, 0) == hipSuccess ? 0 : -EIO;
+    int cw = TIER_CW;
+    for (const TierStep &t : p.pair_tier.steps) {
+        hipError_t e;
+        if (t.grid) {
+            int g = t.op.code == POLAR_OP_G ? 1 : 0, k = t.op.level, n4 = t.op.n / 4;
+            int ub = t.op.upos >= 0 ? t.op.upos / 4 : -1;
+            const long waves = pairs * (long)((n4 + cw - 1) / cw);
+            void *args[] = {(void *)&llr, (void *)&scratch, (void *)&N, (void *)&b, (void *)&pd, (void *)&sr,
+                            (void *)&g, (void *)&k, (void *)&n4, (void *)&ub, (void *)&cw};
+            e = hipModuleLaunchKernel(st.fn_tier, (unsigned)((waves + 3) / 4), 1, 1, 256, 1, 1, 0, (hipStream_t)stream,
+                                      args, nullptr);
+        } else {
+            e = segment(st.fn_seg, t.off);
         }
         if (e != hipSuccess) return -EIO;
     }

@@ -28,7 +28,9 @@ __global__ void __launch_bounds__(1024) polar_sc_decode_trace_kernel(
                             lds0, trace);
 }
 
-// DPP exchange self-test: out[h*64 + lane] = lane id seen through xorlane<1<<h>
+// cross-lane self-test: out[h*64 + lane] = lane id seen through xorlane<1<<h> (h = 0..3), then
+// the two results of v_permlane16_swap (rows 4, 5) and v_permlane32_swap (rows 6, 7) of the
+// lane id with itself (the frame-pair layout's cross-row steps, polar_sc_pair.h)
 __global__ void polar_sc_lane_selftest_kernel(uint32_t *out)
 {
     uint32_t l = threadIdx.x;
@@ -36,6 +38,12 @@ __global__ void polar_sc_lane_selftest_kernel(uint32_t *out)
     out[1 * 64 + l] = xorlane<2>(l);
     out[2 * 64 + l] = xorlane<4>(l);
     out[3 * 64 + l] = xorlane<8>(l);
+    const auto p16 = __builtin_amdgcn_permlane16_swap(l, l, false, false);
+    const auto p32 = __builtin_amdgcn_permlane32_swap(l, l, false, false);
+    out[4 * 64 + l] = p16[0];
+    out[5 * 64 + l] = p16[1];
+    out[6 * 64 + l] = p32[0];
+    out[7 * 64 + l] = p32[1];
 }
 
 }  // namespace polar

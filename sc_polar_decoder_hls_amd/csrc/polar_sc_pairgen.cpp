@@ -1,0 +1,506 @@
+// polar_sc_pairgen.cpp -- generated decode kernels of pair plans (N >= 2048 in the shipped
+// datapath): the frame-pair layout of polar_sc_pair.h.
+//
+// A pair plan's device schedule (polar_sc_host.cpp compile_node with subtrees of S words) has
+// two parts:
+//   * the upper levels (nodes wider than S words): F / G / REP / R1 / SPC / H records over
+//     slot rows, emitted here as calls of the loop functions of polar_sc_pair.h, split over
+//     the W waves of the pair where that is legal;
+//   * every mixed node of S words: one OP_SUB record, whose own schedule becomes straight-line
+//     register code (PairGen::sub_function) -- the per-mask kernel's split-word code
+//     (polar_sc_jit.cpp Gen) rewritten for four words per register and the cross-row steps of
+//     the nodes of 2 and 4 words.
+// The reference is specialised per code the same way (Frozen_Bit_Generator writes the mask into
+// polar_parameters.h and the HLS design is re-synthesised for it, Writer.h:110-162).
+#include "polar_sc_plan.hpp"
+
+#include <map>
+#include <stdexcept>
+#include <sstream>
+#include <string>
+#include <vector>
+
+namespace polar_host {
+
+namespace {
+
+struct PairGen {
+    const std::vector<polar_sc_op> &ops;   // subtree schedule, levels / positions relative to its root
+    std::ostringstream o;
+    int LG;                                // the subtree root has 2^LG words
+    std::map<int, std::string> small1;     // result masks of 1-word nodes, by word position
+    std::map<int, std::string> small2;     // result masks of 2-word nodes (row r: word r & 1)
+    int nvar = 0;
+
+    PairGen(const std::vector<polar_sc_op> &ops_, int lg) : ops(ops_), LG(lg) {}
+
+    static int regs(int sd) { return sd >= 2 ? 1 << (sd - 2) : 1; }   // registers of a node of 2^sd words
+    static int planes(int r) { return r >= 16 ? r / 16 : 1; }
+    static std::string M(int sd, int i) { return "m" + std::to_string(sd) + "[" + std::to_string(i) + "]"; }
+    // sign plane of register i of a node of 2^sd words, shifted so that register i is at bit 0
+    static std::string P(int sd, int i)
+    {
+        std::ostringstream s;
+        if (i % 16 == 0) s << "s" << sd << "[" << i / 16 << "]";
+        else s << "(s" << sd << "[" << i / 16 << "] >> " << i % 16 << ")";
+        return s.str();
+    }
+    // partial sums of local words l .. l + 15 (local word l at bit 0)
+    static std::string get16(int l)
+    {
+        std::ostringstream s;
+        if (l % 16 == 0) s << "bw[" << l / 16 << "]";
+        else s << "(bw[" << l / 16 << "] >> " << l % 16 << ")";
+        return s.str();
+    }
+    static std::string U(int ub, int k) { return ub >= 0 ? get16(ub + 16 * k) : std::string("0u"); }
+    static std::string hexmask(int l, int cnt)
+    {
+        std::ostringstream s;
+        const unsigned m = ((1u << cnt) - 1u) << (l % 16);
+        s << "0x" << std::hex << (m | (m << 16)) << std::dec << "u";
+        return s.str();
+    }
+    // local words [l, l + cnt) (cnt <= 16, one dword) := acc (bit j = local word l + j)
+    void put(int l, int cnt, const std::string &acc)
+    {
+        if (cnt >= 16) o << "    bw[" << l / 16 << "] = " << acc << ";\n";
+        else
+            o << "    bw[" << l / 16 << "] = bsel(" << hexmask(l, cnt) << ", (" << acc << ") << " << l % 16 << ", bw["
+              << l / 16 << "]);\n";
+    }
+    std::string var(const char *p) { return std::string(p) + std::to_string(nvar++) + "_"; }
+    void fence() { o << "  __builtin_amdgcn_sched_barrier(0);\n"; }
+    void chunk_fence(int i, int n)
+    {
+        if ((i & 7) == 7 && i + 1 < n) fence();
+    }
+    // after an F-type op the parent words stay live until the matching G: an empty asm that
+    // redefines them keeps the F op's intermediates from being carried across the left subtree
+    void clobber_parent(int sd, int n4)
+    {
+        if (sd == LG) return;   // root words are re-read from the slot
+        for (int i = 0; i < 2 * n4; i++) o << "  asm volatile(\"\" : \"+v\"(" << M(sd, i) << "));\n";
+        for (int k = 0; k < planes(2 * n4); k++) o << "  asm volatile(\"\" : \"+v\"(s" << sd << "[" << k << "]));\n";
+    }
+    static const char *swp(int pd) { return pd == 2 ? "swap32" : "swap16"; }
+    // split root words (for REP / R1 / SPC children of the subtree root)
+    void root_split(int words)
+    {
+        for (int k = 0; k < planes(words); k++) o << "  s" << LG << "[" << k << "] = 0u;\n";
+        for (int i = 0; i < words; i++) {
+            o << "  { const u32 v_ = CH(" << i << "); " << M(LG, i) << " = v_ & MAG; s" << LG << "[" << i / 16
+              << "] = plane_put<" << i % 16 << ">(s" << LG << "[" << i / 16 << "], v_); }\n";
+            chunk_fence(i, words);
+        }
+    }
+    // u flags of a small G-type op (bit 0 / 16 planes) from the left sibling's result mask
+    std::string small_u(int n, int upos)
+    {
+        if (upos < 0) return "0u";
+        const std::map<int, std::string> &m = n == 1 ? small1 : small2;
+        auto it = m.find(upos);
+        if (it == m.end()) throw std::runtime_error("pairgen: missing small result");
+        return "(" + it->second + " & 0x00010001u)";
+    }
+
+    // ---- ops on nodes of >= 4 output words: lane-private, four words per register ----------
+    void big_op(const polar_sc_op &op, int pd, int cd, int n4)
+    {
+        const int np = planes(n4), l0 = op.pos / 4, ub = op.upos >= 0 ? op.upos / 4 : -1;
+        const bool root = pd == LG;   // the subtree root: SM16 words re-read from its stage slot
+        if (root && (op.code == POLAR_OP_REP || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC)) root_split(2 * n4);
+        if (root && op.code == POLAR_OP_F) {
+            o << "  { // F n " << op.n << " (root)\n    u32 P_[" << np << "] = {};\n";
+            for (int i = 0; i < n4; i++) {
+                o << "    " << M(cd, i) << " = F_root<" << i % 16 << ">(CH(" << i << "), CH(" << n4 + i << "), P_[" << i / 16
+                  << "]);\n";
+                chunk_fence(i, n4);
+            }
+            for (int k = 0; k < np; k++) o << "    s" << cd << "[" << k << "] = P_[" << k << "];\n";
+            o << "  }\n";
+            return;
+        }
+        if (root && op.code == POLAR_OP_G) {
+            o << "  { // G n " << op.n << " upos " << op.upos << " (root)\n    u32 c_, P_[" << np << "] = {};\n";
+            for (int i = 0; i < n4; i++) {
+                if ((i & 15) == 0) o << "    c_ = " << (ub >= 0 ? get16(ub + i) : std::string("0u")) << ";\n";
+                o << "    " << M(cd, i) << " = G_root<" << i % 16 << ">(CH(" << i << "), CH(" << n4 + i << "), (c_ << "
+                  << 15 - (i & 15) << "), P_[" << i / 16 << "]);\n";
+                chunk_fence(i, n4);
+            }
+            for (int k = 0; k < np; k++) o << "    s" << cd << "[" << k << "] = P_[" << k << "];\n";
+            o << "  }\n";
+            return;
+        }
+        switch (op.code) {
+        case POLAR_OP_F:
+            o << "  { // F n " << op.n << "\n";
+            for (int i = 0; i < n4; i++) {
+                o << "    " << M(cd, i) << " = pk_min(" << M(pd, i) << ", " << M(pd, n4 + i) << ");\n";
+                chunk_fence(i, n4);
+            }
+            for (int k = 0; k < np; k++)
+                o << "    s" << cd << "[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << ";\n";
+            o << "  }\n";
+            clobber_parent(pd, n4);
+            break;
+        case POLAR_OP_G:
+            o << "  { // G n " << op.n << " upos " << op.upos << "\n    u32 X_[" << np << "], LT_[" << np << "] = {};\n";
+            for (int k = 0; k < np; k++)
+                o << "    X_[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << " ^ " << U(ub, k) << ";\n";
+            for (int i = 0; i < n4; i++) {
+                o << "    " << M(cd, i) << " = G_split<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i) << ", X_["
+                  << i / 16 << "], LT_[" << i / 16 << "]);\n";
+                chunk_fence(i, n4);
+            }
+            for (int k = 0; k < np; k++)
+                o << "    s" << cd << "[" << k << "] = " << P(pd, n4 + 16 * k) << " ^ (X_[" << k << "] & ~LT_[" << k
+                  << "]);\n";
+            o << "  }\n";
+            break;
+        case POLAR_OP_REP: {
+            // value chain in two's complement over the words in order (4 i + row), the exact
+            // SM chain only when a total is 0
+            o << "  { // REP n " << op.n << "\n    u32 acc_ = 0u, FS_[" << np << "];\n";
+            for (int k = 0; k < np; k++)
+                o << "    FS_[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << ";\n";
+            for (int i = 0; i < n4; i++) {
+                o << "    { const X4 t_ = rows4(row_sum_biased(F_split_biased<" << i % 16 << ">(" << M(pd, i) << ", "
+                  << M(pd, n4 + i) << ", FS_[" << i / 16 << "])));\n"
+                  << "      acc_ = rep_acc(rep_acc(rep_acc(rep_acc(acc_, t_.t0), t_.t1), t_.t2), t_.t3); }\n";
+                chunk_fence(i, n4);
+            }
+            o << "    if (rep_any_zero(acc_)) {\n      acc_ = 0u;\n";
+            for (int i = 0; i < n4; i++)
+                o << "      { const X4 t_ = rows4(row_add_tree(F_split_sm<" << i % 16 << ">(" << M(pd, i) << ", "
+                  << M(pd, n4 + i) << ", FS_[" << i / 16 << "]), ln));\n"
+                  << "        acc_ = G_sm<REPSAT>(t_.t0, acc_, 0u); acc_ = G_sm<REPSAT>(t_.t1, acc_, 0u);\n"
+                  << "        acc_ = G_sm<REPSAT>(t_.t2, acc_, 0u); acc_ = G_sm<REPSAT>(t_.t3, acc_, 0u); }\n";
+            o << "    }\n    const u32 full_ = pk_sra(acc_, 15);\n";
+            for (int j = 0; j < n4; j += 16) put(l0 + j, n4 < 16 ? n4 : 16, "full_");
+            o << "  }\n";
+            clobber_parent(pd, n4);
+            break;
+        }
+        case POLAR_OP_R1:
+        case POLAR_OP_SPC: {
+            const bool spc = op.code == POLAR_OP_SPC;
+            o << "  { // " << (spc ? "SPC" : "R1") << " n " << op.n << " upos " << op.upos << "\n    u32 X_[" << np
+              << "], LT_[" << np << "] = {};\n";
+            for (int k = 0; k < np; k++)
+                o << "    X_[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << " ^ " << U(ub, k) << ";\n";
+            if (spc) o << "    u32 klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu, par_ = 0u;\n    const u32 rw_ = c.row << 4;\n";
+            for (int i = 0; i < n4; i++) {
+                if (spc)
+                    o << "    { const u32 l_ = G_split<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i) << ", X_["
+                      << i / 16 << "], LT_[" << i / 16 << "]);\n"
+                      << "      klo_ = __builtin_elementwise_min(klo_, (l_ << 24) | rw_ | " << (i << 6) << "u);\n"
+                      << "      khi_ = __builtin_elementwise_min(khi_, ((l_ >> 16) << 24) | rw_ | " << (i << 6)
+                      << "u); }\n";
+                else
+                    o << "    LT_[" << i / 16 << "] = plane_put<" << i % 16 << ">(LT_[" << i / 16 << "], pk_sub(" << M(pd, i)
+                      << ", " << M(pd, n4 + i) << "));\n";
+                chunk_fence(i, n4);
+            }
+            for (int k = 0; k < np; k++) {
+                o << "    { const u32 h_ = " << P(pd, n4 + 16 * k) << " ^ (X_[" << k << "] & ~LT_[" << k << "]);\n";
+                put(l0 + 16 * k, n4 < 16 ? n4 : 16, "h_");
+                if (spc) o << "      par_ ^= h_; }\n";
+                else o << "    }\n";
+            }
+            if (spc) {
+                if (n4 < 16) {
+                    const unsigned m = (1u << n4) - 1u;
+                    o << "    par_ &= 0x" << std::hex << (m | (m << 16)) << std::dec << "u;\n";
+                }
+                o << "    par_ = ((__builtin_popcount(par_ & 0xFFFFu) & 1u) << 15) | ((__builtin_popcount(par_ >> 16) & 1u) << 31);\n"
+                     "    par_ = row_xor(par_);\n"
+                     "    klo_ = row_min_u32(klo_ | ln.br); khi_ = row_min_u32(khi_ | ln.br);\n"
+                     "    { X2 p_ = swap16(par_); par_ = p_.a ^ p_.b; p_ = swap32(par_); par_ = p_.a ^ p_.b;\n"
+                     "      X2 a_ = swap16(klo_), b_ = swap16(khi_);\n"
+                     "      klo_ = __builtin_elementwise_min(a_.a, a_.b); khi_ = __builtin_elementwise_min(b_.a, b_.b);\n"
+                     "      a_ = swap32(klo_); b_ = swap32(khi_);\n"
+                     "      klo_ = __builtin_elementwise_min(a_.a, a_.b); khi_ = __builtin_elementwise_min(b_.a, b_.b); }\n"
+                     "    const u32 ilo_ = (klo_ >> 6) & 0x3FFFFu, ihi_ = (khi_ >> 6) & 0x3FFFFu;\n"
+                     "    const bool flo_ = land(land(par_ & 0x8000u, (klo_ & 15u) == ln.br), ((klo_ >> 4) & 3u) == c.row);\n"
+                     "    const bool fhi_ = land(land(par_ & 0x80000000u, (khi_ & 15u) == ln.br), ((khi_ >> 4) & 3u) == c.row);\n";
+                if (n4 <= 16) {
+                    o << "    bw[" << l0 / 16 << "] ^= sel(flo_, 1u << (" << l0 % 16 << " + ilo_), 0u) | sel(fhi_, 0x10000u << ("
+                      << l0 % 16 << " + ihi_), 0u);\n";
+                } else {
+                    for (int k = 0; k < n4 / 16; k++)
+                        o << "    bw[" << l0 / 16 + k << "] ^= sel(land(flo_, (ilo_ >> 4) == " << k
+                          << "u), 1u << (ilo_ & 15u), 0u) | sel(land(fhi_, (ihi_ >> 4) == " << k
+                          << "u), 0x10000u << (ihi_ & 15u), 0u);\n";
+                }
+            }
+            o << "  }\n";
+            break;
+        }
+        case POLAR_OP_H:
+        case POLAR_OP_H0: {
+            const bool h = op.code == POLAR_OP_H;
+            o << "  { // " << (h ? "H" : "H0") << " n " << op.n << "\n";
+            if (n4 >= 16) {
+                for (int k = 0; k < n4 / 16; k++)
+                    o << "    bw[" << l0 / 16 + k << "] " << (h ? "^=" : "=") << " bw[" << (l0 + n4) / 16 + k << "];\n";
+            } else {
+                const int j = l0 / 16;
+                if (h)
+                    o << "    bw[" << j << "] ^= (bw[" << j << "] >> " << n4 << ") & " << hexmask(l0, n4) << ";\n";
+                else
+                    o << "    bw[" << j << "] = bsel(" << hexmask(l0, n4) << ", bw[" << j << "] >> " << n4 << ", bw[" << j
+                      << "]);\n";
+            }
+            o << "  }\n";
+            break;
+        }
+        default:
+            throw std::runtime_error("pairgen: unexpected op");
+        }
+    }
+
+    // ---- ops with 1 or 2 output words: the cross-row steps --------------------------------
+    void small_op(const polar_sc_op &op, int pd, int cd)
+    {
+        const int n = op.n;
+        const char *sw = swp(pd);
+        switch (op.code) {
+        case POLAR_OP_F:
+            o << "  { // F n " << n << "\n    const X2 m_ = " << sw << "(" << M(pd, 0) << "), s_ = " << sw << "(s" << pd
+              << "[0]);\n    " << M(cd, 0) << " = pk_min(m_.a, m_.b); s" << cd << "[0] = s_.a ^ s_.b;\n  }\n";
+            break;
+        case POLAR_OP_G:
+            o << "  { // G n " << n << " upos " << op.upos << "\n    const X2 m_ = " << sw << "(" << M(pd, 0) << "), s_ = "
+              << sw << "(s" << pd << "[0]);\n    u32 LT_ = 0u; const u32 X_ = s_.a ^ s_.b ^ " << small_u(n, op.upos)
+              << ";\n    " << M(cd, 0) << " = G_split<0>(m_.a, m_.b, X_, LT_);\n    s" << cd
+              << "[0] = s_.b ^ (X_ & ~LT_);\n  }\n";
+            break;
+        case POLAR_OP_FLEAF:
+        case POLAR_OP_GLEAF: {
+            const bool f = op.code == POLAR_OP_FLEAF;
+            const std::string x = var("x");
+            o << "  u32 " << x << ";\n  { // " << (f ? "F" : "G") << "+leaf pos " << op.pos << " fb 0x" << std::hex << op.fb
+              << std::dec << "\n    const X2 m_ = swap16(" << M(pd, 0) << "), s_ = swap16(s" << pd << "[0]);\n";
+            if (f) {
+                o << "    const u32 M_ = pk_min(m_.a, m_.b), S_ = plane_mask<0>(s_.a ^ s_.b);\n";
+            } else {
+                o << "    const u32 xm_ = opaque(plane_mask<0>(s_.a ^ s_.b ^ " << small_u(1, op.upos) << "));\n"
+                  << "    const u32 d_ = pk_sub(m_.a, m_.b);\n"
+                  << "    const u32 M_ = pk_min(bsel(xm_, pk_abs_i16(d_), pk_add(m_.a, m_.b)), GSAT2);\n"
+                  << "    const u32 S_ = plane_mask<0>(s_.b) ^ (xm_ & ~pk_sra(d_, 15));\n";
+            }
+            o << "    " << x << " = leaf_ms<0x" << std::hex << (op.fb & 0xFFFFu) << std::dec << "u, 0, 16>(M_, S_, ln);\n  }\n";
+            small1[op.pos] = x;
+            break;
+        }
+        case POLAR_OP_REP: {
+            const std::string x = var("x");
+            o << "  u32 " << x << ";\n  { // REP n " << n << "\n    const X2 m_ = " << sw << "(" << M(pd, 0)
+              << "), s_ = " << sw << "(s" << pd << "[0]);\n    const u32 FS_ = s_.a ^ s_.b;\n"
+              << "    const u32 t_ = row_sum_biased(F_split_biased<0>(m_.a, m_.b, FS_));\n";
+            if (n == 1) o << "    u32 acc_ = rep_acc(0u, t_);\n";
+            else o << "    const X2 q_ = swap16(t_);\n    u32 acc_ = rep_acc(rep_acc(0u, q_.a), q_.b);\n";
+            o << "    if (rep_any_zero(acc_)) {\n      const u32 e_ = row_add_tree(F_split_sm<0>(m_.a, m_.b, FS_), ln);\n";
+            if (n == 1) o << "      acc_ = G_sm<REPSAT>(e_, 0u, 0u);\n";
+            else o << "      const X2 r_ = swap16(e_);\n      acc_ = G_sm<REPSAT>(r_.b, G_sm<REPSAT>(r_.a, 0u, 0u), 0u);\n";
+            o << "    }\n    " << x << " = pk_sra(acc_, 15);\n  }\n";
+            (n == 1 ? small1 : small2)[op.pos] = x;
+            break;
+        }
+        case POLAR_OP_R1:
+        case POLAR_OP_SPC: {
+            const bool spc = op.code == POLAR_OP_SPC;
+            const std::string x = var("x");
+            o << "  u32 " << x << ";\n  { // " << (spc ? "SPC" : "R1") << " n " << n << "\n    const X2 m_ = " << sw << "("
+              << M(pd, 0) << "), s_ = " << sw << "(s" << pd << "[0]);\n    u32 LT_ = 0u; const u32 X_ = s_.a ^ s_.b ^ "
+              << small_u(n, op.upos) << ";\n";
+            if (!spc) {
+                o << "    LT_ = plane_put<0>(0u, pk_sub(m_.a, m_.b));\n"
+                  << "    " << x << " = plane_mask<0>(s_.b ^ (X_ & ~LT_));\n  }\n";
+            } else {
+                o << "    const u32 l_ = G_split<0>(m_.a, m_.b, X_, LT_);\n"
+                  << "    const u32 h_ = plane_mask<0>(s_.b ^ (X_ & ~LT_));\n"
+                  << "    u32 par_ = row_xor(h_);\n";
+                const std::string wk = n == 1 ? "0u" : "((c.row & 1u) << 4)";
+                o << "    u32 klo_ = row_min_u32(((l_ & 0xFFu) << 24) | " << wk << " | ln.br);\n"
+                  << "    u32 khi_ = row_min_u32((((l_ >> 16) & 0xFFu) << 24) | " << wk << " | ln.br);\n";
+                if (n == 2)
+                    o << "    { const X2 p_ = swap16(par_); par_ = p_.a ^ p_.b;\n"
+                         "      const X2 a_ = swap16(klo_), b_ = swap16(khi_);\n"
+                         "      klo_ = __builtin_elementwise_min(a_.a, a_.b); khi_ = __builtin_elementwise_min(b_.a, b_.b); }\n";
+                const std::string wsel_lo = n == 1 ? "true" : "((klo_ >> 4) & 1u) == (c.row & 1u)";
+                const std::string wsel_hi = n == 1 ? "true" : "((khi_ >> 4) & 1u) == (c.row & 1u)";
+                o << "    const bool flo_ = land(land(par_ & 0x8000u, (klo_ & 15u) == ln.br), " << wsel_lo << ");\n"
+                  << "    const bool fhi_ = land(land(par_ & 0x80000000u, (khi_ & 15u) == ln.br), " << wsel_hi << ");\n"
+                  << "    " << x << " = h_ ^ sel(flo_, 0xFFFFu, 0u) ^ sel(fhi_, 0xFFFF0000u, 0u);\n  }\n";
+            }
+            (n == 1 ? small1 : small2)[op.pos] = x;
+            break;
+        }
+        case POLAR_OP_H:
+        case POLAR_OP_H0: {
+            const bool h = op.code == POLAR_OP_H;
+            if (n == 1) {
+                // node of 2 words at pos: row r holds word r & 1 = [xL ^ xR, xR]
+                const std::string x = var("x"), R = small1.at(op.pos + 1);
+                o << "  const u32 " << x << " = " << R;
+                if (h) o << " ^ (" << small1.at(op.pos) << " & row_even(c.row))";
+                o << ";   // " << (h ? "H" : "H0") << " n 1\n";
+                small2[op.pos] = x;
+            } else {
+                // node of 4 words at pos: row r holds word r, into the partial sums at local pos / 4
+                const std::string R = small2.at(op.pos + 2);
+                o << "  { // " << (h ? "H" : "H0") << " n 2\n    const u32 x4_ = " << R;
+                if (h) o << " ^ (" << small2.at(op.pos) << " & row_lo2(c.row))";
+                o << ";\n";
+                put(op.pos / 4, 1, "x4_ & 0x00010001u");
+                o << "  }\n";
+            }
+            break;
+        }
+        default:
+            throw std::runtime_error("pairgen: unexpected small op");
+        }
+    }
+
+    void op(const polar_sc_op &op)
+    {
+        const int pd = LG - op.level, cd = pd - 1;
+        fence();
+        if (op.code == POLAR_OP_H || op.code == POLAR_OP_H0) {
+            // H of a node of 2n words: small when the node is 2 or 4 words
+            if (op.n <= 2) small_op(op, pd, cd);
+            else big_op(op, pd, cd, op.n / 4);
+            return;
+        }
+        if (op.n >= 4) big_op(op, pd, cd, op.n / 4);
+        else small_op(op, pd, cd);
+    }
+
+    // subtree decoder `id`: root words from slot rows src_[64 j] (SM8 pairs), partial sums to
+    // the pair's bit dwords from local word l0
+    void sub_function(int id)
+    {
+        const int words = 1 << LG, R = regs(LG), nbw = words / 4 >= 16 ? words / 64 : 1;
+        // (plain arguments: a PairCtx passed by reference would live on the private stack)
+        o << "__device__ __noinline__ void polar_psub_" << id << "(const u16 *src_, u32 *hb_, int l0)\n{\n"
+          << "  const u32 lane_ = threadIdx.x & 63u;\n  Lanes ln; ln.init(lane_ & 15u);\n"
+          << "  struct { u32 row; } c; c.row = lane_ >> 4;\n  u32 bw[" << nbw << "] = {};\n";
+        bool split_root = false;   // REP / R1 / SPC children of the root read split root words
+        for (const polar_sc_op &op : ops)
+            if (op.level == 0 && (op.code == POLAR_OP_REP || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC))
+                split_root = true;
+        for (int d = 0; d <= LG; d++)
+            if (d < LG || split_root)
+                o << "  u32 m" << d << "[" << regs(d) << "], s" << d << "[" << planes(regs(d)) << "];\n";
+        (void)R;
+        for (const polar_sc_op &op : ops) {
+            if (op.code == POLAR_OP_END) break;
+            this->op(op);
+        }
+        if (words / 4 >= 16) {
+            for (int j = 0; j < nbw; j++) o << "  BST(" << j << ", bw[" << j << "]);\n";
+        } else {
+            const unsigned m = (1u << (words / 4)) - 1u;
+            o << "  BSTM(0x" << std::hex << (m | (m << 16)) << std::dec << "u, bw[0]);\n";
+        }
+        o << "}\n\n";
+    }
+};
+// a root word of a subtree decoder: SM8 pair of its stage slot row -> SM16
+// partial-sum dword d of the subtree to the pair's bits (masked: subtrees of < 64 words)
+const char *const kPairCH = "#define CH(j) slot_unpack((u32)src_[(j) * 64])\n"
+                            "#define BST(d, v) (hb_[((l0 >> 4) + (d)) * 64] = (v))\n"
+                            "#define BSTM(m, v) (hb_[(l0 >> 4) * 64] = (hb_[(l0 >> 4) * 64] & ~((m) << (l0 & 15))) | \\\n"
+                            "    (((v) << (l0 & 15)) & ((m) << (l0 & 15))))\n";
+
+// upper-level record -> call of a polar_sc_pair.h loop function
+void upper_call(std::ostringstream &o, const polar_sc_op &op)
+{
+    const int n4 = op.n / 4, l0 = op.pos / 4, ub = op.upos >= 0 ? op.upos / 4 : -1;
+    o << "    c.sync(); ";
+    switch (op.code) {
+    case POLAR_OP_F: o << "pop_fg_split<false>(c, " << op.level << ", " << n4 << ", -1);"; break;
+    case POLAR_OP_G: o << "pop_fg_split<true>(c, " << op.level << ", " << n4 << ", " << ub << ");"; break;
+    case POLAR_OP_REP: o << "if (c.lead) pop_rep(c, " << op.level << ", " << n4 << ", " << l0 << ");"; break;
+    case POLAR_OP_R1: o << "pop_r1spc<false>(c, " << op.level << ", " << n4 << ", " << ub << ", " << l0 << ");"; break;
+    case POLAR_OP_SPC: o << "pop_r1spc<true>(c, " << op.level << ", " << n4 << ", " << ub << ", " << l0 << ");"; break;
+    case POLAR_OP_H: o << "pop_h<false>(c, " << l0 << ", " << n4 << ");"; break;
+    case POLAR_OP_H0: o << "pop_h<true>(c, " << l0 << ", " << n4 << ");"; break;
+    case POLAR_OP_SUB:
+        o << "if (c.lead) polar_psub_" << op.fb << "(c.slot_ptr(c.lvl_row(" << op.level << ")), c.hb, " << l0 << ");";
+        break;
+    default: throw std::runtime_error("pairgen: unexpected upper op");
+    }
+    o << "   // " << op.code << " level " << op.level << " n " << op.n << " pos " << op.pos << "\n";
+}
+
+// one decode kernel: a block of W waves per frame pair; `seg` selects the schedule segment
+// (the cases between POLAR_OP_SEGEND records; 0 when the plan has no grid tier)
+void pair_kernel(std::ostringstream &o, const char *name, const std::vector<polar_sc_op> &ops)
+{
+    o << "extern \"C\" __global__ void __launch_bounds__(" << 64 * PAIR_WAVES_MAX << ") " << name << "(\n"
+      << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, unsigned int *__restrict__ scratch,\n"
+      << "    int N, int batch, int out_stride, int pair_dwords, int slot_rows, int lds_row0, int seg)\n{\n"
+      << "  extern __shared__ __attribute__((aligned(16))) unsigned short smem_[];\n"
+      << "  PairCtx c;\n"
+      << "  const int W = blockDim.x >> 6, wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+      << "  const long pair = blockIdx.x;\n"
+      << "  if (2 * pair >= batch) return;\n"
+      << "  pair_init(c, llr, scratch, N, batch, pair, pair_dwords, slot_rows, lds_row0, wi, W, (lds_u16 *)smem_);\n"
+      << "  switch (seg) {\n  case 0:\n";
+    int seg = 0;
+    for (const polar_sc_op &op : ops) {
+        if (op.code == POLAR_OP_END) break;
+        if (op.code == POLAR_OP_SEGEND) {
+            o << "    return;\n  case " << ++seg << ":\n";
+            continue;
+        }
+        upper_call(o, op);
+    }
+    o << "    c.sync();\n"
+      << "    pair_out(c, out + (2 * pair) * (long)out_stride, out + (2 * pair + 1) * (long)out_stride, 2 * pair < batch,\n"
+      << "             2 * pair + 1 < batch, out_stride);\n"
+      << "    return;\n  default: return;\n  }\n}\n";
+}
+
+}  // namespace
+
+// The whole generated source of a pair plan: subtree decoders, the decode kernel (one case
+// per schedule segment of the grid tier, or one), the tier kernel.
+std::string pair_source(const polar_sc_plan &p)
+{
+    std::ostringstream o;
+    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits << "\n#include \"polar_sc_pair.h\"\n"
+      << "namespace polar {\n" << kPairCH;
+    int lg = 0;
+    while ((1 << lg) < p.sub_words) lg++;
+    for (size_t id = 0; id < p.subs.size(); id++) {
+        PairGen g(p.subs[id], lg);
+        g.sub_function((int)id);
+        o << g.o.str();
+    }
+    o << "}  // namespace polar\nusing namespace polar;\n";
+    // the decode kernel over the whole schedule, and (grid-tier plans) the segment kernel
+    pair_kernel(o, "polar_sc_pair_kernel", p.pair_ops);
+    // test hook (polar_sc_debug_subtree): subtree decoder `id` on 64 lanes of root slot rows
+    // in[64 j + lane], its partial-sum dwords to out[64 d + lane]
+    o << "extern \"C\" __global__ void __launch_bounds__(64) polar_sc_pair_subtest_kernel(\n"
+      << "    const unsigned short *__restrict__ in, unsigned int *__restrict__ out, int id)\n{\n"
+      << "  const int lane = threadIdx.x & 63;\n  switch (id) {\n";
+    for (size_t id = 0; id < p.subs.size(); id++)
+        o << "  case " << id << ": polar_psub_" << id << "(in + lane, out + lane, 0); return;\n";
+    o << "  default: return;\n  }\n}\n";
+    if (!p.pair_tier.steps.empty()) {
+        pair_kernel(o, "polar_sc_pair_seg_kernel", p.pair_tier.seg_ops);
+        o << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_pair_tier_kernel(\n"
+          << "    const signed char *__restrict__ llr, unsigned int *__restrict__ scratch, int N, int batch, int pair_dwords,\n"
+          << "    int slot_rows, int code_g, int k, int n4, int ub, int cw)\n{\n"
+          << "  pair_tier_body(llr, scratch, N, batch, pair_dwords, slot_rows, code_g, k, n4, ub, cw);\n}\n";
+    }
+    return o.str();
+}
+
+}  // namespace polar_host

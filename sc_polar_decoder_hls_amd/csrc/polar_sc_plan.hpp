@@ -22,6 +22,8 @@ struct DevState {
     hipFunction_t fn = nullptr;
     hipFunction_t fn_trace = nullptr;   // hybrid plans: the per-op monitor variant
     hipFunction_t fn_tier = nullptr;    // grid-tier plans: upper-level F / G over all groups
+    hipFunction_t fn_seg = nullptr;     // pair plans with a grid tier: the segment kernel
+    hipFunction_t fn_subtest = nullptr; // pair plans: one generated subtree decoder (test hook)
     void *seg_ops[2] = {nullptr, nullptr};   // grid-tier plans: the segment schedules per tier plan
     hipModule_t imodule = nullptr;      // per-mask plans with llr_bits != 6: hipRTC interpreter
     hipFunction_t ifn_trace = nullptr;  //   (per-op monitor only)
@@ -69,6 +71,19 @@ constexpr uint32_t FB_EXACT = 1u << 19;
 // spilled subtree code) failed to launch (HSA_STATUS_ERROR_INVALID_ISA).
 constexpr int HYBRID_MAX_WAVES = 8;
 
+// pair plans (polar_sc_pair.h): at most this many waves per frame pair (512-thread blocks,
+// <= 256 VGPRs per wave), subtrees of at most PAIR_SUB_WORDS words in registers
+constexpr int PAIR_WAVES_MAX = 8;
+constexpr int PAIR_SUB_WORDS = 256;
+
+// grid tier of a pair plan: `seg_ops` is the upper schedule with POLAR_OP_SEGEND where the grid
+// launches of `steps` (grid records) run; steps alternate with the segment kernel's cases
+struct PairTier {
+    int tw = 0;
+    std::vector<TierStep> steps;       // grid: op; segment: off = segment index (the kernel's `seg`)
+    std::vector<polar_sc_op> seg_ops;
+};
+
 }  // namespace polar_host
 
 struct polar_sc_plan {
@@ -106,6 +121,14 @@ struct polar_sc_plan {
     // (when it differs): the root only, taken by batches with a frame group per CU or more
     // (polar_sc_jit.cpp launch_tier). Empty: single-kernel decode.
     std::vector<polar_host::TierPlan> tiers;
+    // pair plans (N >= 2048, shipped datapath; polar_sc_pairgen.cpp): one frame pair per wave,
+    // subtrees of sub_words words as generated register code (subs), the upper levels as
+    // loops over stage-slot rows (pair_ops); optional grid tier (pair_tier.steps non-empty)
+    int pair = 0;
+    std::vector<polar_sc_op> pair_ops;
+    polar_host::PairTier pair_tier;
+    int pair_slot_rows = 0;          // stage-slot rows per pair (levels of nodes G/2 .. sub_words)
+    int pair_dwords = 0;             // HBM scratch per pair: slot rows (128 B) + bit dwords (256 B)
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;
     mutable std::mutex host_mu;                             // polar_sc_decode_host staging
@@ -120,6 +143,9 @@ namespace polar_host {
 // per-mask kernel: generate source, compile with hipRTC for gfx950 (host only), load it on
 // the current device, launch it
 std::string jit_source(const polar_sc_plan &p);
+std::string pair_source(const polar_sc_plan &p);
+int jit_launch_pair(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
+                    int out_stride, void *stream);
 int jit_compile(const polar_sc_plan &p);                 // fills p.jit_code (idempotent)
 int jit_load(const polar_sc_plan &p, DevState &st);      // module + function on this device
 int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out,

@@ -40,7 +40,7 @@ def test_tuning_validation_and_no_environment(pkg, monkeypatch):
     """polar_sc_tuning: out-of-range fields -> -EINVAL; the plan (and its generated kernel
     source) depends on the mask, config and tuning only, never on the environment."""
     m = util.mask("FB_N1024_K512")
-    for bad in ({"kernel": 2}, {"waves_per_group": 3}, {"waves_per_group": 32}, {"sub_words": 256},
+    for bad in ({"kernel": 4}, {"waves_per_group": 3}, {"waves_per_group": 32}, {"sub_words": 512},
                 {"tier_words": -2}, {"tier_words": 1000}, {"lds_slots": 300}, {"hybrid_waves": 16}):
         with pytest.raises(pkg.PolarError) as e:
             pkg.Decoder(m, tuning=bad)

@@ -31,6 +31,12 @@ def test_dpp_row_exchange(pkg, cuda):
     lanes = np.arange(64)
     for h in range(4):
         np.testing.assert_array_equal(t[h], lanes ^ (1 << h), err_msg="xorlane<%d>" % (1 << h))
+    # frame-pair layout (polar_sc_pair.h swap16 / swap32): rows (x0 x1 x2 x3) ->
+    # (x0 x0 x2 x2), (x1 x1 x3 x3) and (x0 x1 x0 x1), (x2 x3 x2 x3)
+    np.testing.assert_array_equal(t[4], lanes & ~16, err_msg="permlane16_swap a")
+    np.testing.assert_array_equal(t[5], lanes | 16, err_msg="permlane16_swap b")
+    np.testing.assert_array_equal(t[6], lanes & ~32, err_msg="permlane32_swap a")
+    np.testing.assert_array_equal(t[7], lanes | 32, err_msg="permlane32_swap b")
 
 
 @pytest.mark.parametrize("name", ["FB_N128_K64", "FB_N256_K128", "FB_N512_K256", "FB_N1024_K512",

@@ -1,0 +1,217 @@
+"""Pair plans (polar_sc_pair.h, polar_sc_pairgen.cpp): one frame pair per wave, four words per
+register, generated subtree decoders of up to 256 words, upper levels as loops over stage-slot
+rows (LDS or HBM), optional grid tier.
+
+CPU tests: plan statistics, hipRTC compilation of the generated source.
+GPU tests: bit-exact against the oracle (literal my_module FSM) on reference masks and on
+structured masks that put R0 / R1 / REP / SPC nodes at every size (the cross-row steps of the
+nodes of 1, 2 and 4 words), for every waves-per-pair count, subtree size, LDS / HBM slot
+placement and with the grid tier."""
+import functools
+
+import numpy as np
+import pytest
+
+import util
+from test_gpu_parity import _assert_same
+
+
+def pair(pkg, mask, **tuning):
+    return pkg.Decoder(mask, tuning=dict(tuning, kernel=3))
+
+
+def structured_mask(rng, N, p_special=0.7):
+    """Nodes of random size whose frozen pattern is R0 / R1 / REP / SPC (or random), so that the
+    pruned node ops appear at every level (1 .. N/64 words)."""
+    m = (rng.random(N) < 0.5).astype(np.uint8)
+    pos = 0
+    while pos < N:
+        size = 16 << int(rng.integers(0, 6))
+        size = min(size, N - pos)
+        if rng.random() < p_special:
+            kind = int(rng.integers(0, 4))
+            blk = np.zeros(size, np.uint8)
+            if kind == 1:
+                blk[:] = 1                  # R1
+            elif kind == 2:
+                blk[-1] = 1                 # REP
+            elif kind == 3:
+                blk[:] = 1
+                blk[0] = 0                  # SPC
+            m[pos:pos + size] = blk
+        pos += size
+    return m
+
+
+@functools.lru_cache(maxsize=None)
+def struct_masks(N):
+    rng = np.random.default_rng(N)
+    return tuple(structured_mask(rng, N) for _ in range(3))
+
+
+@functools.lru_cache(maxsize=None)
+def wave_mask():
+    return structured_mask(np.random.default_rng(4242), 16384, 0.9)
+
+
+PARITY_MASKS = [("frozen_n_2048_k_1024", 23), ("FB_N2048_K1024", 8), ("frozen_n_4096_k_2048", 17),
+                ("frozen_n_8192_k_4096", 9), ("frozen_n_16384_k_8192", 7), ("frozen_n_32768_k_29492", 5),
+                ("frozen_n_2048_k_1844", 12), ("frozen_n_16384_k_14746", 6), ("frozen_n_65536_k_32768", 5)]
+STRUCT_SUB_WORDS = (16, 64, 256)
+
+
+def struct_sub_words(N):
+    return [sw for sw in STRUCT_SUB_WORDS if sw <= N // 32]   # subtrees of at most half the code
+
+
+def gpu_plans():
+    """(name, mask, tuning) of every plan the GPU tests below decode with: their hipRTC code
+    objects are compiled ahead by __graft_entry__.build() (the GPU box loads them from the
+    in-tree cache instead of compiling)."""
+    out = [(n, util.mask(n), {"kernel": 3}) for n, _ in PARITY_MASKS]
+    for N in (2048, 8192, 32768):
+        for i, m in enumerate(struct_masks(N)):
+            out += [("struct%d_%d" % (N, i), m, {"kernel": 3, "sub_words": sw}) for sw in struct_sub_words(N)]
+    out += [("frozen_n_2048_k_1024", util.mask("frozen_n_2048_k_1024"), {"kernel": 3, "sub_words": sw})
+            for sw in (16, 32, 64)]
+    out += [("frozen_n_8192_k_4096", util.mask("frozen_n_8192_k_4096"), {"kernel": 3, "sub_words": 256}),
+            ("frozen_n_16384_k_8192", util.mask("frozen_n_16384_k_8192"), {"kernel": 3, "sub_words": 64}),
+            ("wave_mask", wave_mask(), {"kernel": 3, "sub_words": 64}),
+            ("frozen_n_32768_k_29492", util.mask("frozen_n_32768_k_29492"),
+             {"kernel": 3, "tier_words": 512, "sub_words": 128}),
+            ("frozen_n_262144_k_131072", util.mask("frozen_n_262144_k_131072"), {"kernel": 3}),
+            ("frozen_n_262144_k_131072", util.mask("frozen_n_262144_k_131072"), {"kernel": 3, "tier_words": 1024})]
+    return out
+
+
+def run(pkg, torch, dec, llr):
+    out = dec.decode(torch.from_numpy(np.ascontiguousarray(llr)).cuda())
+    torch.cuda.synchronize()
+    return pkg.unpack_bits(out.cpu().numpy(), dec.N)
+
+
+def test_pair_plan_stats(pkg):
+    s = pair(pkg, util.mask("frozen_n_65536_k_32768")).stats
+    assert (s["kernel"], s["sub_words"], s["storage"]) == (3, 256, 1)
+    assert s["n_sub_calls"] >= s["n_sub_kinds"] > 0 and s["tier_steps"] == 0
+    # per pair: (G - S) / 4 slot rows of 128 B + G / 64 bit rows of 256 B
+    assert s["scratch_bytes_per_wave"] == (4096 - 256) // 4 * 128 + 4096 // 64 * 256
+    s = pair(pkg, util.mask("frozen_n_2048_k_1024")).stats
+    assert s["sub_words"] == 64
+    s = pair(pkg, util.mask("frozen_n_262144_k_131072"), tier_words=1024).stats
+    assert s["tier_words"] == 1024 and s["tier_steps"] > 20
+    with pytest.raises(pkg.PolarError):
+        pair(pkg, util.mask("frozen_n_4096_k_2048"), sub_words=256)   # > G / 2
+
+
+@pytest.mark.parametrize("N", [2048, 8192])
+def test_pair_generated_code_emulated(pkg, oracle_mod, N):
+    """CPU: the generated subtree decoders transpiled and run on emulated 64-lane waves
+    (tests/pair_emu.py: DPP rows, permlane swaps) with the upper levels restated on the same
+    layout decode bit-exactly like the oracle -- structured masks, every subtree size."""
+    import pair_emu
+    for i, mask in enumerate(struct_masks(N)):
+        llr, _ = util.synth_frames(mask, 2, ebn0_db=0.5, seed=i)
+        ref = oracle_mod.decode_fsm(mask, llr)
+        for sw in struct_sub_words(N):
+            dec = pair(pkg, mask, sub_words=sw)
+            _assert_same(pair_emu.decode(dec, llr), ref, "emulated N=%d mask %d S=%d" % (N, i, sw))
+    mask = util.mask("frozen_n_2048_k_1024")
+    rng = np.random.default_rng(2)
+    u = rng.integers(0, 2, size=(4, mask.size), dtype=np.uint8) & mask[None, :]
+    x = util.encode_np(u)
+    llr = np.where(x == 1, -9, 9).astype(np.int8)
+    for sw in (16, 32, 64):
+        assert (pair_emu.decode(pair(pkg, mask, sub_words=sw), llr) == x).all()
+
+
+@pytest.mark.gpu
+def test_pair_subtrees_equal_emulation(pkg, cuda):
+    """Every generated subtree decoder on the device (polar_sc_debug_subtree) equals its CPU
+    emulation on random root LLRs."""
+    import pair_emu
+    rng = np.random.default_rng(5)
+    for name, sw in (("frozen_n_2048_k_1024", 64), ("frozen_n_2048_k_1024", 16), ("frozen_n_8192_k_4096", 256)):
+        dec = pair(pkg, util.mask(name), sub_words=sw)
+        subs = pair_emu.Sub(dec.kernel_source(), dec.stats["n_sub_kinds"])
+        for sid in range(dec.stats["n_sub_kinds"]):
+            rows = pair_emu.random_rows(rng, sw)
+            got = dec.debug_subtree(sid, rows)
+            ref = pair_emu.run_sub(dec, sid, rows, subs)
+            assert (got == ref).all(), "%s S=%d subtree %d" % (name, sw, sid)
+
+
+@pytest.mark.parametrize("sub_words", [16, 128])
+def test_pair_source_compiles(pkg, sub_words):
+    """hipRTC build of a generated pair source (host only)."""
+    dec = pair(pkg, util.mask("frozen_n_8192_k_4096"), sub_words=sub_words)
+    assert dec.compile()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,batch", PARITY_MASKS)
+def test_pair_parity_masks(pkg, cuda, oracle_mod, name, batch):
+    mask = util.mask(name)
+    llr, _ = util.synth_frames(mask, batch, ebn0_db=1.0, seed=batch)
+    _assert_same(run(pkg, cuda, pair(pkg, mask), llr), oracle_mod.decode_fsm(mask, llr), name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [2048, 8192, 32768])
+def test_pair_parity_structured(pkg, cuda, oracle_mod, N):
+    """R0 / R1 / REP / SPC nodes of every size, AWGN and edge LLRs (zeros, -32, saturated)."""
+    rng = np.random.default_rng(N + 1)
+    for rep, mask in enumerate(struct_masks(N)):
+        llr, _ = util.synth_frames(mask, 6, ebn0_db=0.5, seed=rep)
+        edge = rng.choice(np.array([0, 0, 1, -1, 31, -31, -32, 5], np.int8), size=(3, N))
+        llr = np.concatenate([llr, edge])
+        for sw in struct_sub_words(N):
+            dec = pair(pkg, mask, sub_words=sw)
+            _assert_same(run(pkg, cuda, dec, llr), oracle_mod.decode_fsm(mask, llr), "N=%d rep %d S=%d" % (N, rep, sw))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wpg", [1, 2, 4, 8])
+def test_pair_waves_per_pair(pkg, cuda, oracle_mod, wpg):
+    """W waves per frame pair split the upper F / G / R1 / SPC / H ops (the SPC partials meet
+    in LDS); subtrees and REP run on the lead wave."""
+    for name in ("frozen_n_16384_k_8192", None):
+        mask = util.mask(name) if name else wave_mask()
+        llr, _ = util.synth_frames(mask, 7, ebn0_db=1.0, seed=wpg)
+        dec = pair(pkg, mask, waves_per_group=wpg, sub_words=64)
+        _assert_same(run(pkg, cuda, dec, llr), oracle_mod.decode_fsm(mask, llr), "%s W=%d" % (name, wpg))
+
+
+@pytest.mark.gpu
+def test_pair_all_hbm_slots_large_batch(pkg, cuda, oracle_mod):
+    """A batch large enough that no slot level fits the LDS share of a pair (every level in
+    HBM): equal to the hybrid kernel on every frame and to the oracle on a sample."""
+    mask = util.mask("frozen_n_2048_k_1024")
+    B = 40001
+    llr, _ = util.synth_frames(mask, B, ebn0_db=1.5, seed=3)
+    got = run(pkg, cuda, pair(pkg, mask), llr)
+    ref = run(pkg, cuda, pkg.Decoder(mask, tuning={"kernel": 2}), llr)
+    _assert_same(got, ref, "pair vs hybrid")
+    idx = np.r_[0:40, B - 40:B]
+    _assert_same(got[idx], oracle_mod.decode_fsm(mask, llr[idx]), "pair vs oracle")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 4, 9])
+def test_pair_grid_tier(pkg, cuda, oracle_mod, batch):
+    """Grid tier forced at 512 words on N = 32768 (ragged batches): grid launches of the upper
+    F / G over all pairs, the segments in between."""
+    mask = util.mask("frozen_n_32768_k_29492")
+    llr, _ = util.synth_frames(mask, batch, ebn0_db=3.0, seed=batch)
+    dec = pair(pkg, mask, tier_words=512, sub_words=128)
+    assert dec.stats["tier_steps"] > 0
+    _assert_same(run(pkg, cuda, dec, llr), oracle_mod.decode_fsm(mask, llr), "tier batch %d" % batch)
+
+
+@pytest.mark.gpu
+def test_pair_c5_sample(pkg, cuda, oracle_mod):
+    mask = util.mask("frozen_n_262144_k_131072")
+    llr, _ = util.synth_frames(mask, 3, ebn0_db=1.0, seed=5)
+    ref = oracle_mod.decode_fsm(mask, llr)
+    _assert_same(run(pkg, cuda, pair(pkg, mask), llr), ref, "C5 pair")
+    _assert_same(run(pkg, cuda, pair(pkg, mask, tier_words=1024), llr), ref, "C5 pair tier")
