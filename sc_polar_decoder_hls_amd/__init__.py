@@ -119,6 +119,13 @@ def lib():
     if not os.path.exists(_build.LIB):
         raise RuntimeError("libpolar_sc.so is not built (%s); run sc_polar_decoder_hls_amd.build() "
                            "or __graft_entry__.build()" % _build.LIB)
+    # torch first: its bundled HIP runtime is then the one the library binds to (loaded the
+    # other way round, the process would hold two HIP runtimes and the library would see no
+    # device once torch initialises its own)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(_build.LIB)
     p, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
     sig = {

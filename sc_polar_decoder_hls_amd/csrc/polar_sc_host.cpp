@@ -480,12 +480,20 @@ int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
 // held: if non-null, receives the plan lock (still held on success) so that the caller can
 // launch with the scratch pointer it was given before another thread may reallocate it
 enum DevMode { DEV_DECODE, DEV_TRACE, DEV_I16 };
+// HIP failure inside the library: -EIO, and the HIP error on stderr when POLAR_SC_VERBOSE is set
+int hip_fail(const char *what, hipError_t e)
+{
+    static const bool verbose = std::getenv("POLAR_SC_VERBOSE") != nullptr;
+    if (verbose) std::fprintf(stderr, "polar_sc: %s: %s\n", what, hipGetErrorString(e));
+    return -EIO;
+}
+
 int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, DevMode mode = DEV_DECODE,
                   std::unique_lock<std::mutex> *held = nullptr)
 {
     const bool interp = mode != DEV_DECODE;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return -EIO;
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return hip_fail("hipGetDevice", e);
     std::unique_lock<std::mutex> lk(p->mu);
     DevState &st = p->dev[dev];
     if (st.simds == 0) {
@@ -511,7 +519,8 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, DevMode 
         dops.push_back(dops.back());
         size_t bytes = dops.size() * sizeof(polar_sc_op);
         if (hipMalloc(&st.ops, bytes) != hipSuccess) return -ENOMEM;
-        if (hipMemcpy(st.ops, dops.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+        if (hipError_t e = hipMemcpy(st.ops, dops.data(), bytes, hipMemcpyHostToDevice); e != hipSuccess)
+            return hip_fail("schedule upload", e);
     }
     if (mode == DEV_I16 && !p->ops16.empty() && !st.ops16) {
         std::vector<polar_sc_op> dops = p->ops16;
@@ -1137,12 +1146,16 @@ int polar_sc_debug_subtree(const polar_sc_plan *p, uint32_t id, const uint16_t *
     if (id >= p->subs.size()) return -EINVAL;
     DevState *st = nullptr;
     int rc = ensure_device(p, 1, &st);
-    if (rc) return rc;
+    if (rc) {
+        std::fprintf(stderr, "polar_sc_debug_subtree: device setup failed (%d): %s\n", rc, p->jit_log.c_str());
+        return rc;
+    }
     int i = (int)id;
     void *args[] = {(void *)&in_dev, (void *)&out_dev, (void *)&i};
-    if (hipModuleLaunchKernel(st->fn_subtest, 1, 1, 1, 64, 1, 1, 0, nullptr, args, nullptr) != hipSuccess)
-        return -EIO;
-    return hipDeviceSynchronize() == hipSuccess ? 0 : -EIO;
+    hipError_t e = hipModuleLaunchKernel(st->fn_subtest, 1, 1, 1, 64, 1, 1, 0, nullptr, args, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) std::fprintf(stderr, "polar_sc_debug_subtree: %s\n", hipGetErrorString(e));
+    return e == hipSuccess ? 0 : -EIO;
 }
 
 int polar_sc_selftest_lanes(uint32_t *out_dev)

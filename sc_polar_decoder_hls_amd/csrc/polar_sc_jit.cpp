@@ -734,12 +734,21 @@ int jit_load(const polar_sc_plan &p, DevState &st)
 {
     if (st.fn) return 0;
     int rc = jit_compile(p);
-    if (rc) return rc;
-    if (hipModuleLoadData(&st.module, p.jit_code.data()) != hipSuccess) return -EIO;
+    if (rc) {
+        std::fprintf(stderr, "polar_sc: hipRTC build failed (%d)%s%s\n", rc, p.jit_log.empty() ? "" : ":\n",
+                     p.jit_log.c_str());
+        return rc;
+    }
+    if (hipError_t e = hipModuleLoadData(&st.module, p.jit_code.data()); e != hipSuccess) {
+        std::fprintf(stderr, "polar_sc: hipModuleLoadData: %s\n", hipGetErrorString(e));
+        return -EIO;
+    }
     if (p.pair) {
-        if (hipModuleGetFunction(&st.fn, st.module, "polar_sc_pair_kernel") != hipSuccess) return -EIO;
-        if (hipModuleGetFunction(&st.fn_subtest, st.module, "polar_sc_pair_subtest_kernel") != hipSuccess)
+        if (hipModuleGetFunction(&st.fn, st.module, "polar_sc_pair_kernel") != hipSuccess ||
+            hipModuleGetFunction(&st.fn_subtest, st.module, "polar_sc_pair_subtest_kernel") != hipSuccess) {
+            std::fprintf(stderr, "polar_sc: pair kernels missing from the code object\n");
             return -EIO;
+        }
         if (!p.pair_tier.steps.empty() &&
             (hipModuleGetFunction(&st.fn_seg, st.module, "polar_sc_pair_seg_kernel") != hipSuccess ||
              hipModuleGetFunction(&st.fn_tier, st.module, "polar_sc_pair_tier_kernel") != hipSuccess))

@@ -352,10 +352,11 @@ struct PairGen {
             } else {
                 // node of 4 words at pos: row r holds word r, into the partial sums at local pos / 4
                 const std::string R = small2.at(op.pos + 2);
-                o << "  { // " << (h ? "H" : "H0") << " n 2\n    const u32 x4_ = " << R;
+                // (block-local names never end in a digit + '_': the small results are x<k>_)
+                o << "  { // " << (h ? "H" : "H0") << " n 2\n    const u32 w_ = " << R;
                 if (h) o << " ^ (" << small2.at(op.pos) << " & row_lo2(c.row))";
                 o << ";\n";
-                put(op.pos / 4, 1, "x4_ & 0x00010001u");
+                put(op.pos / 4, 1, "w_ & 0x00010001u");
                 o << "  }\n";
             }
             break;

@@ -351,6 +351,8 @@ def _stmt(st):
             name, cnt, init = mm.group(1), mm.group(3), mm.group(5)
             if m.group(2) != "u32":
                 _NOWRAP.add(name)
+            if init is not None and re.search(r"\b%s\b" % re.escape(name), init):
+                raise ValueError("pair_emu: %r is read in its own initializer (C++ shadowing)" % name)
             if cnt is not None:
                 out.append("%s = [V(0) for _ in range(%s)]" % (name, cnt))
             elif init is None:

@@ -59,7 +59,7 @@ def test_tuning_validation_and_no_environment(pkg, monkeypatch):
     assert pkg.Decoder(big).stats == st
     assert pkg.Decoder(m, tuning={"kernel": "interp"}).stats["kernel"] == 0
     txt = open(os.path.join(util.ROOT, "sc_polar_decoder_hls_amd", "csrc", "polar_sc_host.cpp")).read()
-    assert "getenv" not in txt
+    assert re.findall(r'getenv\("(\w+)"\)', txt) == ["POLAR_SC_VERBOSE"]   # error detail on stderr only
     txt = open(os.path.join(util.ROOT, "sc_polar_decoder_hls_amd", "csrc", "polar_sc_jit.cpp")).read()
     assert re.findall(r'getenv\("(\w+)"\)', txt) == ["POLAR_SC_RTC_CACHE"]
 
