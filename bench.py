@@ -68,6 +68,12 @@ def kernel_name(stats):
     """The kernel that carries the decode of a plan (polar_sc_plan_stats.kernel / .storage)."""
     if stats["kernel"] == 1:
         return "polar_sc_mask_kernel (per-mask hipRTC kernel)"
+    if stats["kernel"] == 3:
+        k = ("polar_sc_pair_kernel (hipRTC: one frame pair per wave, %d generated %d-LLR subtree decoders, "
+             "upper levels over stage-slot rows)" % (stats["n_sub_kinds"], 16 * stats["sub_words"]))
+        if stats.get("tier_steps"):
+            k += " + grid tier (%d launches per decode)" % stats["tier_steps"]
+        return k
     store = "HBM-scratch" if stats["storage"] == 1 else "LDS"
     if stats["kernel"] == 2:
         k = ("polar_sc_hybrid_kernel (hipRTC: %s interpreter + %d generated %d-LLR subtree decoders)"

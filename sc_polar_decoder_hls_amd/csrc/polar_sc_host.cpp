@@ -812,8 +812,11 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     const bool sub_ok = sub_words >= 2 && sub_words <= 128 && (sub_words & (sub_words - 1)) == 0;
     std::vector<polar_sc_op> dev_sched;
     // pair plans (polar_sc_pair.h): one frame pair per wave, generated subtrees of up to 256
-    // words; polar_sc_tuning.kernel = 3 (2 = the hybrid kernel of 8-frame groups)
-    const bool want_pair = !p->jit && jit_on && !kinds && dflt && p->G >= 128 && t.kernel == 3;
+    // words -- the default for N >= 2048 (same-box A/B against the hybrid kernel of 8-frame
+    // groups, tools/pair_ab.py: C3 1.64 -> 1.16 ms, C5 4.18 -> 1.78, C5 at 64 frames 3.57 ->
+    // 1.55, N = 16384 x 4096 frames 0.39 -> 0.24, N = 4096 x 16384 0.36 -> 0.23);
+    // polar_sc_tuning.kernel = 2 keeps the hybrid kernel
+    const bool want_pair = !p->jit && jit_on && !kinds && dflt && p->G >= 128 && (t.kernel == 3 || t.kernel == 0);
     if (want_pair) {
         int S = std::min<int>(polar_host::PAIR_SUB_WORDS, (int)p->G / 2);
         if (t.sub_words) {

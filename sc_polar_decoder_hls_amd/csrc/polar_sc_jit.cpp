@@ -17,6 +17,7 @@
 
 #include <dlfcn.h>
 #include <sys/stat.h>
+#include <utime.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -644,6 +645,7 @@ bool cache_load(const std::string &path, std::vector<char> &code)
     std::vector<char> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
     if (buf.size() < 4 || std::memcmp(buf.data(), "\x7f" "ELF", 4) != 0) return false;
     code.swap(buf);
+    (void)utime(path.c_str(), nullptr);   // mark as in use (stale entries can be pruned by age)
     return true;
 }
 

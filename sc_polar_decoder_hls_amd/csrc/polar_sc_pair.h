@@ -148,7 +148,9 @@ __device__ __forceinline__ void pfg_rows(const PairCtx &c, int s0, int d0, int n
         if constexpr (ROOT) return c.chan(j);
         else return c.template ld<SL>(s0 + j);
     };
-    constexpr int CH = (ROOT || !SL) ? 16 : 8;   // HBM sources: more loads in flight
+    // rows per batch: HBM sources keep 2 x 32 row loads in flight (a lone wave per SIMD pair
+    // hides the HBM latency only with many loads outstanding), LDS sources 2 x 8
+    constexpr int CH = (ROOT || !SL) ? 32 : 8;
     int j = j0;
     for (; j + CH <= j1; j += CH) {
         u32 a[CH], b[CH], r[CH];

@@ -86,13 +86,13 @@ def test_int16_channel_matches_int8(pkg, cuda, oracle_mod, q):
 
 @pytest.mark.parametrize("name", ["frozen_n_2048_k_1024", "frozen_n_16384_k_8192", "frozen_n_65536_k_32768"])
 def test_int16_channel_hybrid_plans(pkg, cuda, oracle_mod, name):
-    """polar_sc_decode_i16 on plans whose int8 path is the hybrid kernel (generated subtree
-    decoders, grid tier at N = 65536): the int16 interpreter runs the plan's schedule without
-    subtree records and must give the int8 path's bits (it skipped the subtrees)."""
+    """polar_sc_decode_i16 on plans whose int8 path runs generated subtree decoders (the pair
+    kernel): the int16 interpreter runs the plan's schedule without subtree records and must
+    give the int8 path's bits (it skipped the subtrees)."""
     mask = util.mask(name)
     llr, _ = util.synth_frames(mask, 11, ebn0_db=1.5, seed=1616)
     dec = pkg.Decoder(mask)
-    assert dec.stats["kernel"] == 2 and dec.stats["n_sub_calls"] > 0
+    assert dec.stats["kernel"] in (2, 3) and dec.stats["n_sub_calls"] > 0
     a = dec.decode(cuda.from_numpy(llr).cuda())
     b = dec.decode(cuda.from_numpy(llr.astype(np.int16)).cuda())
     cuda.cuda.synchronize()

@@ -15,7 +15,7 @@ import util
 def make(pkg, mask, jit="1", sub_words=None, tier_words=None):
     """Plan with explicit kernel selection (polar_sc_tuning): jit "0" = the schedule
     interpreter; sub_words / tier_words as given (tier_words 0 = no grid tier)."""
-    t = {"kernel": 0 if jit == "1" else 1}
+    t = {"kernel": 2 if jit == "1" else 1}   # the hybrid kernel explicitly (the default for N >= 2048 is the pair kernel)
     if sub_words is not None:
         t["sub_words"] = sub_words
     if tier_words is not None:
@@ -96,9 +96,9 @@ def test_hybrid_source_compiles(pkg, sub_words):
 @pytest.mark.parametrize("q", [5, 8])
 def test_llr_bits_kernels_compile(pkg, q):
     """LLR_BITS 5..8 plans are specialised through POLAR_Q in the hipRTC kernels: the per-mask
-    kernel (N <= 1024), the hybrid kernel (N > 1024) and, for plans that would use the hipcc
+    kernel (N <= 1024), the pair kernel (N >= 2048) and, for plans that would use the hipcc
     interpreter (PRUNING_LEVEL 1 leaf decoders), the interpreter compiled by hipRTC."""
-    for name, pr, kernel in (("FB_N1024_K512", 2, 1), ("frozen_n_4096_k_2048", 2, 2), ("FB_N1024_K512", 1, 2)):
+    for name, pr, kernel in (("FB_N1024_K512", 2, 1), ("frozen_n_4096_k_2048", 2, 3), ("FB_N1024_K512", 1, 2)):
         c = pkg.default_config()
         c.llr_bits, c.pruning_level = q, pr
         dec = pkg.Decoder(util.mask(name), config=c)
