@@ -820,7 +820,8 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     if (want_pair) {
         int S = std::min<int>(polar_host::PAIR_SUB_WORDS, (int)p->G / 2);
         if (t.sub_words) {
-            if (t.sub_words < 16 || (uint32_t)t.sub_words > p->G / 2) {
+            // >= 32 words: the halves of every upper node are whole 8-row slot groups
+            if (t.sub_words < 32 || (uint32_t)t.sub_words > p->G / 2) {
                 delete p;
                 return -EINVAL;
             }

@@ -624,9 +624,10 @@ std::string cache_path(const std::string &src)
     if (dir.empty()) return "";
     uint64_t h = 1469598103934665603ull;
     h = fnv1a(h, src.data(), src.size());
+    // the embedded headers the source includes (interp.h and pair.h include device.h only)
     h = fnv1a(h, kPolarDeviceSrc, sizeof kPolarDeviceSrc);
-    h = fnv1a(h, kPolarInterpSrc, sizeof kPolarInterpSrc);
-    h = fnv1a(h, kPolarPairSrc, sizeof kPolarPairSrc);
+    if (src.find("\"polar_sc_interp.h\"") != std::string::npos) h = fnv1a(h, kPolarInterpSrc, sizeof kPolarInterpSrc);
+    if (src.find("\"polar_sc_pair.h\"") != std::string::npos) h = fnv1a(h, kPolarPairSrc, sizeof kPolarPairSrc);
     for (const char *o : kRtcOpts) h = fnv1a(h, o, std::strlen(o) + 1);
     int ver_major = 0, ver_minor = 0;
     hiprtcVersion(&ver_major, &ver_minor);

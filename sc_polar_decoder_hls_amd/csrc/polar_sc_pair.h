@@ -21,8 +21,12 @@
 //   * partial sums (bit_mem): per lane, "local word" l = w / 4 of row r; dword d holds local
 //     words 16 d .. 16 d + 15 (bit j low frame, bit 16 + j high frame);
 //   * upper levels (nodes wider than the register-resident subtree of S words): one stage
-//     slot per level, a slot row = 64 lanes x u16 (SM8 pairs: low / high frame byte) = 4 words
-//     of the pair; levels of nodes <= lds_words words sit in LDS, wider ones in HBM scratch.
+//     slot per level; a slot row = 4 words of the pair, stored by row pairs: the slot dword of
+//     rows 2 i, 2 i + 1 of a lane holds the SM8 bytes (row 2 i frame lo, row 2 i + 1 lo, row 2 i
+//     hi, row 2 i + 1 hi), and the four dwords of row pairs 4 g .. 4 g + 3 of a lane are
+//     contiguous (16 B per lane, 1 KB per group of 8 rows: one dwordx4 / b128 access per lane);
+//     levels of nodes <= lds_words words sit in LDS, wider ones in HBM scratch. The upper F / G run on those four bytes at once (SWAR
+//     below) while two magnitudes fit 7 bits (Q <= 7).
 #pragma once
 
 #include "polar_sc_device.h"
@@ -32,6 +36,12 @@ namespace polar {
 typedef unsigned short u16;
 typedef __attribute__((address_space(3))) u16 lds_u16;
 typedef __attribute__((address_space(3))) u32 lds_w32;
+typedef __attribute__((address_space(1))) u32 g_u32;
+typedef __attribute__((address_space(1))) unsigned char g_u8;
+typedef __attribute__((address_space(1))) unsigned short g_u16;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
 // ---------------------------------------------------------------------------------------
 // cross-row exchange (gfx950 v_permlane16_swap_b32 / v_permlane32_swap_b32 with both
@@ -70,47 +80,162 @@ __device__ __forceinline__ bool land(bool a, bool b) { return a && b; }
 __device__ __forceinline__ u32 row_even(u32 row) { return (row & 1u) ? 0u : 0xFFFFFFFFu; }   // rows 0, 2
 __device__ __forceinline__ u32 row_lo2(u32 row) { return row < 2u ? 0xFFFFFFFFu : 0u; }       // rows 0, 1
 
+constexpr int PAIR_MAX_WAVES = 8;   // launch bound 512 threads: <= 256 VGPRs per wave
+
+// ---------------------------------------------------------------------------------------
+// slot dwords (row pairs, SM8 bytes lo_even, lo_odd, hi_even, hi_odd)
+// ---------------------------------------------------------------------------------------
+// row (odd ? 2 i + 1 : 2 i) of a slot dword as the SM16 pair of the register code
+__device__ __forceinline__ u32 prow(u32 d, bool odd)
+{
+    return __builtin_amdgcn_perm(d, d, odd ? 0x03030101u : 0x02020000u) & ((0x8000u | QMAG) * 0x00010001u);
+}
+// two SM16 pairs (rows 2 i, 2 i + 1) -> slot dword
+__device__ __forceinline__ u32 ppack(u32 v0, u32 v1)
+{
+    const u32 t0 = (v0 & (QMAG * 0x00010001u)) | ((v0 >> 8) & 0x00800080u);   // SM8 in bytes 0, 2
+    const u32 t1 = (v1 & (QMAG * 0x00010001u)) | ((v1 >> 8) & 0x00800080u);
+    return __builtin_amdgcn_perm(t1, t0, 0x06020400u);
+}
+// the partial sums of local words q .. q + 15 as one dword (bit i = word q + i of the low
+// frame, bit 16 + i of the high frame) from the dwords d0 (words 16 (q / 16) ..) and d1 (the
+// next 16)
+__device__ __forceinline__ u32 ubits16(u32 d0, u32 d1, int q)
+{
+    const int o = q & 15;
+    const u32 lo = ((d0 & 0xFFFFu) | (d1 << 16)) >> o, hi = ((d0 >> 16) | (d1 & 0xFFFF0000u)) >> o;
+    return (lo & 0xFFFFu) | (hi << 16);
+}
+// partial-sum flags of local words q + k, q + k + 1 (k even) from ubits16(.., q) at the sign
+// bits of the slot bytes (bits 7, 15, 23, 31; the other bits are don't-care: only sign bits
+// are read)
+// (k a constant after unrolling)
+__device__ __forceinline__ u32 ubits4s(u32 d16, int k)
+{
+    const u32 y = (k <= 7 ? d16 << (7 - k) : d16 >> (k - 7)) & 0x01800180u;   // bits 7, 8, 23, 24
+    return y | (y << 7);
+}
+// the same from a partial-sum dword and a run-time even q (bits q & 15, + 1 of it)
+__device__ __forceinline__ u32 ubits4(u32 dword, int q)
+{
+    const u32 y = ((dword >> (q & 15)) & 0x00030003u) << 7;
+    return y | (y << 7);
+}
+
+// SWAR on four SM8 bytes (sign bit 7, magnitude bits 0..6): exact while two magnitudes sum
+// below 128
+constexpr bool PAIR_SWAR = 2u * QMAG < 128u;
+constexpr u32 B_SGN = 0x80808080u, B_MAG = 0x7F7F7F7Fu, B_ONE = 0x01010101u;
+// 0x7F in the bytes whose bit 7 is set, 0 elsewhere
+__device__ __forceinline__ u32 bmask7(u32 t)
+{
+    const u32 g = t & B_SGN;
+    return g - (g >> 7);
+}
+__device__ __forceinline__ u32 bsel7(u32 m, u32 a, u32 b) { return (m & a) | (~m & b); }   // v_bfi
+// F_sm on four bytes: min of the magnitudes, xor of the signs
+__device__ __forceinline__ u32 F4(u32 a, u32 b)
+{
+    const u32 ma = a & B_MAG, mb = b & B_MAG;
+    const u32 ge = bmask7((ma | B_SGN) - mb);   // |a| >= |b|
+    return ((a ^ b) & B_SGN) | bsel7(ge, mb, ma);
+}
+// G_sm<GSAT> on four bytes; u: flip flags at the sign bits
+__device__ __forceinline__ u32 G4(u32 a, u32 b, u32 u)
+{
+    constexpr u32 SATV = GSAT * B_ONE;
+    const u32 ma = a & B_MAG, mb = b & B_MAG, x = a ^ b ^ u;   // x bit 7: sign(a') != sign(b)
+    const u32 t1 = (ma | B_SGN) - mb, t2 = (mb | B_SGN) - ma;   // bit 7: |a| >= |b|, |b| >= |a|
+    const u32 ad = bsel7(bmask7(t1), t1, t2);                  // | |a| - |b| | in bits 0..6
+    u32 m = bsel7(bmask7(x), ad, ma + mb);                      // bit 7 clear
+    m = bsel7(bmask7((m | B_SGN) - SATV), SATV, m);             // min(m, GSAT)
+    return ((b ^ (x & t1)) & B_SGN) | m;                        // |a| < |b| ? sign(b) : sign(a')
+}
+// channel bytes (two's complement, low Q bits) -> SM8: conv_pair on four bytes
+__device__ __forceinline__ u32 conv4(u32 raw)
+{
+    constexpr u32 QM = (1u << QB) - 1u, QP = 1u << QB;
+    const u32 t = raw & (QM * B_ONE), v = QP * B_ONE - t;       // QP - t in [1, QP] per byte
+    const u32 mn = bsel7(bmask7((t | B_SGN) - v), v, t);        // min(t, QP - t)
+    return ((t + (127u - QP / 2u) * B_ONE) & B_SGN) | (mn & (QMAG * B_ONE));   // sign: t > QP / 2
+}
+// F / G of a slot dword pair (either arithmetic)
+template <bool ISG>
+__device__ __forceinline__ u32 fg4(u32 a, u32 b, u32 u)
+{
+    if constexpr (PAIR_SWAR) {
+        if constexpr (ISG) return G4(a, b, u);
+        else return F4(a, b);
+    } else if constexpr (ISG) {
+        return ppack(G_sm<GSAT>(prow(a, false), prow(b, false), (u << 8) & SGN),
+                     G_sm<GSAT>(prow(a, true), prow(b, true), u & SGN));
+    } else {
+        return ppack(F_sm(prow(a, false), prow(b, false)), F_sm(prow(a, true), prow(b, true)));
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // per-pair context
 // ---------------------------------------------------------------------------------------
-constexpr int PAIR_MAX_WAVES = 8;   // launch bound 512 threads: <= 256 VGPRs per wave
-
+// 14 registers: passed by value to the noinline upper-level functions (in registers; a
+// reference would put it on the private stack). Global pointers carry address space 1 so that
+// the loads and stores through them are global_*, not flat_*.
 struct PairCtx {
-    const unsigned char *chl, *chh;   // channel bytes at this lane's position, frames lo / hi
-    u16 *hs;                          // HBM stage slots of the pair (lane offset included)
-    lds_u16 *ls;                      // LDS stage slots [lds_row0, ..) (lane offset included)
-    u32 *hb;                          // HBM partial-sum dwords of the pair (lane offset included)
-    lds_w32 *lx;                      // LDS exchange area: 3 dwords x waves (lane offset included)
+    const g_u8 *chl, *chh;            // channel bytes at this lane's position, frames lo / hi
+    g_u32 *hs;                        // HBM stage slots of the pair (lane offset 4 lane included)
+    g_u32 *hb;                        // HBM partial-sum dwords of the pair (lane offset included)
+    lds_w32 *ls;                      // LDS stage slots [lds_row0, ..) (lane offset 4 lane included)
+    int lxo;                          // LDS exchange area (3 dwords x waves, dword per lane) offset
     int G;                            // 16-LLR words per frame
-    int lds_row0;                     // first slot row held in LDS
+    int lds_row0;                     // first slot row held in LDS (even)
     int wi, W;                        // wave index in the pair's workgroup, waves
-    int row;                          // DPP row 0..3
-    bool lead;                        // the wave that runs the serial ops
-    Lanes ln;
-    // first slot row of level k (a node of G >> k words), k >= 1
+    __device__ __forceinline__ u32 row() const { return (threadIdx.x & 63u) >> 4; }   // DPP row
+    __device__ __forceinline__ bool lead() const { return wi == 0; }   // runs the serial ops
+    __device__ __forceinline__ Lanes lanes() const
+    {
+        Lanes ln;
+        ln.init(threadIdx.x & 15u);
+        return ln;
+    }
+    __device__ __forceinline__ lds_w32 *lx() const { return ls + lxo - 3 * (int)(threadIdx.x & 63u); }
+    // first slot row of level k (a node of G >> k words), k >= 1 (even)
     __device__ __forceinline__ int lvl_row(int k) const { return (G - (G >> (k - 1))) >> 2; }
     __device__ __forceinline__ bool in_lds(int r) const { return r >= lds_row0; }
+    // dword offset of slot row pair r / 2 (r even) from the lane's base
+    static __device__ __forceinline__ int sofs(int r) { return (r >> 3) * 256 + ((r >> 1) & 3); }
+    // slot dword of rows r, r + 1 (r even)
     template <bool L>
-    __device__ __forceinline__ u32 ld(int r) const
+    __device__ __forceinline__ u32 ld2(int r) const
     {
-        if constexpr (L) return slot_unpack((u32)ls[(r - lds_row0) * 64]);
-        else return slot_unpack((u32)hs[r * 64]);
+        if constexpr (L) return ls[sofs(r - lds_row0)];
+        else return hs[sofs(r)];
+    }
+    // slot dwords of rows r .. r + 7 (r a multiple of 8)
+    template <bool L>
+    __device__ __forceinline__ u32x4 ld8(int r) const
+    {
+        if constexpr (L) return *(const lds_u32x4 *)(ls + ((r - lds_row0) >> 3) * 256);
+        else return *(const g_u32x4 *)(hs + (r >> 3) * 256);
     }
     template <bool L>
-    __device__ __forceinline__ void st(int r, u32 v) const
+    __device__ __forceinline__ void st8(int r, u32x4 v) const
     {
-        if constexpr (L) ls[(r - lds_row0) * 64] = (u16)slot_pack(v);
-        else hs[r * 64] = (u16)slot_pack(v);
+        if constexpr (L) *(lds_u32x4 *)(ls + ((r - lds_row0) >> 3) * 256) = v;
+        else *(g_u32x4 *)(hs + (r >> 3) * 256) = v;
     }
-    // raw slot row r (SM8 pair) through a generic pointer (subtree roots)
-    __device__ __forceinline__ const u16 *slot_ptr(int r) const
+    // the slot from row r on (r a multiple of 8) through a generic pointer (subtree roots)
+    __device__ __forceinline__ const u32 *slot_ptr(int r) const
     {
-        return in_lds(r) ? (const u16 *)(ls + (r - lds_row0) * 64) : hs + r * 64;
+        return in_lds(r) ? (const u32 *)(ls + ((r - lds_row0) >> 3) * 256) : (const u32 *)(hs + (r >> 3) * 256);
     }
-    // channel register j of the root: words 4 j + row of both frames (wrapper_in + qconv_format)
-    __device__ __forceinline__ u32 chan(int j) const
+    // channel rows j, j + 1 (j even) as a slot dword (wrapper_in + qconv_format)
+    __device__ __forceinline__ u32 chan2(int j) const
     {
-        return conv_pair((u32)chl[64 * j] | ((u32)chh[64 * j] << 16));
+        const u32 lo = (u32)chl[64 * j] | ((u32)chl[64 * j + 64] << 8);
+        const u32 hi = (u32)chh[64 * j] | ((u32)chh[64 * j + 64] << 8);
+        const u32 raw = lo | (hi << 16);
+        if constexpr (PAIR_SWAR) return conv4(raw);
+        else return ppack(conv_pair(raw & 0x00FF00FFu), conv_pair((raw >> 8) & 0x00FF00FFu));
     }
     __device__ __forceinline__ u32 bld(int d) const { return hb[d * 64]; }
     __device__ __forceinline__ void bst(int d, u32 v) const { hb[d * 64] = v; }
@@ -140,50 +265,90 @@ __device__ __forceinline__ u32 ubit_p(u32 dword, int q) { return (dword << (15 -
 // split over the W waves of the pair in contiguous row ranges
 // ---------------------------------------------------------------------------------------
 // F_STATE / G_STATE word loops (my_module.h:373-445, 704-781): dst[j] = F(src[j], src[n4 + j])
-// or G(src[j], src[n4 + j], bit_mem[local word ub + j]) for rows j in [j0, j1)
+// or G(src[j], src[n4 + j], bit_mem[local word ub + j]) for rows j in [j0, j1) (even bounds),
+// one slot dword (two rows, both frames) per step
 template <bool ISG, bool ROOT, bool SL, bool DL>
 __device__ __forceinline__ void pfg_rows(const PairCtx &c, int s0, int d0, int n4, int ub, int j0, int j1)
 {
-    auto src = [&](int j) -> u32 {
-        if constexpr (ROOT) return c.chan(j);
-        else return c.template ld<SL>(s0 + j);
+    // groups of 8 rows (4 row pairs, one dwordx4 per lane) per batch; two batches in flight
+    // (ping-pong: the loads of the next batch are issued before the arithmetic of this one).
+    // HBM: 2 x 4 dwordx4 loads (+ 3 partial-sum dwords) per batch; the channel 8 x 4 byte
+    // loads; LDS 2 x 2 b128.
+    constexpr int NG = ROOT ? 1 : (SL ? 2 : 4);
+    constexpr int RB = 8 * NG;   // rows per batch
+    auto src = [&](int j) -> u32x4 {
+        if constexpr (ROOT) return u32x4{c.chan2(j), c.chan2(j + 2), c.chan2(j + 4), c.chan2(j + 6)};
+        else return c.template ld8<SL>(s0 + j);
     };
-    // rows per batch: HBM sources keep 2 x 32 row loads in flight (a lone wave per SIMD pair
-    // hides the HBM latency only with many loads outstanding), LDS sources 2 x 8
-    constexpr int CH = (ROOT || !SL) ? 32 : 8;
-    int j = j0;
-    for (; j + CH <= j1; j += CH) {
-        u32 a[CH], b[CH], r[CH];
+    struct Batch {
+        u32x4 a[NG], b[NG];
+        u32 u0, u1, u2;   // (scalars: a selected array element would go to scratch)
+    };
+    auto load = [&](Batch &x, int j) {
 #pragma unroll
-        for (int t = 0; t < CH; t++) {
-            a[t] = src(j + t);
-            b[t] = src(n4 + j + t);
+        for (int g = 0; g < NG; g++) {
+            x.a[g] = src(j + 8 * g);
+            x.b[g] = src(n4 + j + 8 * g);
         }
         if constexpr (ISG) {
-            u32 u0 = 0, u1 = 0;
-            if (ub >= 0) {
-                u0 = c.bld((ub + j) >> 4);
-                u1 = c.bld((ub + j + CH - 1) >> 4);
-            }
-#pragma unroll
-            for (int t = 0; t < CH; t++) {
-                const int q = ub + j + t;
-                const u32 u = ub >= 0 ? ubit_p((((q >> 4) == ((ub + j) >> 4)) ? u0 : u1), q) : 0u;
-                r[t] = G_sm<GSAT>(a[t], b[t], u);
-            }
-        } else {
-#pragma unroll
-            for (int t = 0; t < CH; t++) r[t] = F_sm(a[t], b[t]);
+            // the partial sums of local words ub + j .. ub + j + RB - 1: at most 3 dwords
+            const int dlast = (ub + n4 - 1) >> 4, q0 = (ub + j) >> 4;
+            x.u0 = ub >= 0 ? c.bld(q0) : 0u;
+            x.u1 = ub >= 0 ? c.bld(q0 + 1 < dlast ? q0 + 1 : dlast) : 0u;
+            x.u2 = ub >= 0 ? c.bld(q0 + 2 < dlast ? q0 + 2 : dlast) : 0u;
+        }
+    };
+    auto work = [&](const Batch &x, int j) {
+        u32 uq[(RB + 15) / 16];   // partial sums of words ub + j + 16 h .. (RB <= 32: from u0 .. u2)
+        if constexpr (ISG) {
+            uq[0] = ubits16(x.u0, x.u1, ub + j);
+            if constexpr (RB > 16) uq[1] = ubits16(x.u1, x.u2, ub + j);
         }
 #pragma unroll
-        for (int t = 0; t < CH; t++) c.template st<DL>(d0 + j + t, r[t]);
+        for (int g = 0; g < NG; g++) {
+            u32x4 r;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                if constexpr (ISG) {
+                    const int k = 8 * g + 2 * t;   // row in the batch
+                    const u32 u = ub >= 0 ? ubits4s(uq[k >> 4], k & 15) : 0u;
+                    r[t] = fg4<true>(x.a[g][t], x.b[g][t], u);
+                } else {
+                    r[t] = fg4<false>(x.a[g][t], x.b[g][t], 0u);
+                }
+            }
+            c.template st8<DL>(d0 + j + 8 * g, r);
+        }
+    };
+    // row counts are multiples of 8 (subtrees of >= 32 words)
+    const int nb = (j1 - j0) / RB, jlast = j0 + (nb - 1) * RB;
+    int j = j0;
+    if (nb > 0) {
+        Batch x, y;
+        load(x, j);
+        for (;;) {
+            load(y, j + RB < jlast ? j + RB : jlast);   // (the last batch re-loads itself: unused)
+            work(x, j);
+            j += RB;
+            if (j > jlast) break;
+            load(x, j + RB < jlast ? j + RB : jlast);
+            work(y, j);
+            j += RB;
+            if (j > jlast) break;
+        }
     }
-    for (; j < j1; j++) {
-        const u32 a = src(j), b = src(n4 + j);
-        u32 r;
-        if constexpr (ISG) r = G_sm<GSAT>(a, b, ub >= 0 ? ubit_p(c.bld((ub + j) >> 4), ub + j) : 0u);
-        else r = F_sm(a, b);
-        c.template st<DL>(d0 + j, r);
+    for (; j < j1; j += 8) {   // remaining groups
+        Batch x;
+        const u32x4 a = src(j), b = src(n4 + j);
+        u32x4 r;
+        const u32 ud = ub >= 0 ? c.bld((ub + j) >> 4) : 0u;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            if constexpr (ISG) r[t] = fg4<true>(a[t], b[t], ub >= 0 ? ubits4(ud, ub + j + 2 * t) : 0u);
+            else r[t] = fg4<false>(a[t], b[t], 0u);
+        }
+        (void)x;
+        c.template st8<DL>(d0 + j, r);
     }
 }
 
@@ -205,21 +370,23 @@ __device__ __forceinline__ void pop_fg(const PairCtx &c, int k, int n4, int ub, 
     }
 }
 template <bool ISG>
-__device__ __noinline__ void pop_fg_split(const PairCtx &c, int k, int n4, int ub)
+__device__ __noinline__ void pop_fg_split(PairCtx c, int k, int n4, int ub)
 {
-    pop_fg<ISG>(c, k, n4, ub, (n4 * c.wi) / c.W, (n4 * (c.wi + 1)) / c.W);
+    const int ng = n4 >> 3;   // groups of 8 rows
+    pop_fg<ISG>(c, k, n4, ub, 8 * ((ng * c.wi) / c.W), 8 * ((ng * (c.wi + 1)) / c.W));
 }
 
-// source word pair of a pruned-node op (REP / R1 / SPC): row j of the parent's two halves
+// source dwords of a pruned-node op (REP / R1 / SPC): rows j, j + 1 (j even) of the parent's
+// two halves, slot format
 template <bool ROOT, bool SL>
 __device__ __forceinline__ void psrc2(const PairCtx &c, int s0, int n4, int j, u32 &a, u32 &b)
 {
     if constexpr (ROOT) {
-        a = c.chan(j);
-        b = c.chan(n4 + j);
+        a = c.chan2(j);
+        b = c.chan2(n4 + j);
     } else {
-        a = c.template ld<SL>(s0 + j);
-        b = c.template ld<SL>(s0 + n4 + j);
+        a = c.template ld2<SL>(s0 + j);
+        b = c.template ld2<SL>(s0 + n4 + j);
     }
 }
 
@@ -231,29 +398,36 @@ template <bool ROOT, bool SL>
 __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int l0)
 {
     u32 acc = 0;
-    for (int j = 0; j < n4; j++) {
+    for (int j = 0; j < n4; j += 2) {
         u32 a, b;
         psrc2<ROOT, SL>(c, s0, n4, j, a, b);
-        const u32 lam = F_sm(a, b), sg = pk_sra(lam, 15);
-        const X4 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
-        acc = rep_acc(rep_acc(rep_acc(rep_acc(acc, t.t0), t.t1), t.t2), t.t3);
+#pragma unroll
+        for (int o = 0; o < 2; o++) {
+            const u32 lam = F_sm(prow(a, o), prow(b, o)), sg = pk_sra(lam, 15);
+            const X4 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
+            acc = rep_acc(rep_acc(rep_acc(rep_acc(acc, t.t0), t.t1), t.t2), t.t3);
+        }
     }
     if (rep_any_zero(acc)) {
+        const Lanes ln = c.lanes();
         acc = 0;
-        for (int j = 0; j < n4; j++) {
+        for (int j = 0; j < n4; j += 2) {
             u32 a, b;
             psrc2<ROOT, SL>(c, s0, n4, j, a, b);
-            const X4 t = rows4(row_add_tree(F_sm(a, b), c.ln));
-            acc = G_sm<REPSAT>(t.t0, acc, 0u);
-            acc = G_sm<REPSAT>(t.t1, acc, 0u);
-            acc = G_sm<REPSAT>(t.t2, acc, 0u);
-            acc = G_sm<REPSAT>(t.t3, acc, 0u);
+#pragma unroll
+            for (int o = 0; o < 2; o++) {
+                const X4 t = rows4(row_add_tree(F_sm(prow(a, o), prow(b, o)), ln));
+                acc = G_sm<REPSAT>(t.t0, acc, 0u);
+                acc = G_sm<REPSAT>(t.t1, acc, 0u);
+                acc = G_sm<REPSAT>(t.t2, acc, 0u);
+                acc = G_sm<REPSAT>(t.t3, acc, 0u);
+            }
         }
     }
     const u32 full = pk_sra(acc, 15);   // two's complement or SM16: the decision is bit 15 / 31
     for (int l = 0; l < n4; l += 16) pbits_put(c, l0 + l, n4 - l < 16 ? n4 - l : 16, full);
 }
-__device__ __noinline__ void pop_rep(const PairCtx &c, int k, int n4, int l0)
+__device__ __noinline__ void pop_rep(PairCtx c, int k, int n4, int l0)
 {
     if (k == 0) prep_body<true, false>(c, 0, n4, l0);
     else if (c.in_lds(c.lvl_row(k))) prep_body<false, true>(c, c.lvl_row(k), n4, l0);
@@ -270,9 +444,11 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
                                             bool part)
 {
     u32 acc = 0, par = 0, klo = 0xFFFFFFFFu, khi = 0xFFFFFFFFu, ud = 0;
+    u32 da = 0, db = 0;
+    const int row = (int)c.row();
     for (int j = j0; j < j1; j++) {
-        u32 a, b;
-        psrc2<ROOT, SL>(c, s0, n4, j, a, b);
+        if (((j - j0) & 1) == 0) psrc2<ROOT, SL>(c, s0, n4, j, da, db);
+        const u32 a = prow(da, j & 1), b = prow(db, j & 1);
         u32 u = 0;
         if (ub >= 0) {
             if (j == j0 || ((ub + j) & 15) == 0) ud = c.bld((ub + j) >> 4);
@@ -288,15 +464,16 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
         }
         if constexpr (SPC) {
             par ^= h;
-            const u32 wk = (u32)(4 * j + c.row) << 4;   // word index in the node
+            const u32 wk = (u32)(4 * j + row) << 4;   // word index in the node
             klo = __builtin_elementwise_min(klo, ((lam & 0xFFu) << 24) | wk);
             khi = __builtin_elementwise_min(khi, (((lam >> 16) & 0xFFu) << 24) | wk);
         }
     }
     if constexpr (SPC) {
+        const Lanes ln = c.lanes();
         par = row_xor(par);
-        klo = row_min_u32(klo | c.ln.br);
-        khi = row_min_u32(khi | c.ln.br);
+        klo = row_min_u32(klo | ln.br);
+        khi = row_min_u32(khi | ln.br);
         {   // across the four rows
             X2 p = swap16(par);
             par = p.a ^ p.b;
@@ -311,12 +488,12 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
             khi = __builtin_elementwise_min(b.a, b.b);
         }
         if (c.W > 1) {   // across the waves of the pair
-            lds_w32 *const x = c.lx;
+            lds_w32 *const x = c.lx();
             x[(3 * c.wi) * 64] = part ? par : 0u;
             x[(3 * c.wi + 1) * 64] = part ? klo : 0xFFFFFFFFu;
             x[(3 * c.wi + 2) * 64] = part ? khi : 0xFFFFFFFFu;
             __syncthreads();
-            if (!c.lead) return;
+            if (!c.lead()) return;
             par = 0;
             klo = khi = 0xFFFFFFFFu;
             for (int w = 0; w < c.W; w++) {
@@ -326,8 +503,8 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
             }
         }
         // the flipped word: 4 (key >> 6) + ((key >> 4) & 3), position bitrev4^-1(key & 15)
-        const bool flo = (par & 0x8000u) && (klo & 15u) == c.ln.br && (int)((klo >> 4) & 3u) == c.row;
-        const bool fhi = (par & 0x80000000u) && (khi & 15u) == c.ln.br && (int)((khi >> 4) & 3u) == c.row;
+        const bool flo = (par & 0x8000u) && (klo & 15u) == ln.br && (int)((klo >> 4) & 3u) == row;
+        const bool fhi = (par & 0x80000000u) && (khi & 15u) == ln.br && (int)((khi >> 4) & 3u) == row;
         if (flo) {
             const int l = l0 + (int)((klo >> 6) & 0x3FFFFu);
             c.bst(l >> 4, c.bld(l >> 4) ^ (1u << (l & 15)));
@@ -339,7 +516,7 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
     }
 }
 template <bool SPC>
-__device__ __noinline__ void pop_r1spc(const PairCtx &c, int k, int n4, int ub, int l0)
+__device__ __noinline__ void pop_r1spc(PairCtx c, int k, int n4, int ub, int l0)
 {
     // whole dwords per wave (n4 is a multiple of 16 above the subtrees of >= 64 words)
     const int nd = (n4 + 15) >> 4;
@@ -355,7 +532,7 @@ __device__ __noinline__ void pop_r1spc(const PairCtx &c, int k, int n4, int ub, 
 // H_STATE / H0_STATE (my_module.h:903-932, 1020-1042) on local words [l0, l0 + n4) and
 // [l0 + n4, l0 + 2 n4): whole dwords split over the waves
 template <bool H0>
-__device__ __noinline__ void pop_h(const PairCtx &c, int l0, int n4)
+__device__ __noinline__ void pop_h(PairCtx c, int l0, int n4)
 {
     if (n4 >= 16) {
         const int nd = n4 >> 4, da = l0 >> 4, db = (l0 + n4) >> 4;
@@ -372,7 +549,7 @@ __device__ __noinline__ void pop_h(const PairCtx &c, int l0, int n4)
             for (int t = 0; t < 8; t++) c.bst(da + e + t, a[t] ^ b[t]);
         }
         for (; e < e1; e++) c.bst(da + e, (H0 ? 0u : c.bld(da + e)) ^ c.bld(db + e));
-    } else if (c.lead) {
+    } else if (c.lead()) {
         const u32 m = ((1u << n4) - 1u) << (l0 & 15), mm = m | (m << 16);
         const u32 d = c.bld(l0 >> 4), sh = (d >> n4) & mm;
         c.bst(l0 >> 4, H0 ? ((d & ~mm) | sh) : (d ^ sh));
@@ -382,19 +559,20 @@ __device__ __noinline__ void pop_h(const PairCtx &c, int l0, int n4)
 // END (my_module.h:1848-1869) + wrapper_out: the partial sums of every local word, transposed
 // inside each row (lane j of row r: the 16 position bits of local word 16 d + j = word
 // 4 (16 d + j) + r), stored as u16 words in natural order
-__device__ __noinline__ void pair_out(const PairCtx &c, unsigned short *o_lo, unsigned short *o_hi, bool st_lo,
-                                         bool st_hi, int out_stride)
+__device__ __noinline__ void pair_out(PairCtx c, g_u16 *o_lo, g_u16 *o_hi, bool st_lo, bool st_hi, int out_stride)
 {
+    const Lanes ln = c.lanes();
+    const int row = (int)c.row();
     const int nd = c.G >> 6;   // dwords per lane (G / 4 local words)
     const int e0 = (nd * c.wi) / c.W, e1 = (nd * (c.wi + 1)) / c.W;
     for (int d = e0; d < e1; d++) {
-        const u32 t = row_transpose16(to_position_order(c.bld(d), c.ln), c.ln);
-        const int w = 4 * (16 * d + (int)c.ln.pl) + c.row;
+        const u32 t = row_transpose16(to_position_order(c.bld(d), ln), ln);
+        const int w = 4 * (16 * d + (int)ln.pl) + row;
         if (st_lo) o_lo[w] = (unsigned short)(t & 0xFFFFu);
         if (st_hi) o_hi[w] = (unsigned short)(t >> 16);
     }
-    if (c.lead)
-        for (int w = c.G + (int)c.ln.pl + 16 * c.row; w < out_stride; w += 64) {   // pad words
+    if (c.lead())
+        for (int w = c.G + (int)ln.pl + 16 * row; w < out_stride; w += 64) {   // pad words
             if (st_lo) o_lo[w] = 0;
             if (st_hi) o_hi[w] = 0;
         }
@@ -404,26 +582,23 @@ __device__ __noinline__ void pair_out(const PairCtx &c, unsigned short *o_lo, un
 // the partial-sum dwords (256 B rows); LDS: slot rows [lds_row0, total) then the SPC exchange
 __device__ __forceinline__ bool pair_init(PairCtx &c, const signed char *llr, unsigned int *scratch, int N, int batch,
                                           long pair, int pair_dwords, int slot_rows, int lds_row0, int wi, int W,
-                                          lds_u16 *lbase)
+                                          lds_w32 *lbase)
 {
     const int lane = threadIdx.x & 63;
     c.G = N >> 4;
-    c.row = lane >> 4;
-    c.ln.init((u32)(lane & 15));
     c.wi = wi;
     c.W = W;
-    c.lead = wi == 0;
     c.lds_row0 = lds_row0;
     const long f_lo = 2 * pair, f_hi = 2 * pair + 1;
     const long fl = f_lo < batch ? f_lo : (long)batch - 1, fh = f_hi < batch ? f_hi : (long)batch - 1;
-    const int off = 16 * c.row + (int)c.ln.pos;
-    c.chl = (const unsigned char *)llr + fl * (long)N + off;
-    c.chh = (const unsigned char *)llr + fh * (long)N + off;
-    unsigned int *base = scratch + pair * (long)pair_dwords;
-    c.hs = (u16 *)base + lane;
+    const int off = 16 * (int)c.row() + (int)c.lanes().pos;
+    c.chl = (const g_u8 *)llr + fl * (long)N + off;
+    c.chh = (const g_u8 *)llr + fh * (long)N + off;
+    g_u32 *base = (g_u32 *)scratch + pair * (long)pair_dwords;
+    c.hs = base + 4 * lane;
     c.hb = base + (slot_rows >> 1) * 64 + lane;   // slot_rows x 128 B = slot_rows / 2 dword rows
-    c.ls = lbase + lane;
-    c.lx = (lds_w32 *)(lbase + (slot_rows > lds_row0 ? slot_rows - lds_row0 : 0) * 64) + lane;
+    c.ls = lbase + 4 * lane;
+    c.lxo = ((slot_rows > lds_row0 ? slot_rows - lds_row0 : 0) >> 1) * 64;
     return f_lo < batch;
 }
 

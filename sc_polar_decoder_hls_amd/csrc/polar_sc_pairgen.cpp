@@ -380,13 +380,13 @@ struct PairGen {
         else small_op(op, pd, cd);
     }
 
-    // subtree decoder `id`: root words from slot rows src_[64 j] (SM8 pairs), partial sums to
+    // subtree decoder `id`: root words from the slot dwords at src_ (rows j, j + 1: CH), partial sums to
     // the pair's bit dwords from local word l0
     void sub_function(int id)
     {
         const int words = 1 << LG, R = regs(LG), nbw = words / 4 >= 16 ? words / 64 : 1;
         // (plain arguments: a PairCtx passed by reference would live on the private stack)
-        o << "__device__ __noinline__ void polar_psub_" << id << "(const u16 *src_, u32 *hb_, int l0)\n{\n"
+        o << "__device__ __noinline__ void polar_psub_" << id << "(const u32 *src_, g_u32 *hb_, int l0)\n{\n"
           << "  const u32 lane_ = threadIdx.x & 63u;\n  Lanes ln; ln.init(lane_ & 15u);\n"
           << "  struct { u32 row; } c; c.row = lane_ >> 4;\n  u32 bw[" << nbw << "] = {};\n";
         bool split_root = false;   // REP / R1 / SPC children of the root read split root words
@@ -410,9 +410,9 @@ struct PairGen {
         o << "}\n\n";
     }
 };
-// a root word of a subtree decoder: SM8 pair of its stage slot row -> SM16
+// a root word of a subtree decoder: row j of its stage slot (row-pair dwords, SM8) -> SM16
 // partial-sum dword d of the subtree to the pair's bits (masked: subtrees of < 64 words)
-const char *const kPairCH = "#define CH(j) slot_unpack((u32)src_[(j) * 64])\n"
+const char *const kPairCH = "#define CH(j) prow(src_[((j) >> 3) * 256 + (((j) >> 1) & 3)], ((j) & 1) != 0)\n"
                             "#define BST(d, v) (hb_[((l0 >> 4) + (d)) * 64] = (v))\n"
                             "#define BSTM(m, v) (hb_[(l0 >> 4) * 64] = (hb_[(l0 >> 4) * 64] & ~((m) << (l0 & 15))) | \\\n"
                             "    (((v) << (l0 & 15)) & ((m) << (l0 & 15))))\n";
@@ -425,13 +425,13 @@ void upper_call(std::ostringstream &o, const polar_sc_op &op)
     switch (op.code) {
     case POLAR_OP_F: o << "pop_fg_split<false>(c, " << op.level << ", " << n4 << ", -1);"; break;
     case POLAR_OP_G: o << "pop_fg_split<true>(c, " << op.level << ", " << n4 << ", " << ub << ");"; break;
-    case POLAR_OP_REP: o << "if (c.lead) pop_rep(c, " << op.level << ", " << n4 << ", " << l0 << ");"; break;
+    case POLAR_OP_REP: o << "if (c.lead()) pop_rep(c, " << op.level << ", " << n4 << ", " << l0 << ");"; break;
     case POLAR_OP_R1: o << "pop_r1spc<false>(c, " << op.level << ", " << n4 << ", " << ub << ", " << l0 << ");"; break;
     case POLAR_OP_SPC: o << "pop_r1spc<true>(c, " << op.level << ", " << n4 << ", " << ub << ", " << l0 << ");"; break;
     case POLAR_OP_H: o << "pop_h<false>(c, " << l0 << ", " << n4 << ");"; break;
     case POLAR_OP_H0: o << "pop_h<true>(c, " << l0 << ", " << n4 << ");"; break;
     case POLAR_OP_SUB:
-        o << "if (c.lead) polar_psub_" << op.fb << "(c.slot_ptr(c.lvl_row(" << op.level << ")), c.hb, " << l0 << ");";
+        o << "if (c.lead()) polar_psub_" << op.fb << "(c.slot_ptr(c.lvl_row(" << op.level << ")), c.hb, " << l0 << ");";
         break;
     default: throw std::runtime_error("pairgen: unexpected upper op");
     }
@@ -445,12 +445,12 @@ void pair_kernel(std::ostringstream &o, const char *name, const std::vector<pola
     o << "extern \"C\" __global__ void __launch_bounds__(" << 64 * PAIR_WAVES_MAX << ") " << name << "(\n"
       << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, unsigned int *__restrict__ scratch,\n"
       << "    int N, int batch, int out_stride, int pair_dwords, int slot_rows, int lds_row0, int seg)\n{\n"
-      << "  extern __shared__ __attribute__((aligned(16))) unsigned short smem_[];\n"
+      << "  extern __shared__ __attribute__((aligned(16))) unsigned int smem_[];\n"
       << "  PairCtx c;\n"
       << "  const int W = blockDim.x >> 6, wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
       << "  const long pair = blockIdx.x;\n"
       << "  if (2 * pair >= batch) return;\n"
-      << "  pair_init(c, llr, scratch, N, batch, pair, pair_dwords, slot_rows, lds_row0, wi, W, (lds_u16 *)smem_);\n"
+      << "  pair_init(c, llr, scratch, N, batch, pair, pair_dwords, slot_rows, lds_row0, wi, W, (lds_w32 *)smem_);\n"
       << "  switch (seg) {\n  case 0:\n";
     int seg = 0;
     for (const polar_sc_op &op : ops) {
@@ -462,7 +462,8 @@ void pair_kernel(std::ostringstream &o, const char *name, const std::vector<pola
         upper_call(o, op);
     }
     o << "    c.sync();\n"
-      << "    pair_out(c, out + (2 * pair) * (long)out_stride, out + (2 * pair + 1) * (long)out_stride, 2 * pair < batch,\n"
+      << "    pair_out(c, (g_u16 *)out + (2 * pair) * (long)out_stride, (g_u16 *)out + (2 * pair + 1) * (long)out_stride,\n"
+      << "             2 * pair < batch,\n"
       << "             2 * pair + 1 < batch, out_stride);\n"
       << "    return;\n  default: return;\n  }\n}\n";
 }
@@ -487,12 +488,21 @@ std::string pair_source(const polar_sc_plan &p)
     // the decode kernel over the whole schedule, and (grid-tier plans) the segment kernel
     pair_kernel(o, "polar_sc_pair_kernel", p.pair_ops);
     // test hook (polar_sc_debug_subtree): subtree decoder `id` on 64 lanes of root slot rows
-    // in[64 j + lane], its partial-sum dwords to out[64 d + lane]
+    // in[64 j + lane] (u16 SM8 pairs, repacked into row-pair dwords in LDS), its partial-sum
+    // dwords to out[64 d + lane]
     o << "extern \"C\" __global__ void __launch_bounds__(64) polar_sc_pair_subtest_kernel(\n"
       << "    const unsigned short *__restrict__ in, unsigned int *__restrict__ out, int id)\n{\n"
-      << "  const int lane = threadIdx.x & 63;\n  switch (id) {\n";
+      << "  __shared__ unsigned int rows_[" << p.sub_words / 8 << " * 64];\n"
+      << "  const int lane = threadIdx.x & 63;\n"
+      << "  for (int i = 0; i < " << p.sub_words / 8 << "; i++) {\n"
+      << "    const unsigned int r0 = in[128 * i + lane], r1 = in[128 * i + 64 + lane];\n"
+      << "    rows_[(i >> 2) * 256 + 4 * lane + (i & 3)] = (r0 & 0xFFu) | ((r1 & 0xFFu) << 8) | ((r0 >> 8) << 16) |\n"
+      << "                                                ((r1 >> 8) << 24);\n"
+      << "  }\n"
+      << "  const unsigned int *src = rows_ + 4 * lane;\n"
+      << "  switch (id) {\n";
     for (size_t id = 0; id < p.subs.size(); id++)
-        o << "  case " << id << ": polar_psub_" << id << "(in + lane, out + lane, 0); return;\n";
+        o << "  case " << id << ": polar_psub_" << id << "(src, (g_u32 *)out + lane, 0); return;\n";
     o << "  default: return;\n  }\n}\n";
     if (!p.pair_tier.steps.empty()) {
         pair_kernel(o, "polar_sc_pair_seg_kernel", p.pair_tier.seg_ops);

@@ -57,7 +57,7 @@ def wave_mask():
 PARITY_MASKS = [("frozen_n_2048_k_1024", 23), ("FB_N2048_K1024", 8), ("frozen_n_4096_k_2048", 17),
                 ("frozen_n_8192_k_4096", 9), ("frozen_n_16384_k_8192", 7), ("frozen_n_32768_k_29492", 5),
                 ("frozen_n_2048_k_1844", 12), ("frozen_n_16384_k_14746", 6), ("frozen_n_65536_k_32768", 5)]
-STRUCT_SUB_WORDS = (16, 64, 256)
+STRUCT_SUB_WORDS = (32, 64, 256)
 
 
 def struct_sub_words(N):
@@ -73,7 +73,7 @@ def gpu_plans():
         for i, m in enumerate(struct_masks(N)):
             out += [("struct%d_%d" % (N, i), m, {"kernel": 3, "sub_words": sw}) for sw in struct_sub_words(N)]
     out += [("frozen_n_2048_k_1024", util.mask("frozen_n_2048_k_1024"), {"kernel": 3, "sub_words": sw})
-            for sw in (16, 32, 64)]
+            for sw in (32, 64)]
     out += [("frozen_n_8192_k_4096", util.mask("frozen_n_8192_k_4096"), {"kernel": 3, "sub_words": 256}),
             ("frozen_n_16384_k_8192", util.mask("frozen_n_16384_k_8192"), {"kernel": 3, "sub_words": 64}),
             ("wave_mask", wave_mask(), {"kernel": 3, "sub_words": 64}),
@@ -102,6 +102,8 @@ def test_pair_plan_stats(pkg):
     assert s["tier_words"] == 1024 and s["tier_steps"] > 20
     with pytest.raises(pkg.PolarError):
         pair(pkg, util.mask("frozen_n_4096_k_2048"), sub_words=256)   # > G / 2
+    with pytest.raises(pkg.PolarError):
+        pair(pkg, util.mask("frozen_n_4096_k_2048"), sub_words=16)    # < 32: 8-row slot groups
 
 
 @pytest.mark.parametrize("N", [2048, 8192])
@@ -121,7 +123,7 @@ def test_pair_generated_code_emulated(pkg, oracle_mod, N):
     u = rng.integers(0, 2, size=(4, mask.size), dtype=np.uint8) & mask[None, :]
     x = util.encode_np(u)
     llr = np.where(x == 1, -9, 9).astype(np.int8)
-    for sw in (16, 32, 64):
+    for sw in (32, 64):
         assert (pair_emu.decode(pair(pkg, mask, sub_words=sw), llr) == x).all()
 
 
@@ -131,7 +133,7 @@ def test_pair_subtrees_equal_emulation(pkg, cuda):
     emulation on random root LLRs."""
     import pair_emu
     rng = np.random.default_rng(5)
-    for name, sw in (("frozen_n_2048_k_1024", 64), ("frozen_n_2048_k_1024", 16), ("frozen_n_8192_k_4096", 256)):
+    for name, sw in (("frozen_n_2048_k_1024", 64), ("frozen_n_2048_k_1024", 32), ("frozen_n_8192_k_4096", 256)):
         dec = pair(pkg, util.mask(name), sub_words=sw)
         subs = pair_emu.Sub(dec.kernel_source(), dec.stats["n_sub_kinds"])
         for sid in range(dec.stats["n_sub_kinds"]):
@@ -141,7 +143,7 @@ def test_pair_subtrees_equal_emulation(pkg, cuda):
             assert (got == ref).all(), "%s S=%d subtree %d" % (name, sw, sid)
 
 
-@pytest.mark.parametrize("sub_words", [16, 128])
+@pytest.mark.parametrize("sub_words", [32, 128])
 def test_pair_source_compiles(pkg, sub_words):
     """hipRTC build of a generated pair source (host only)."""
     dec = pair(pkg, util.mask("frozen_n_8192_k_4096"), sub_words=sub_words)

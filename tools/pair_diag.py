@@ -30,11 +30,11 @@ def main():
     N = 2048
     allinfo = np.ones(N, np.uint8)
     cases.append(("allinfo_noiseless_S64", allinfo, {"sub_words": 64}, "noiseless"))
-    cases.append(("allinfo_noiseless_S16", allinfo, {"sub_words": 16}, "noiseless"))
+    cases.append(("allinfo_noiseless_S32", allinfo, {"sub_words": 32}, "noiseless"))
     m = util.mask("frozen_n_2048_k_1024")
     cases.append(("n2048_noiseless_S64", m, {"sub_words": 64}, "noiseless"))
     cases.append(("n2048_awgn_S64", m, {"sub_words": 64}, "awgn"))
-    cases.append(("n2048_awgn_S16", m, {"sub_words": 16}, "awgn"))
+    cases.append(("n2048_awgn_S32", m, {"sub_words": 32}, "awgn"))
     half = np.zeros(N, np.uint8)
     half[N // 2:] = 1
     cases.append(("upperhalf_noiseless_S64", half, {"sub_words": 64}, "noiseless"))
@@ -42,7 +42,7 @@ def main():
     cases.append(("n2048_noiseless_S64_W1", m, {"sub_words": 64, "waves_per_group": 1}, "noiseless"))
     cases.append(("n2048_noiseless_S64_W2", m, {"sub_words": 64, "waves_per_group": 2}, "noiseless"))
     cases.append(("n2048_noiseless_S32", m, {"sub_words": 32}, "noiseless"))
-    cases.append(("n2048_noiseless_S16_W1", m, {"sub_words": 16, "waves_per_group": 1}, "noiseless"))
+    cases.append(("n2048_noiseless_S32_W1", m, {"sub_words": 32, "waves_per_group": 1}, "noiseless"))
     rh = m.copy()
     rh[N // 2:] = 1
     cases.append(("n2048_left_rightR1_S64", rh, {"sub_words": 64}, "noiseless"))

@@ -16,7 +16,7 @@ def main():
     import util
     import pair_emu
     rng = np.random.default_rng(5)
-    for name, sw in (("frozen_n_2048_k_1024", 64), ("frozen_n_2048_k_1024", 16), ("frozen_n_2048_k_1024", 32)):
+    for name, sw in (("frozen_n_2048_k_1024", 64), ("frozen_n_2048_k_1024", 32)):
         dec = pkg.Decoder(util.mask(name), tuning={"kernel": 3, "sub_words": sw})
         subs = pair_emu.Sub(dec.kernel_source(), dec.stats["n_sub_kinds"])
         bad = 0

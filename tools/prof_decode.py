@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--ebn0", type=float, default=2.5)
     ap.add_argument("--rotate", type=int, default=0,
                     help="distinct input batches cycled through (0: as bench.py, >= 300 MB in total)")
+    ap.add_argument("--tuning", default="", help="polar_sc_tuning fields, e.g. kernel=3,tier_words=2048")
     a = ap.parse_args()
     import torch
     import bench
@@ -25,7 +26,8 @@ def main():
     import util
     mask = util.mask(a.mask)
     dev = torch.device("cuda", 0)
-    dec = pkg.Decoder(mask)
+    tun = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, a.tuning.split(",")))}
+    dec = pkg.Decoder(mask, tuning=tun or None)
     dec.prepare(a.batch)
     nb = a.rotate if a.rotate > 0 else max(1, min(8, -(-bench.ROTATE_BYTES // (a.batch * mask.size))))
     llrs = [bench.gen_frames_torch(torch, mask, a.batch, a.ebn0, 0xF0 + b, dev)[0] for b in range(nb)]
