@@ -75,49 +75,71 @@ def build(force=False, verbose=False):
     return LIB
 
 
-def prewarm_plans(plans, threads=8, verbose=False):
-    """Compile the hipRTC kernels of [(name, info mask, tuning dict)] into the code-object cache
-    (host only, in parallel, largest first)."""
+def _cfg_fields(cfg):
+    if cfg is None:
+        return None
+    return {f: int(getattr(cfg, f)) for f, _ in cfg._fields_}
+
+
+def _compile_item(item):
+    """Worker of the prewarm pool: one plan's hipRTC kernels into the code-object cache."""
+    import sys
     import time
-    from concurrent.futures import ThreadPoolExecutor
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
     import sc_polar_decoder_hls_amd as pkg
-
-    def one(item):
-        name, m, tun = item
-        t0 = time.time()
-        dec = pkg.Decoder(m, tuning=tun)
-        ok = dec.compile()
-        dec.close()
-        return name, tun, ok, time.time() - t0
-
-    items = sorted(plans, key=lambda it: -it[1].size)
-    with ThreadPoolExecutor(max(1, threads)) as ex:
-        for name, tun, ok, dt in ex.map(one, items):
-            if verbose:
-                print("prewarm %-28s %s %s %.1f s" % (name, tun, "compiled" if ok else "(no hipRTC kernel)", dt))
+    name, m, cfg, tun = item
+    t0 = time.time()
+    c = None
+    if cfg is not None:
+        c = pkg.default_config()
+        for k, v in cfg.items():
+            setattr(c, k, v)
+    dec = pkg.Decoder(m, c, tuning=tun)
+    ok = dec.compile()
+    dec.close()
+    return name, tun, ok, time.time() - t0
 
 
-def prewarm(masks, configs=(None,), threads=8, verbose=False):
+def _run_pool(items, procs, verbose):
+    """hipRTC serialises compilations inside one process (a single thread makes progress at a
+    time), so the prewarm fans out over worker PROCESSES (spawned: nothing of the parent's HIP
+    runtime state is inherited). Largest codes first: the long compiles overlap the short ones."""
+    import multiprocessing as mp
+    items = sorted(items, key=lambda it: -it[1].size)
+    procs = max(1, min(procs, len(items)))
+    if procs == 1:
+        res = map(_compile_item, items)
+        for r in res:
+            _report(r, verbose)
+        return
+    with mp.get_context("spawn").Pool(procs) as pool:
+        for r in pool.imap_unordered(_compile_item, items):
+            _report(r, verbose)
+
+
+def _report(r, verbose):
+    name, tun, ok, dt = r
+    if verbose:
+        print("prewarm %-28s %s %s %.1f s" % (name, tun or "", "compiled" if ok else "(no hipRTC kernel)", dt),
+              flush=True)
+
+
+def _default_procs():
+    # a C5 hybrid / pair compile holds a few GB: bounded by memory as well as cores
+    return int(os.environ.get("POLAR_SC_PREWARM_PROCS", min(6, os.cpu_count() or 1)))
+
+
+def prewarm_plans(plans, procs=None, verbose=False):
+    """Compile the hipRTC kernels of [(name, info mask, tuning dict)] into the code-object cache
+    (host only, in parallel worker processes, largest first)."""
+    _run_pool([(n, m, None, t) for n, m, t in plans], procs or _default_procs(), verbose)
+
+
+def prewarm(masks, configs=(None,), procs=None, verbose=False):
     """Compile the hipRTC kernels of the plans of `masks` ({name: info mask}) x `configs`
     into the on-disk code-object cache next to the library (lib/rtc_cache/), host only, in
     parallel. A GPU box then loads them instead of compiling (the C5 hybrid kernel takes about
     two minutes of hipRTC)."""
-    import time
-    from concurrent.futures import ThreadPoolExecutor
-    import sc_polar_decoder_hls_amd as pkg
-
-    def one(item):
-        name, m, cfg = item
-        t0 = time.time()
-        dec = pkg.Decoder(m, cfg)
-        ok = dec.compile()
-        dec.close()
-        return name, ok, time.time() - t0
-
-    items = [(n, m, c) for n, m in masks.items() for c in configs]
-    # largest first: the long compiles overlap the short ones
-    items.sort(key=lambda it: -it[1].size)
-    with ThreadPoolExecutor(max(1, threads)) as ex:
-        for name, ok, dt in ex.map(one, items):
-            if verbose:
-                print("prewarm %-28s %s %.1f s" % (name, "compiled" if ok else "(no hipRTC kernel)", dt))
+    items = [(n, m, _cfg_fields(c), None) for n, m in masks.items() for c in configs]
+    _run_pool(items, procs or _default_procs(), verbose)
