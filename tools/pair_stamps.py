@@ -125,14 +125,19 @@ def build(mask_name, batch, tuning):
     for j, line in enumerate(lines):
         if line.startswith("    return;"):
             break
-        m = re.match(r"    c\.sync\(\); (.*;)\s+// (\d+) level (\d+) n (\d+) pos (\d+)$", line)
+        m = re.match(r"    c\.sync\(\); (.*;)\s+// (chain )?(\d+) level (\d+) n (\d+) pos (\d+)(.*)$", line)
         if not m:
             continue
         n += 1
-        code, lev, nn, pos = (int(x) for x in m.groups()[1:])
+        code, lev, nn, pos = (int(x) for x in m.groups()[2:6])
         name = NAMES.get(code, str(code))
-        labels.append("%s level %d n %d pos %d" % (name, lev, nn, pos))
-        classes.append("SUB" if code == 13 else "%s level %d" % (name, lev) if code in (1, 2) else name)
+        if m.group(2):   # fused F / G descent (pop_chain): the records after '|'
+            recs = [name] + [NAMES.get(int(r.split()[0]), "?") for r in m.group(7).split("|")[1:]]
+            labels.append("chain %s level %d n %d pos %d" % ("".join(recs), lev, nn, pos))
+            classes.append("chain from level %d" % lev)
+        else:
+            labels.append("%s level %d n %d pos %d" % (name, lev, nn, pos))
+            classes.append("SUB" if code == 13 else "%s level %d" % (name, lev) if code in (1, 2) else name)
         lines[j] = "    c.sync(); %s " % m.group(1) + stamp % n
     src = src[:i] + "\n".join(lines)
     nst = n + 1
