@@ -88,7 +88,9 @@ typedef struct polar_sc_tuning {
                                  else 256, 512 or 1024 */
     int32_t hybrid_waves;     /* hybrid plans: waves per group of the kernel's launch bound,
                                  0 = automatic (8), else 4 or 8 */
-    int32_t reserved[2];      /* must be 0 */
+    int32_t chain_max;        /* pair plans: F / G records fused into one descent chain
+                                 (pop_chain), 0 = automatic (3), 1 = no fusion, 2 or 3 */
+    int32_t reserved;         /* must be 0 */
 } polar_sc_tuning;
 
 /* Immutable decode plan: N, config, frozen mask, compiled decode schedule and its device

@@ -5,6 +5,7 @@ schedule compiler / C ABI (csrc/polar_sc_host.cpp) behind include/polar_sc.h.
 """
 import os
 import subprocess
+import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -113,9 +114,27 @@ def _run_pool(items, procs, verbose):
         for r in res:
             _report(r, verbose)
         return
-    with mp.get_context("spawn").Pool(procs) as pool:
-        for r in pool.imap_unordered(_compile_item, items):
+    # (a pool whose workers cannot start -- e.g. the parent runs a script from stdin, which
+    # spawned children cannot re-import -- raises BrokenProcessPool instead of hanging: then
+    # compile in-process)
+    from concurrent.futures import ProcessPoolExecutor, as_completed
+    from concurrent.futures.process import BrokenProcessPool
+    main = sys.modules.get("__main__")
+    if not os.path.isfile(getattr(main, "__file__", "") or ""):
+        for r in map(_compile_item, items):
             _report(r, verbose)
+        return
+    done = set()
+    try:
+        with ProcessPoolExecutor(procs, mp_context=mp.get_context("spawn")) as ex:
+            futs = {ex.submit(_compile_item, it): i for i, it in enumerate(items)}
+            for f in as_completed(futs):
+                _report(f.result(), verbose)
+                done.add(futs[f])
+    except BrokenProcessPool:
+        for i, it in enumerate(items):
+            if i not in done:
+                _report(_compile_item(it), verbose)
 
 
 def _report(r, verbose):

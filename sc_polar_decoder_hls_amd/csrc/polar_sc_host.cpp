@@ -467,8 +467,8 @@ bool tuning_valid(const polar_sc_tuning &t)
            (t.sub_words == 0 || (pow2(t.sub_words) && t.sub_words >= 2 && t.sub_words <= 256)) &&
            t.tier_words >= -1 && (t.tier_words <= 0 || pow2(t.tier_words)) &&
            (t.lds_slots == 0 || t.lds_slots == 256 || t.lds_slots == 512 || t.lds_slots == 1024) &&
-           (t.hybrid_waves == 0 || t.hybrid_waves == 4 || t.hybrid_waves == 8) && t.reserved[0] == 0 &&
-           t.reserved[1] == 0;
+           (t.hybrid_waves == 0 || t.hybrid_waves == 4 || t.hybrid_waves == 8) && t.chain_max >= 0 &&
+           t.chain_max <= 3 && t.reserved == 0;
 }
 
 int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }

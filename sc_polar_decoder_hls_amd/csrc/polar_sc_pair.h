@@ -237,6 +237,11 @@ struct PairCtx {
         if constexpr (PAIR_SWAR) return conv4(raw);
         else return ppack(conv_pair(raw & 0x00FF00FFu), conv_pair((raw >> 8) & 0x00FF00FFu));
     }
+    // channel rows j .. j + 7 (j a multiple of 8) as four slot dwords, byte loads (chan2)
+    __device__ __forceinline__ u32x4 chan8b(int j) const
+    {
+        return u32x4{chan2(j), chan2(j + 2), chan2(j + 4), chan2(j + 6)};
+    }
     __device__ __forceinline__ u32 bld(int d) const { return hb[d * 64]; }
     __device__ __forceinline__ void bst(int d, u32 v) const { hb[d * 64] = v; }
     __device__ __forceinline__ void sync() const
@@ -244,6 +249,74 @@ struct PairCtx {
         if (W > 1) __syncthreads();
     }
 };
+
+// ---------------------------------------------------------------------------------------
+// channel reads by dwords (wrapper_in): the four lanes of a quad hold the positions 4 q ..
+// 4 q + 3 of a word (lane_pos keeps quads whole). Lane k of the quad loads the dword of those
+// positions of combination k = (frame lo / hi = k >> 1, row 2 i + (k & 1)) and a 4 x 4 byte
+// transpose inside the quad (two quad DPP moves, two v_perm with per-lane selectors) gives
+// every lane its position of all four: the slot dword. One 4-byte load per lane and slot
+// dword instead of four byte loads.
+// ---------------------------------------------------------------------------------------
+// wave-uniform copy of a pointer (SGPRs): loads through (uniform base + 32-bit lane offset)
+// take the saddr form, one VGPR per address instead of a 64-bit pair per load
+template <class T>
+__device__ __forceinline__ T *uniform_ptr(T *p)
+{
+    const unsigned long v = (unsigned long)p;
+    const u32 lo = __builtin_amdgcn_readfirstlane((u32)v), hi = __builtin_amdgcn_readfirstlane((u32)(v >> 32));
+    return (T *)(((unsigned long)hi << 32) | lo);
+}
+struct ChanQ {
+    const g_u8 *base;   // frame lo, byte 0 (wave-uniform)
+    u32 off;            // this lane's combination at row 0, positions 4 q .. (bytes from base)
+    u32 s1, s2;         // v_perm selectors of the two transpose rounds
+    bool al;            // frames 4-byte aligned (else the byte-load path)
+};
+__device__ __forceinline__ ChanQ chan_quad(const PairCtx &c)
+{
+    const u32 lane = threadIdx.x & 63u, pl = lane & 15u, k = pl & 3u, m = lane_pos(pl) & 3u;
+    ChanQ q;
+    // chl = frame lo + 16 row + pos; chh - chl = (hi frame - lo frame) N (uniform)
+    q.base = uniform_ptr(c.chl - (16u * (lane >> 4) + lane_pos(pl)));
+    const u32 dhi = __builtin_amdgcn_readfirstlane((u32)(c.chh - c.chl));
+    q.off = 16u * (lane >> 4) + (pl & ~3u) + 64u * (k & 1u) + ((k & 2u) ? dhi : 0u);
+    // round 1: [x_k[m], x_k^1[m], x_k[m ^ 2], x_k^1[m ^ 2]] from (own = bytes 0..3, partner = 4..7)
+    q.s1 = m | ((4u + m) << 8) | ((m ^ 2u) << 16) | ((4u + (m ^ 2u)) << 24);
+    // round 2: byte k <- y[0], k ^ 1 <- y[1], k ^ 2 <- partner y[2] (6), k ^ 3 <- partner y[3] (7)
+    q.s2 = (0u << (8 * k)) | (1u << (8 * (k ^ 1u))) | (6u << (8 * (k ^ 2u))) | (7u << (8 * (k ^ 3u)));
+    q.al = ((u32)(unsigned long)q.base & 3u) == 0u;
+    return q;
+}
+__device__ __forceinline__ u32 quad_transpose(u32 x, const ChanQ &q)
+{
+    const u32 t1 = __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+    const u32 y = __builtin_amdgcn_perm(t1, x, q.s1);
+    const u32 t2 = __builtin_amdgcn_update_dpp(0u, y, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    return __builtin_amdgcn_perm(t2, y, q.s2);
+}
+__device__ __forceinline__ u32 chan_conv(u32 raw)
+{
+    if constexpr (PAIR_SWAR) return conv4(raw);
+    else return ppack(conv_pair(raw & 0x00FF00FFu), conv_pair((raw >> 8) & 0x00FF00FFu));
+}
+// channel rows j .. j + 7 (j a multiple of 8) as four slot dwords, aligned frames
+__device__ __forceinline__ u32x4 chan8a(const ChanQ &q, int j)
+{
+    u32 raw[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++)   // rows j + 2 t, + 1: words 4 (j + 2 t) + r (+ 4)
+        raw[t] = *(const g_u32 *)(q.base + (64u * (u32)(j + 2 * t) + q.off));
+    u32x4 r;
+#pragma unroll
+    for (int t = 0; t < 4; t++) r[t] = chan_conv(quad_transpose(raw[t], q));
+    return r;
+}
+__device__ __forceinline__ u32x4 chan8(const PairCtx &c, const ChanQ &q, int j)
+{
+    if (!q.al) return c.chan8b(j);
+    return chan8a(q, j);
+}
 
 // bits of local words [l0, l0 + cnt) (cnt <= 16, inside one dword) := acc (bit j = word l0 + j
 // at bit position (l0 + j) % 16, both halves)
@@ -274,10 +347,12 @@ __device__ __forceinline__ void pfg_rows(const PairCtx &c, int s0, int d0, int n
     // (ping-pong: the loads of the next batch are issued before the arithmetic of this one).
     // HBM: 2 x 4 dwordx4 loads (+ 3 partial-sum dwords) per batch; the channel 8 x 4 byte
     // loads; LDS 2 x 2 b128.
-    constexpr int NG = ROOT ? 1 : (SL ? 2 : 4);
+    constexpr int NG = ROOT ? 2 : (SL ? 2 : 4);
+    ChanQ cq;
+    if constexpr (ROOT) cq = chan_quad(c);
     constexpr int RB = 8 * NG;   // rows per batch
     auto src = [&](int j) -> u32x4 {
-        if constexpr (ROOT) return u32x4{c.chan2(j), c.chan2(j + 2), c.chan2(j + 4), c.chan2(j + 6)};
+        if constexpr (ROOT) return chan8(c, cq, j);
         else return c.template ld8<SL>(s0 + j);
     };
     struct Batch {
@@ -374,6 +449,137 @@ __device__ __noinline__ void pop_fg_split(PairCtx c, int k, int n4, int ub)
 {
     const int ng = n4 >> 3;   // groups of 8 rows
     pop_fg<ISG>(c, k, n4, ub, 8 * ((ng * c.wi) / c.W), 8 * ((ng * (c.wi + 1)) / c.W));
+}
+
+// A chain of D F / G records, each consuming the node the previous one wrote (the F_STATE
+// descent of my_module.h:373-445 from a node to its leftmost subtree, or G_STATE then that
+// descent): record 0 at level k over n4 output rows (ISG0: G with the partial sums at local
+// word ub, else F), records i = 1 .. D - 1 at level k + i: F, or G with zero partial sums
+// (the H0 route, bit i of gm). Every level is still written (its G reads it later), but the
+// chain's own reads of levels k + 1 .. k + D - 1 come from registers: per column of 8 output
+// rows of the last record, the 2^(D-1) row groups of record 0 at rows j0 + m nl are computed
+// and folded pairwise. Columns split over the W waves, two in flight.
+// AL: the channel frames are 4-byte aligned (dword reads, chan8), else byte reads (chan8b).
+// PP: two columns in flight (ping-pong), except for root chains of D >= 4 (64 channel dwords
+// per column; the generator emits D <= 3).
+template <int D, bool ROOT, bool ISG0, bool AL>
+__device__ __noinline__ void pchain(PairCtx c, int k, int n4, int ub, u32 gm)
+{
+    constexpr int M = 1 << (D - 1);
+    constexpr bool PP = !ROOT || D <= 3;   // (D <= 3 from the generator)
+    const int nl = n4 >> (D - 1);   // rows of the last record's output (a multiple of 8)
+    const int ng = nl >> 3;
+    const int g0 = (ng * c.wi) / c.W, g1 = (ng * (c.wi + 1)) / c.W;
+    if (g1 <= g0) return;
+    const int s0 = ROOT ? 0 : c.lvl_row(k);
+    const bool sl = !ROOT && c.in_lds(s0);
+    ChanQ cq;
+    if constexpr (ROOT) cq = chan_quad(c);
+    // HBM slots and partial sums through a wave-uniform base + one 32-bit lane offset
+    const u32 lane = threadIdx.x & 63u;
+    const g_u8 *const hsb = (const g_u8 *)uniform_ptr(c.hs - 4u * lane);
+    const g_u8 *const hbb = (const g_u8 *)uniform_ptr(c.hb - lane);
+    auto ldh = [&](int r) -> u32x4 { return *(const g_u32x4 *)(hsb + ((u32)(r >> 3) * 1024u + 16u * lane)); };
+    auto sth = [&](int r, u32x4 v) { *(g_u32x4 *)(hsb + ((u32)(r >> 3) * 1024u + 16u * lane)) = v; };
+    auto st = [&](int r, u32x4 v) {
+        if (c.in_lds(r)) c.template st8<true>(r, v);
+        else sth(r, v);
+    };
+    struct Col {
+        u32x4 a[M], b[M];
+        u32 u[M];
+    };
+    auto load = [&](Col &x, int g) {
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+            const int j = 8 * g + m * nl;
+            if constexpr (ROOT && AL) {
+                x.a[m] = chan8a(cq, j);
+                x.b[m] = chan8a(cq, n4 + j);
+            } else if constexpr (ROOT) {
+                x.a[m] = c.chan8b(j);
+                x.b[m] = c.chan8b(n4 + j);
+            } else if (sl) {
+                x.a[m] = c.template ld8<true>(s0 + j);
+                x.b[m] = c.template ld8<true>(s0 + n4 + j);
+            } else {
+                x.a[m] = ldh(s0 + j);
+                x.b[m] = ldh(s0 + n4 + j);
+            }
+            if constexpr (ISG0) x.u[m] = ub >= 0 ? *(const g_u32 *)(hbb + ((u32)((ub + j) >> 4) * 256u + 4u * lane)) : 0u;
+        }
+    };
+    auto work = [&](Col &x, int g) {
+        const int j0 = 8 * g;
+        const int d1 = c.lvl_row(k + 1);
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+            const int j = j0 + m * nl;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                if constexpr (ISG0) x.a[m][t] = fg4<true>(x.a[m][t], x.b[m][t], ub >= 0 ? ubits4(x.u[m], ub + j + 2 * t) : 0u);
+                else x.a[m][t] = fg4<false>(x.a[m][t], x.b[m][t], 0u);
+            }
+            st(d1 + j, x.a[m]);
+        }
+#pragma unroll
+        for (int i = 1; i < D; i++) {
+            const int h = M >> i;
+            const int di = c.lvl_row(k + 1 + i);
+            if ((gm >> i) & 1u) {
+#pragma unroll
+                for (int m = 0; m < h; m++) {
+#pragma unroll
+                    for (int t = 0; t < 4; t++) x.a[m][t] = fg4<true>(x.a[m][t], x.a[m + h][t], 0u);
+                    st(di + j0 + m * nl, x.a[m]);
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < h; m++) {
+#pragma unroll
+                    for (int t = 0; t < 4; t++) x.a[m][t] = fg4<false>(x.a[m][t], x.a[m + h][t], 0u);
+                    st(di + j0 + m * nl, x.a[m]);
+                }
+            }
+        }
+    };
+    if constexpr (!PP) {
+        for (int g = g0; g < g1; g++) {
+            Col x;
+            load(x, g);
+            work(x, g);
+        }
+    } else {
+        Col x, y;
+        int g = g0;
+        load(x, g);
+        for (;;) {
+            if (g + 1 < g1) load(y, g + 1);
+            work(x, g);
+            if (++g >= g1) break;
+            if (g + 1 < g1) load(x, g + 1);
+            work(y, g);
+            if (++g >= g1) break;
+        }
+    }
+}
+template <int D, bool ROOT, bool ISG0>
+__device__ __forceinline__ void pop_chain(const PairCtx &c, int k, int n4, int ub, u32 gm)
+{
+    if (c.W > 1 && ((n4 >> (D - 1)) >> 3) < 2 * c.W) {
+        // fewer than two columns per wave: the records one by one, each split over all the
+        // waves by row groups (what the chain saves in reads is less than the waves it idles)
+        pop_fg_split<ISG0>(c, k, n4, ub);
+#pragma unroll
+        for (int i = 1; i < D; i++) {
+            c.sync();
+            if ((gm >> i) & 1u) pop_fg_split<true>(c, k + i, n4 >> i, -1);
+            else pop_fg_split<false>(c, k + i, n4 >> i, -1);
+        }
+        return;
+    }
+    if (ROOT && !chan_quad(c).al) pchain<D, ROOT, ISG0, false>(c, k, n4, ub, gm);
+    else pchain<D, ROOT, ISG0, true>(c, k, n4, ub, gm);
 }
 
 // source dwords of a pruned-node op (REP / R1 / SPC): rows j, j + 1 (j even) of the parent's

@@ -438,9 +438,46 @@ void upper_call(std::ostringstream &o, const polar_sc_op &op)
     o << "   // " << op.code << " level " << op.level << " n " << op.n << " pos " << op.pos << "\n";
 }
 
+// F / G records that fuse into one pop_chain call (polar_sc_pair.h): record i + 1 is F, or G
+// with zero partial sums (the H0 route), on the node record i wrote -- one level down, half the
+// words. At most PAIR_CHAIN_MAX records (2^(D-1) row groups of each operand per column): a
+// noinline chain of 4 records takes ~250 VGPRs, and hipRTC then spills it into AGPRs past the
+// 256 registers a 512-thread launch allows (the dispatch is rejected); 3 records stay at ~160
+// for the whole kernel (tools/check_rtc_registers.py, tests/test_pair.py).
+constexpr int PAIR_CHAIN_MAX = 3;
+int chain_len(const std::vector<polar_sc_op> &ops, size_t i, int cmax)
+{
+    const polar_sc_op &o0 = ops[i];
+    if (o0.code != POLAR_OP_F && o0.code != POLAR_OP_G) return 1;
+    int d = 1;
+    while (d < cmax && i + d < ops.size()) {
+        const polar_sc_op &p = ops[i + d - 1], &q = ops[i + d];
+        const bool fg = q.code == POLAR_OP_F || (q.code == POLAR_OP_G && q.upos < 0);
+        if (!fg || q.level != p.level + 1 || 2 * q.n != p.n) break;
+        d++;
+    }
+    return d;
+}
+void chain_call(std::ostringstream &o, const std::vector<polar_sc_op> &ops, size_t i, int d)
+{
+    const polar_sc_op &o0 = ops[i];
+    unsigned gm = 0;
+    for (int k = 1; k < d; k++)
+        if (ops[i + k].code == POLAR_OP_G) gm |= 1u << k;
+    const bool g0 = o0.code == POLAR_OP_G;
+    o << "    c.sync(); pop_chain<" << d << ", " << (o0.level == 0 ? "true" : "false") << ", " << (g0 ? "true" : "false")
+      << ">(c, " << o0.level << ", " << o0.n / 4 << ", " << (g0 && o0.upos >= 0 ? o0.upos / 4 : -1) << ", " << gm
+      << "u);   // chain";
+    for (int k = 0; k < d; k++) {
+        const polar_sc_op &q = ops[i + k];
+        o << (k ? " |" : "") << " " << q.code << " level " << q.level << " n " << q.n << " pos " << q.pos;
+    }
+    o << "\n";
+}
+
 // one decode kernel: a block of W waves per frame pair; `seg` selects the schedule segment
 // (the cases between POLAR_OP_SEGEND records; 0 when the plan has no grid tier)
-void pair_kernel(std::ostringstream &o, const char *name, const std::vector<polar_sc_op> &ops)
+void pair_kernel(std::ostringstream &o, const char *name, const std::vector<polar_sc_op> &ops, int cmax)
 {
     o << "extern \"C\" __global__ void __launch_bounds__(" << 64 * PAIR_WAVES_MAX << ") " << name << "(\n"
       << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, unsigned int *__restrict__ scratch,\n"
@@ -453,10 +490,17 @@ void pair_kernel(std::ostringstream &o, const char *name, const std::vector<pola
       << "  pair_init(c, llr, scratch, N, batch, pair, pair_dwords, slot_rows, lds_row0, wi, W, (lds_w32 *)smem_);\n"
       << "  switch (seg) {\n  case 0:\n";
     int seg = 0;
-    for (const polar_sc_op &op : ops) {
+    for (size_t i = 0; i < ops.size(); i++) {
+        const polar_sc_op &op = ops[i];
         if (op.code == POLAR_OP_END) break;
         if (op.code == POLAR_OP_SEGEND) {
             o << "    return;\n  case " << ++seg << ":\n";
+            continue;
+        }
+        const int d = chain_len(ops, i, cmax);
+        if (d >= 2) {
+            chain_call(o, ops, i, d);
+            i += (size_t)d - 1;
             continue;
         }
         upper_call(o, op);
@@ -486,7 +530,8 @@ std::string pair_source(const polar_sc_plan &p)
     }
     o << "}  // namespace polar\nusing namespace polar;\n";
     // the decode kernel over the whole schedule, and (grid-tier plans) the segment kernel
-    pair_kernel(o, "polar_sc_pair_kernel", p.pair_ops);
+    const int cmax = p.tune.chain_max ? p.tune.chain_max : PAIR_CHAIN_MAX;
+    pair_kernel(o, "polar_sc_pair_kernel", p.pair_ops, cmax);
     // test hook (polar_sc_debug_subtree): subtree decoder `id` on 64 lanes of root slot rows
     // in[64 j + lane] (u16 SM8 pairs, repacked into row-pair dwords in LDS), its partial-sum
     // dwords to out[64 d + lane]
@@ -505,7 +550,7 @@ std::string pair_source(const polar_sc_plan &p)
         o << "  case " << id << ": polar_psub_" << id << "(src, (g_u32 *)out + lane, 0); return;\n";
     o << "  default: return;\n  }\n}\n";
     if (!p.pair_tier.steps.empty()) {
-        pair_kernel(o, "polar_sc_pair_seg_kernel", p.pair_tier.seg_ops);
+        pair_kernel(o, "polar_sc_pair_seg_kernel", p.pair_tier.seg_ops, cmax);
         o << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_pair_tier_kernel(\n"
           << "    const signed char *__restrict__ llr, unsigned int *__restrict__ scratch, int N, int batch, int pair_dwords,\n"
           << "    int slot_rows, int code_g, int k, int n4, int ub, int cw)\n{\n"

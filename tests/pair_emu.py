@@ -479,9 +479,17 @@ def _upper_ops(src):
     k0 = src.index("polar_sc_pair_kernel(")
     body = src[k0:src.index("pair_out(", k0)]
     ops = []
-    for m in re.finditer(r"(pop_fg_split<(\w+)>|pop_rep|pop_r1spc<(\w+)>|pop_h<(\w+)>|polar_psub_(\d+))\(([^;]*)\);", body):
-        args = [a.strip() for a in _split_top(m.group(6))]
-        if m.group(1).startswith("pop_fg_split"):
+    for m in re.finditer(r"(pop_fg_split<(\w+)>|pop_rep|pop_r1spc<(\w+)>|pop_h<(\w+)>|polar_psub_(\d+)|"
+                         r"pop_chain<(\d+), (\w+), (\w+)>)\(([^;]*)\);", body):
+        args = [a.strip() for a in _split_top(m.group(9))]
+        if m.group(1).startswith("pop_chain"):
+            # a fused descent: record 0 (F, or G with partial sums at ub), then F / zero-u G
+            d, isg0 = int(m.group(6)), m.group(8) == "true"
+            k, n4, ub, gm = int(args[1]), int(args[2]), int(args[3]), int(args[4].rstrip("u"))
+            ops.append(("G" if isg0 else "F", k, n4, ub))
+            for i in range(1, d):
+                ops.append(("G" if (gm >> i) & 1 else "F", k + i, n4 >> i, -1))
+        elif m.group(1).startswith("pop_fg_split"):
             ops.append(("G" if m.group(2) == "true" else "F", int(args[1]), int(args[2]), int(args[3])))
         elif m.group(1) == "pop_rep":
             ops.append(("REP", int(args[1]), int(args[2]), int(args[3])))

@@ -217,3 +217,39 @@ def test_pair_c5_sample(pkg, cuda, oracle_mod):
     ref = oracle_mod.decode_fsm(mask, llr)
     _assert_same(run(pkg, cuda, pair(pkg, mask), llr), ref, "C5 pair")
     _assert_same(run(pkg, cuda, pair(pkg, mask, tier_words=1024), llr), ref, "C5 pair tier")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["frozen_n_16384_k_8192", "frozen_n_65536_k_32768"])
+def test_pair_misaligned_channel(pkg, cuda, oracle_mod, name):
+    """Channel rows at an odd device address: the root chains take the byte-load path instead
+    of the dword loads + quad transpose (chan8b vs chan8a), with the same bits."""
+    mask = util.mask(name)
+    llr, _ = util.synth_frames(mask, 3, ebn0_db=1.0, seed=11)
+    flat = cuda.zeros(llr.size + 16, dtype=cuda.int8, device="cuda")
+    view = flat[1:1 + llr.size].view(llr.shape)
+    view.copy_(cuda.from_numpy(llr))
+    dec = pair(pkg, mask)
+    out = dec.decode(view)
+    cuda.cuda.synchronize()
+    _assert_same(pkg.unpack_bits(out.cpu().numpy(), mask.size), oracle_mod.decode_fsm(mask, llr), "misaligned " + name)
+
+
+def test_pair_register_budget(pkg, tmp_path, monkeypatch):
+    """hipRTC code objects of the largest pair plans fit the registers of a 512-thread launch
+    (VGPRs + AGPRs <= 256 per lane at two waves per SIMD): a generated call graph that needs
+    more is spilled into AGPRs by hipRTC and the dispatch is rejected on the device
+    (HSA_STATUS_ERROR_INVALID_ISA)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import check_rtc_registers as cr
+    monkeypatch.setenv("POLAR_SC_RTC_CACHE", str(tmp_path))
+    for m, tun in ((util.mask("frozen_n_262144_k_131072"), {}), (struct_masks(32768)[0], {"sub_words": 64})):
+        assert pair(pkg, m, **tun).compile()
+    cos = list(tmp_path.glob("*.co"))
+    assert len(cos) == 2
+    for co in cos:
+        for name, vgpr, agpr, wg in cr.kernels(str(co)):
+            over, total = cr.over_budget(vgpr, agpr, wg)
+            assert not over, "%s: %s vgpr %d agpr %d for %d threads" % (co.name, name, vgpr, agpr, wg)

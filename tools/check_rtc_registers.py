@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Register budget of every hipRTC code object in lib/rtc_cache (CPU only).
+
+A kernel whose VGPRs + AGPRs exceed what its launch bound allows (512 unified registers per
+SIMD lane, shared by the waves of a workgroup that land on one SIMD) is rejected at dispatch
+(HSA_STATUS_ERROR_INVALID_ISA): hipRTC can add AGPRs to a 256-VGPR call graph. This lists
+every kernel with its counts and exits 1 when one is over budget.
+
+usage: python tools/check_rtc_registers.py [cache dir]
+"""
+import glob
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+
+
+def kernels(path):
+    notes = subprocess.run([READELF, "--notes", path], capture_output=True, text=True).stdout
+    out = []
+    for blk in re.split(r"\n\s+- \.agpr_count:", notes)[1:]:
+        agpr = int(blk.split()[0])
+        name = re.search(r"\.name:\s+(\S+)", blk)
+        vgpr = re.search(r"\.vgpr_count:\s+(\d+)", blk)
+        wg = re.search(r"\.max_flat_workgroup_size:\s+(\d+)", blk)
+        if name and vgpr and wg:
+            out.append((name.group(1), int(vgpr.group(1)), agpr, int(wg.group(1))))
+    return out
+
+
+def over_budget(vgpr, agpr, wg):
+    # unified register file of 512 per lane and SIMD; VGPRs are padded to 4 before the AGPRs
+    waves_per_simd = max(1, -(-wg // 64) // 4)
+    total = (-(-vgpr // 4) * 4 if agpr else vgpr) + agpr
+    return total * waves_per_simd > 512, total
+
+
+def main():
+    d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "sc_polar_decoder_hls_amd", "lib", "rtc_cache")
+    bad = 0
+    for co in sorted(glob.glob(os.path.join(d, "*.co"))):
+        for name, vgpr, agpr, wg in kernels(co):
+            over, total = over_budget(vgpr, agpr, wg)
+            if over or agpr:
+                print("%s %-32s vgpr %3d agpr %3d wg %4d%s" % (os.path.basename(co), name, vgpr, agpr, wg,
+                                                               "  OVER BUDGET" if over else ""))
+            bad += over
+    print("%d kernel(s) over budget" % bad)
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

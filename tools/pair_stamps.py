@@ -6,8 +6,8 @@ build (container, CPU):  python tools/pair_stamps.py build [--mask M] [--batch B
     Takes the plan's generated source (Decoder.kernel_source()), adds a stamps argument and
     reads s_memtime after pair_init and after every schedule op of segment 0; lane 0 of the
     lead wave of each pair writes the stamps with vector stores. Links a HIP driver (random
-    channel bytes, the plan's launch shape) into build_tools/pair_stamps_<mask>.
-run (GPU box):           ./build_tools/pair_stamps_<mask> > gpurun_out/pair_stamps.txt
+    channel bytes, the plan's launch shape) into build_tools/pair_stamps_<mask>_b<batch>.
+run (GPU box):           ./build_tools/pair_stamps_<mask>_b<batch> > gpurun_out/pair_stamps.txt
     Prints per op (and per op class) the median over pairs of its duration in s_memtime
     ticks (shader clock) of the last of 5 launches, plus the launch's HIP-event time.
 """
@@ -147,10 +147,10 @@ def build(mask_name, batch, tuning):
     tab = ("static const char *LABEL[] = {%s};\nstatic const char *CLASS[] = {%s};\n"
            % (", ".join('"%s"' % s for s in labels), ", ".join('"%s"' % s for s in classes)))
     os.makedirs(OUT, exist_ok=True)
-    path = os.path.join(OUT, "pair_stamps_%s.hip" % mask_name)
+    path = os.path.join(OUT, "pair_stamps_%s_b%d.hip" % (mask_name, batch))
     with open(path, "w") as f:
         f.write("#include <hip/hip_runtime.h>\n" + defs + src + tab + DRIVER)
-    exe = os.path.join(OUT, "pair_stamps_%s" % mask_name)
+    exe = os.path.join(OUT, "pair_stamps_%s_b%d" % (mask_name, batch))
     subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", CSRC, "-o", exe, path])
     print(exe, "ops", n, "W", W, "lds_row0", lds_row0, "of", slot_rows)
 
