@@ -155,6 +155,12 @@ def prewarm_plans(plans, procs=None, verbose=False):
     _run_pool([(n, m, None, t) for n, m, t in plans], procs or _default_procs(), verbose)
 
 
+def prewarm_items(items, procs=None, verbose=False):
+    """Compile the hipRTC kernels of [(name, info mask, config fields dict or None, tuning dict
+    or None)] into the code-object cache (host only, in parallel)."""
+    _run_pool(list(items), procs or _default_procs(), verbose)
+
+
 def prewarm(masks, configs=(None,), procs=None, verbose=False):
     """Compile the hipRTC kernels of the plans of `masks` ({name: info mask}) x `configs`
     into the on-disk code-object cache next to the library (lib/rtc_cache/), host only, in

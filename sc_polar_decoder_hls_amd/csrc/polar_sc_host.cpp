@@ -347,13 +347,15 @@ void emit_word(std::vector<polar_sc_op> &out, const polar_sc_plan &p, int code, 
 void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int level, uint32_t g0, uint32_t cnt,
                   bool is_root, SubCtx *sc)
 {
-    if (sc && !is_root && cnt == sc->words) {
+    // (sc->words counts device words; g0 / cnt count PAR groups of p16 words: PAR 64 -> 4)
+    if (sc && !is_root && cnt * p.p16 == sc->words) {
         std::vector<polar_sc_op> sub;
         compile_node(p, sub, level, g0, cnt, false, nullptr);
+        const int w0 = (int)(g0 * p.p16);
         for (polar_sc_op &o : sub) {
             o.level -= level;
-            o.pos -= (int)g0;
-            if (o.upos >= 0) o.upos -= (int)g0;
+            o.pos -= w0;
+            if (o.upos >= 0) o.upos -= w0;
         }
         std::string key((const char *)sub.data(), sub.size() * sizeof(polar_sc_op));
         auto it = sc->ids.find(key);
@@ -366,7 +368,7 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
             id = it->second;
         }
         sc->calls++;
-        emit(out, polar_host::POLAR_OP_SUB, level, (int)cnt, (int)g0, -1, (uint32_t)id);
+        emit(out, polar_host::POLAR_OP_SUB, level, (int)(cnt * p.p16), w0, -1, (uint32_t)id);
         return;
     }
     const uint32_t h = cnt / 2;
@@ -799,8 +801,13 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // PRUNING_LEVEL 1 leaf decoders other than the plain leaf run on the interpreter only
     bool kinds = false;
     for (const polar_sc_op &o : p->ops)
-        if ((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && (o.fb >> 16)) kinds = true;
+        if (((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && ((o.fb >> 16) & 7u)) ||
+            o.code == polar_host::POLAR_OP_PLEAF)
+            kinds = true;
     const bool dflt = default_format(c);
+    // pair plans also take PAR 64 (the PAR word = one register of four device words; the host
+    // expands its leaf into F / G_extended / 16-LLR leaf records, par_expand)
+    const bool pair_fmt = dflt || (c.par == 64 && c.sigmag == 1 && c.extended == 1 && c.llr_bits <= 8);
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR
     // level's F / G / H then run inside the straight-line code instead of as interpreter ops
@@ -816,7 +823,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // groups, tools/pair_ab.py: C3 1.64 -> 1.16 ms, C5 4.18 -> 1.78, C5 at 64 frames 3.57 ->
     // 1.55, N = 16384 x 4096 frames 0.39 -> 0.24, N = 4096 x 16384 0.36 -> 0.23);
     // polar_sc_tuning.kernel = 2 keeps the hybrid kernel
-    const bool want_pair = !p->jit && jit_on && !kinds && dflt && p->G >= 128 && (t.kernel == 3 || t.kernel == 0);
+    const bool want_pair = !p->jit && jit_on && !kinds && pair_fmt && p->G >= 128 && (t.kernel == 3 || t.kernel == 0);
     if (want_pair) {
         int S = std::min<int>(polar_host::PAIR_SUB_WORDS, (int)p->G / 2);
         if (t.sub_words) {
@@ -1133,7 +1140,12 @@ int polar_sc_plan_kernel_source(const polar_sc_plan *p, char *buf, size_t cap, s
 {
     if (!p || !len) return -EINVAL;
     if (!p->jit && !p->hybrid && !p->pair) return -ENOTSUP;
-    const std::string src = polar_host::jit_source(*p);
+    std::string src;
+    try {
+        src = polar_host::jit_source(*p);
+    } catch (const std::exception &) {
+        return -ENOTSUP;
+    }
     *len = src.size();
     if (buf && cap) {
         size_t n = cap - 1 < src.size() ? cap - 1 : src.size();

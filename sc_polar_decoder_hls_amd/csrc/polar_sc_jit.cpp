@@ -716,7 +716,14 @@ int jit_load16(const polar_sc_plan &p, DevState &st)
 int jit_compile(const polar_sc_plan &p)
 {
     if (!p.jit_code.empty()) return 0;
-    return rtc_compile(jit_source(p), p.jit_code, p.jit_log);
+    std::string src;
+    try {   // (the generators throw on a schedule they do not support: an error, not an abort)
+        src = jit_source(p);
+    } catch (const std::exception &e) {
+        p.jit_log = e.what();
+        return -ENOTSUP;
+    }
+    return rtc_compile(src, p.jit_code, p.jit_log);
 }
 
 // Per-mask plans whose LLR_BITS is not the hipcc-built 6: the per-op monitor runs the schedule

@@ -80,6 +80,59 @@ __device__ __forceinline__ bool land(bool a, bool b) { return a && b; }
 __device__ __forceinline__ u32 row_even(u32 row) { return (row & 1u) ? 0u : 0xFFFFFFFFu; }   // rows 0, 2
 __device__ __forceinline__ u32 row_lo2(u32 row) { return row < 2u ? 0xFFFFFFFFu : 0u; }       // rows 0, 1
 
+// G_extended on split words (inside a PAR 64 word, functions.h Spec_P64_ext): G_split without
+// the clamp -- magnitudes grow by at most one bit per level, far below the 15 of an SM16 half
+template <int I>
+__device__ __forceinline__ u32 G_split_x(u32 ma, u32 mb, u32 X, u32 &LT)
+{
+    const u32 xm = opaque(plane_mask<I>(X));
+    const u32 d = pk_sub(ma, mb);
+    LT = plane_put<I>(LT, d);
+    return bsel(xm, pk_abs_i16(d), pk_add(ma, mb));
+}
+
+// PAR 64 (POLAR_LPAR 6): a PAR word is four device words = the four rows of one register of a
+// node (and one slot row); PAR 16: one device word = one row
+constexpr bool PAIR_P64 = LPAR == 6;
+static_assert(LPAR == 4 || LPAR == 6, "pair plans: PAR 16 or 64");
+__device__ __forceinline__ u32 bitrev2(u32 r) { return ((r & 1u) << 1) | (r >> 1); }
+// SPC key bits below the word index (bits 0..5): the tie order of equal magnitudes inside a
+// register -- PAR 16: (word = row, then bitrev4(position)); PAR 64: bitrev6(position in the PAR
+// word) = (bitrev4(position), then bitrev2(row)) (polar_sc_interp.h spc_key)
+__device__ __forceinline__ u32 spc_sub(u32 row, const Lanes &ln)
+{
+    return PAIR_P64 ? (ln.br << 2) | bitrev2(row) : (row << 4) | ln.br;
+}
+// REP accumulation of one register's four row totals (row_sum_biased values, +8192 per half):
+// PAR 16 -- four PAR words in order (word 4 i + row); PAR 64 -- one PAR word, its exact total
+__device__ __forceinline__ u32 rep_acc_rows(u32 acc, u32 t0, u32 t1, u32 t2, u32 t3)
+{
+    if constexpr (PAIR_P64) {
+        const u32 t = pk_sub(pk_add(pk_add(t0, t1), pk_add(t2, t3)), 0x60006000u);   // 4 x 8192 -> 8192
+        return rep_acc(acc, t);
+    } else {
+        return rep_acc(rep_acc(rep_acc(rep_acc(acc, t0), t1), t2), t3);
+    }
+}
+// the exact SM chain (rep_any_zero fallback) over one register: SM16 per lane v (row r = word
+// 4 i + r) -> the ADD_TREE of each PAR word (PAR 64: words (0, 2), (1, 3), then the halves,
+// then the positions -- rep_add_tree's order), accumulated with the REP clamp
+__device__ __forceinline__ u32 rep_sm_rows(u32 acc, u32 v, const Lanes &ln)
+{
+    if constexpr (PAIR_P64) {
+        const X2 q = swap32(v);
+        const u32 v1 = G_sm<0>(q.a, q.b, 0u);
+        const X2 r = swap16(v1);
+        return G_sm<REPSAT>(row_add_tree(G_sm<0>(r.a, r.b, 0u), ln), acc, 0u);
+    } else {
+        const X4 t = rows4(row_add_tree(v, ln));
+        acc = G_sm<REPSAT>(t.t0, acc, 0u);
+        acc = G_sm<REPSAT>(t.t1, acc, 0u);
+        acc = G_sm<REPSAT>(t.t2, acc, 0u);
+        return G_sm<REPSAT>(t.t3, acc, 0u);
+    }
+}
+
 constexpr int PAIR_MAX_WAVES = 8;   // launch bound 512 threads: <= 256 VGPRs per wave
 
 // ---------------------------------------------------------------------------------------
@@ -566,8 +619,8 @@ __device__ __noinline__ void pchain(PairCtx c, int k, int n4, int ub, u32 gm)
 template <int D, bool ROOT, bool ISG0>
 __device__ __forceinline__ void pop_chain(const PairCtx &c, int k, int n4, int ub, u32 gm)
 {
-    if (c.W > 1 && ((n4 >> (D - 1)) >> 3) < 2 * c.W) {
-        // fewer than two columns per wave: the records one by one, each split over all the
+    if (c.W > 1 && ((n4 >> (D - 1)) >> 3) < 4 * c.W) {
+        // fewer than four columns per wave: the records one by one, each split over all the
         // waves by row groups (what the chain saves in reads is less than the waves it idles)
         pop_fg_split<ISG0>(c, k, n4, ub);
 #pragma unroll
@@ -611,7 +664,7 @@ __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int 
         for (int o = 0; o < 2; o++) {
             const u32 lam = F_sm(prow(a, o), prow(b, o)), sg = pk_sra(lam, 15);
             const X4 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
-            acc = rep_acc(rep_acc(rep_acc(rep_acc(acc, t.t0), t.t1), t.t2), t.t3);
+            acc = rep_acc_rows(acc, t.t0, t.t1, t.t2, t.t3);
         }
     }
     if (rep_any_zero(acc)) {
@@ -621,13 +674,7 @@ __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int 
             u32 a, b;
             psrc2<ROOT, SL>(c, s0, n4, j, a, b);
 #pragma unroll
-            for (int o = 0; o < 2; o++) {
-                const X4 t = rows4(row_add_tree(F_sm(prow(a, o), prow(b, o)), ln));
-                acc = G_sm<REPSAT>(t.t0, acc, 0u);
-                acc = G_sm<REPSAT>(t.t1, acc, 0u);
-                acc = G_sm<REPSAT>(t.t2, acc, 0u);
-                acc = G_sm<REPSAT>(t.t3, acc, 0u);
-            }
+            for (int o = 0; o < 2; o++) acc = rep_sm_rows(acc, F_sm(prow(a, o), prow(b, o)), ln);
         }
     }
     const u32 full = pk_sra(acc, 15);   // two's complement or SM16: the decision is bit 15 / 31
@@ -652,6 +699,7 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
     u32 acc = 0, par = 0, klo = 0xFFFFFFFFu, khi = 0xFFFFFFFFu, ud = 0;
     u32 da = 0, db = 0;
     const int row = (int)c.row();
+    const u32 ksub = SPC ? spc_sub((u32)row, c.lanes()) : 0u;
     for (int j = j0; j < j1; j++) {
         if (((j - j0) & 1) == 0) psrc2<ROOT, SL>(c, s0, n4, j, da, db);
         const u32 a = prow(da, j & 1), b = prow(db, j & 1);
@@ -670,7 +718,7 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
         }
         if constexpr (SPC) {
             par ^= h;
-            const u32 wk = (u32)(4 * j + row) << 4;   // word index in the node
+            const u32 wk = ((u32)j << 6) | ksub;   // (word, position) order
             klo = __builtin_elementwise_min(klo, ((lam & 0xFFu) << 24) | wk);
             khi = __builtin_elementwise_min(khi, (((lam >> 16) & 0xFFu) << 24) | wk);
         }
@@ -678,8 +726,8 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
     if constexpr (SPC) {
         const Lanes ln = c.lanes();
         par = row_xor(par);
-        klo = row_min_u32(klo | ln.br);
-        khi = row_min_u32(khi | ln.br);
+        klo = row_min_u32(klo);
+        khi = row_min_u32(khi);
         {   // across the four rows
             X2 p = swap16(par);
             par = p.a ^ p.b;
@@ -709,8 +757,8 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
             }
         }
         // the flipped word: 4 (key >> 6) + ((key >> 4) & 3), position bitrev4^-1(key & 15)
-        const bool flo = (par & 0x8000u) && (klo & 15u) == ln.br && (int)((klo >> 4) & 3u) == row;
-        const bool fhi = (par & 0x80000000u) && (khi & 15u) == ln.br && (int)((khi >> 4) & 3u) == row;
+        const bool flo = (par & 0x8000u) && (klo & 63u) == ksub;
+        const bool fhi = (par & 0x80000000u) && (khi & 63u) == ksub;
         if (flo) {
             const int l = l0 + (int)((klo >> 6) & 0x3FFFFu);
             c.bst(l >> 4, c.bld(l >> 4) ^ (1u << (l & 15)));

@@ -168,15 +168,13 @@ struct PairGen {
             for (int i = 0; i < n4; i++) {
                 o << "    { const X4 t_ = rows4(row_sum_biased(F_split_biased<" << i % 16 << ">(" << M(pd, i) << ", "
                   << M(pd, n4 + i) << ", FS_[" << i / 16 << "])));\n"
-                  << "      acc_ = rep_acc(rep_acc(rep_acc(rep_acc(acc_, t_.t0), t_.t1), t_.t2), t_.t3); }\n";
+                  << "      acc_ = rep_acc_rows(acc_, t_.t0, t_.t1, t_.t2, t_.t3); }\n";
                 chunk_fence(i, n4);
             }
             o << "    if (rep_any_zero(acc_)) {\n      acc_ = 0u;\n";
             for (int i = 0; i < n4; i++)
-                o << "      { const X4 t_ = rows4(row_add_tree(F_split_sm<" << i % 16 << ">(" << M(pd, i) << ", "
-                  << M(pd, n4 + i) << ", FS_[" << i / 16 << "]), ln));\n"
-                  << "        acc_ = G_sm<REPSAT>(t_.t0, acc_, 0u); acc_ = G_sm<REPSAT>(t_.t1, acc_, 0u);\n"
-                  << "        acc_ = G_sm<REPSAT>(t_.t2, acc_, 0u); acc_ = G_sm<REPSAT>(t_.t3, acc_, 0u); }\n";
+                o << "      acc_ = rep_sm_rows(acc_, F_split_sm<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i)
+                  << ", FS_[" << i / 16 << "]), ln);\n";
             o << "    }\n    const u32 full_ = pk_sra(acc_, 15);\n";
             for (int j = 0; j < n4; j += 16) put(l0 + j, n4 < 16 ? n4 : 16, "full_");
             o << "  }\n";
@@ -190,7 +188,7 @@ struct PairGen {
               << "], LT_[" << np << "] = {};\n";
             for (int k = 0; k < np; k++)
                 o << "    X_[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << " ^ " << U(ub, k) << ";\n";
-            if (spc) o << "    u32 klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu, par_ = 0u;\n    const u32 rw_ = c.row << 4;\n";
+            if (spc) o << "    u32 klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu, par_ = 0u;\n    const u32 rw_ = spc_sub(c.row, ln);\n";
             for (int i = 0; i < n4; i++) {
                 if (spc)
                     o << "    { const u32 l_ = G_split<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i) << ", X_["
@@ -216,15 +214,15 @@ struct PairGen {
                 }
                 o << "    par_ = ((__builtin_popcount(par_ & 0xFFFFu) & 1u) << 15) | ((__builtin_popcount(par_ >> 16) & 1u) << 31);\n"
                      "    par_ = row_xor(par_);\n"
-                     "    klo_ = row_min_u32(klo_ | ln.br); khi_ = row_min_u32(khi_ | ln.br);\n"
+                     "    klo_ = row_min_u32(klo_); khi_ = row_min_u32(khi_);\n"
                      "    { X2 p_ = swap16(par_); par_ = p_.a ^ p_.b; p_ = swap32(par_); par_ = p_.a ^ p_.b;\n"
                      "      X2 a_ = swap16(klo_), b_ = swap16(khi_);\n"
                      "      klo_ = __builtin_elementwise_min(a_.a, a_.b); khi_ = __builtin_elementwise_min(b_.a, b_.b);\n"
                      "      a_ = swap32(klo_); b_ = swap32(khi_);\n"
                      "      klo_ = __builtin_elementwise_min(a_.a, a_.b); khi_ = __builtin_elementwise_min(b_.a, b_.b); }\n"
                      "    const u32 ilo_ = (klo_ >> 6) & 0x3FFFFu, ihi_ = (khi_ >> 6) & 0x3FFFFu;\n"
-                     "    const bool flo_ = land(land(par_ & 0x8000u, (klo_ & 15u) == ln.br), ((klo_ >> 4) & 3u) == c.row);\n"
-                     "    const bool fhi_ = land(land(par_ & 0x80000000u, (khi_ & 15u) == ln.br), ((khi_ >> 4) & 3u) == c.row);\n";
+                     "    const bool flo_ = land(par_ & 0x8000u, (klo_ & 63u) == rw_);\n"
+                     "    const bool fhi_ = land(par_ & 0x80000000u, (khi_ & 63u) == rw_);\n";
                 if (n4 <= 16) {
                     o << "    bw[" << l0 / 16 << "] ^= sel(flo_, 1u << (" << l0 % 16 << " + ilo_), 0u) | sel(fhi_, 0x10000u << ("
                       << l0 % 16 << " + ihi_), 0u);\n";
@@ -272,10 +270,11 @@ struct PairGen {
               << "[0]);\n    " << M(cd, 0) << " = pk_min(m_.a, m_.b); s" << cd << "[0] = s_.a ^ s_.b;\n  }\n";
             break;
         case POLAR_OP_G:
-            o << "  { // G n " << n << " upos " << op.upos << "\n    const X2 m_ = " << sw << "(" << M(pd, 0) << "), s_ = "
-              << sw << "(s" << pd << "[0]);\n    u32 LT_ = 0u; const u32 X_ = s_.a ^ s_.b ^ " << small_u(n, op.upos)
-              << ";\n    " << M(cd, 0) << " = G_split<0>(m_.a, m_.b, X_, LT_);\n    s" << cd
-              << "[0] = s_.b ^ (X_ & ~LT_);\n  }\n";
+            // (G_extended inside a PAR 64 word, fb bit 19: no clamp)
+            o << "  { // G n " << n << " upos " << op.upos << ((op.fb & FB_EXACT) ? " exact" : "") << "\n    const X2 m_ = "
+              << sw << "(" << M(pd, 0) << "), s_ = " << sw << "(s" << pd << "[0]);\n    u32 LT_ = 0u; const u32 X_ = s_.a ^ s_.b ^ "
+              << small_u(n, op.upos) << ";\n    " << M(cd, 0) << " = " << ((op.fb & FB_EXACT) ? "G_split_x" : "G_split")
+              << "<0>(m_.a, m_.b, X_, LT_);\n    s" << cd << "[0] = s_.b ^ (X_ & ~LT_);\n  }\n";
             break;
         case POLAR_OP_FLEAF:
         case POLAR_OP_GLEAF: {
@@ -288,7 +287,8 @@ struct PairGen {
             } else {
                 o << "    const u32 xm_ = opaque(plane_mask<0>(s_.a ^ s_.b ^ " << small_u(1, op.upos) << "));\n"
                   << "    const u32 d_ = pk_sub(m_.a, m_.b);\n"
-                  << "    const u32 M_ = pk_min(bsel(xm_, pk_abs_i16(d_), pk_add(m_.a, m_.b)), GSAT2);\n"
+                  << ((op.fb & FB_EXACT) ? "    const u32 M_ = bsel(xm_, pk_abs_i16(d_), pk_add(m_.a, m_.b));\n"
+                                         : "    const u32 M_ = pk_min(bsel(xm_, pk_abs_i16(d_), pk_add(m_.a, m_.b)), GSAT2);\n")
                   << "    const u32 S_ = plane_mask<0>(s_.b) ^ (xm_ & ~pk_sra(d_, 15));\n";
             }
             o << "    " << x << " = leaf_ms<0x" << std::hex << (op.fb & 0xFFFFu) << std::dec << "u, 0, 16>(M_, S_, ln);\n  }\n";
@@ -519,7 +519,8 @@ void pair_kernel(std::ostringstream &o, const char *name, const std::vector<pola
 std::string pair_source(const polar_sc_plan &p)
 {
     std::ostringstream o;
-    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits << "\n#include \"polar_sc_pair.h\"\n"
+    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits << "\n#define POLAR_LPAR " << (p.cfg.par == 64 ? 6 : 4)
+      << "\n#include \"polar_sc_pair.h\"\n"
       << "namespace polar {\n" << kPairCH;
     int lg = 0;
     while ((1 << lg) < p.sub_words) lg++;

@@ -174,6 +174,29 @@ def G_split(I, ma, mb, X, LT):
     return pk_min(bsel(xm, pk_abs_i16(d), pk_add(ma, mb)), GSAT2), LT
 
 
+def G_split_x(I, ma, mb, X, LT):
+    """G_split without the clamp (PAR 64 G_extended)"""
+    xm = plane_mask(I, X)
+    d = pk_sub(ma, mb)
+    return bsel(xm, pk_abs_i16(d), pk_add(ma, mb)), plane_put(I, LT, d)
+
+
+def spc_sub(row, ln):
+    """SPC key bits below the word index, PAR 16: (row, bitrev4(position))"""
+    return (V(row) << 4) | ln.br
+
+
+def rep_acc_rows(acc, t0, t1, t2, t3):
+    return rep_acc(rep_acc(rep_acc(rep_acc(acc, t0), t1), t2), t3)
+
+
+def rep_sm_rows(acc, v, ln):
+    t = rows4(row_add_tree(v, ln))
+    for tt in (t.t0, t.t1, t.t2, t.t3):
+        acc = G_sm(REPSAT, tt, acc, 0)
+    return acc
+
+
 def F_split_biased(I, ma, mb, FS):
     m, s = pk_min(ma, mb), plane_mask(I, FS)
     return pk_add(pk_sub(m ^ s, s), 0x02000200)
@@ -306,7 +329,7 @@ def conv_pair(raw):
 
 
 # ---- transpiler of a generated subtree decoder ------------------------------------------
-_REF_FNS = ("F_root", "G_root", "G_split")
+_REF_FNS = ("F_root", "G_root", "G_split", "G_split_x")
 
 
 def _split_top(s, sep=","):

@@ -84,6 +84,15 @@ def gpu_plans():
     return out
 
 
+def gpu_par64_plans():
+    """(name, mask, config fields, tuning) of the PAR 64 GPU tests (prewarmed by build())."""
+    out = [(n, util.mask(n), {"par": 64}, {"kernel": 3}) for n, _ in PAR64_MASKS]
+    for N in (8192, 32768):
+        for i, m in enumerate(struct_masks(N)[:2]):
+            out += [("struct%d_%d" % (N, i), m, {"par": 64}, {"kernel": 3, "sub_words": sw}) for sw in (64, 256)]
+    return out
+
+
 def run(pkg, torch, dec, llr):
     out = dec.decode(torch.from_numpy(np.ascontiguousarray(llr)).cuda())
     torch.cuda.synchronize()
@@ -253,3 +262,54 @@ def test_pair_register_budget(pkg, tmp_path, monkeypatch):
         for name, vgpr, agpr, wg in cr.kernels(str(co)):
             over, total = cr.over_budget(vgpr, agpr, wg)
             assert not over, "%s: %s vgpr %d agpr %d for %d threads" % (co.name, name, vgpr, agpr, wg)
+
+
+PAR64_MASKS = [("frozen_n_2048_k_1024", 9), ("frozen_n_16384_k_8192", 5), ("frozen_n_16384_k_14746", 5),
+               ("frozen_n_65536_k_32768", 3)]
+
+
+def par64_config(pkg, q=6):
+    c = pkg.default_config()
+    c.par, c.llr_bits = 64, q
+    return c
+
+
+def test_pair_par64_plan(pkg):
+    """PAR 64 (script_tests.sh:11, 124) takes the pair kernel: subtrees cut at PAR-word
+    multiples, the PAR word's exact leaf expanded into F / G_extended / 16-LLR leaf records."""
+    d = pkg.Decoder(util.mask("frozen_n_65536_k_32768"), config=par64_config(pkg))
+    s = d.stats
+    assert (s["kernel"], s["sub_words"]) == (3, 256) and s["n_sub_calls"] > 0
+    src = d.kernel_source()
+    assert "#define POLAR_LPAR 6" in src and "G_split_x" in src
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,batch", PAR64_MASKS)
+def test_pair_par64_parity(pkg, cuda, oracle_mod, name, batch):
+    """PAR 64 on the pair kernel against the oracle's literal FSM at PAR 64: REP over the PAR
+    word's exact ADD_TREE (words (0, 2), (1, 3), halves, positions) with the 2^(Q+5)-1 clamp,
+    SPC ties by (PAR word, bitrev6(position)), G_extended inside the PAR word."""
+    mask = util.mask(name)
+    llr, _ = util.synth_frames(mask, batch, ebn0_db=1.0, seed=batch)
+    edge = np.random.default_rng(batch).choice(np.array([0, 0, 1, -1, 31, -31, -32, 5], np.int8), size=(2, mask.size))
+    llr = np.concatenate([llr, edge])
+    dec = pkg.Decoder(mask, config=par64_config(pkg))
+    assert dec.stats["kernel"] == 3
+    _assert_same(run(pkg, cuda, dec, llr), oracle_mod.decode_fsm(mask, llr, par=64), "PAR 64 " + name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [8192, 32768])
+def test_pair_par64_structured(pkg, cuda, oracle_mod, N):
+    """PAR 64 on structured masks (R0 / R1 / REP / SPC nodes of every size), subtrees of 64
+    and 256 words, AWGN and edge LLRs."""
+    rng = np.random.default_rng(N + 64)
+    for rep, mask in enumerate(struct_masks(N)[:2]):
+        llr, _ = util.synth_frames(mask, 4, ebn0_db=0.5, seed=rep)
+        edge = rng.choice(np.array([0, 0, 1, -1, 31, -31, -32, 5], np.int8), size=(3, N))
+        llr = np.concatenate([llr, edge])
+        ref = oracle_mod.decode_fsm(mask, llr, par=64)
+        for sw in (64, 256):
+            dec = pkg.Decoder(mask, config=par64_config(pkg), tuning={"kernel": 3, "sub_words": sw})
+            _assert_same(run(pkg, cuda, dec, llr), ref, "PAR 64 N=%d rep %d S=%d" % (N, rep, sw))
