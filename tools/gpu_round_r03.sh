@@ -2,7 +2,7 @@
 # Round 3 measurement at HEAD: the whole -m gpu suite, smoke(), the default bench line (C2
 # headline + C3 / C5 / C5-share secondary entries + CPU baseline), kernel-trace stats and the
 # FETCH_SIZE / WRITE_SIZE passes (separate runs) of every config, SQ passes of C2 and C3.
-# usage: bash tools/gpu_round_r03.sh <tag> [skip-tests]
+# usage: bash tools/gpu_round_r03.sh <tag> [skip-tests|tests] [c5ab]
 set -euo pipefail
 TAG=${1:?tag}
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -37,3 +37,16 @@ prof c3 frozen_n_65536_k_32768 4096 4
 prof c5 frozen_n_262144_k_131072 512 3
 prof c5b64 frozen_n_262144_k_131072 64 3
 echo "all ok"
+for b in "$ROOT"/build_tools/pair_stamps_*; do
+  case "$b" in *.hip) continue;; esac
+  timeout -k 10 60 "$b" > "$OUT/$(basename "$b").txt" 2>&1
+done
+echo "stamps ok"
+if [ "${3:-}" = "c5ab" ]; then
+  cd "$ROOT"
+  for r in 1 2; do
+    timeout -k 10 300 python -u tools/pair_ab.py --kernels 3 --configs c5,c5_64 > "$OUT/ab_default_r$r.jsonl" 2>> "$OUT/ab.err"
+    timeout -k 10 300 python -u tools/pair_ab.py --kernels 3 --configs c5,c5_64 --tuning chain_max=1 > "$OUT/ab_nochain_r$r.jsonl" 2>> "$OUT/ab.err"
+  done
+  echo "c5 ab ok"
+fi
