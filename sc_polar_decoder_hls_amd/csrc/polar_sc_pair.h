@@ -619,9 +619,10 @@ __device__ __noinline__ void pchain(PairCtx c, int k, int n4, int ub, u32 gm)
 template <int D, bool ROOT, bool ISG0>
 __device__ __forceinline__ void pop_chain(const PairCtx &c, int k, int n4, int ub, u32 gm)
 {
-    if (c.W > 1 && ((n4 >> (D - 1)) >> 3) < 4 * c.W) {
-        // fewer than four columns per wave: the records one by one, each split over all the
-        // waves by row groups (what the chain saves in reads is less than the waves it idles)
+    if (c.W > 1) {
+        // several waves per pair (small batches): the records one by one, each split over all
+        // the waves by row groups -- same-box A/B at C5 (W = 8): 1.51 ms this way vs 1.63 ms
+        // chained (profiles/r03_ab/chain_c5_ab.txt); the chains pay at W = 1 (C3 -15 %)
         pop_fg_split<ISG0>(c, k, n4, ub);
 #pragma unroll
         for (int i = 1; i < D; i++) {
