@@ -217,44 +217,71 @@ def timed_decodes(torch, sharding, dist, coll_dev, dec, batches, outs, steps, wa
     return sharding.max_over_ranks([elapsed, kern_ms], dist, coll_dev)
 
 
-# Secondary entries of the same JSON line (BASELINE.json configs[2] and [4]): timed in the same
-# process after the headline C2 region, each with its own roofline and a 4-frame oracle check.
-# name: (mask, frames per GPU or None = the 512-frame C5 batch sharded over the ranks, note)
+# Secondary entries of the same JSON line (BASELINE.json configs[2] and [4], and the formats of
+# the reference's own sweep script): timed in the same process after the headline C2 region,
+# each with its own roofline and a 4-frame oracle check.
+# name: (mask, frames per GPU or None = the 512-frame C5 batch sharded over the ranks, datapath
+# fields of polar_sc_config that differ from the shipped one, note)
+SWEEP_FRAMES = 4096
 SECONDARY = (
-    ("c3", "frozen_n_65536_k_32768", 4096, "BASELINE configs[2]: N=65536 K=32768, 4096-frame batch per GPU"),
-    ("c5", "frozen_n_262144_k_131072", None, "BASELINE configs[4]: N=262144 K=131072, 512 frames sharded over the GPUs"),
-    ("c5_share64", "frozen_n_262144_k_131072", 64,
+    ("c3", "frozen_n_65536_k_32768", 4096, {}, "BASELINE configs[2]: N=65536 K=32768, 4096-frame batch per GPU"),
+    ("c5", "frozen_n_262144_k_131072", None, {}, "BASELINE configs[4]: N=262144 K=131072, 512 frames sharded over the GPUs"),
+    ("c5_share64", "frozen_n_262144_k_131072", 64, {},
      "C5's 8-GPU share (64 frames) on one GPU: the per-GPU latency of configs[4] at 8 GPUs"),
+    # script/script_tests.sh:11,124 runs PAR 16 and PAR 64; :7-9 the rate-0.9 codes at QUANT 8
+    ("par16_n16384", "frozen_n_16384_k_8192", SWEEP_FRAMES, {},
+     "PAR 16 (the shipped datapath) on N=16384 K=8192, %d frames per GPU: the PAR 64 entry's baseline" % SWEEP_FRAMES),
+    ("par64_n16384", "frozen_n_16384_k_8192", SWEEP_FRAMES, {"par": 64},
+     "PAR 64 (script_tests.sh:11,124) on N=16384 K=8192, %d frames per GPU" % SWEEP_FRAMES),
+    ("q8_n16384_k14746", "frozen_n_16384_k_14746", SWEEP_FRAMES, {"llr_bits": 8},
+     "QUANT 8 (LLR_BITS 8) on the rate-0.9 code N=16384 K=14746 of script_tests.sh:7-9, %d frames per GPU"
+     % SWEEP_FRAMES),
 )
 
 
-def roofline_entry(name, N, per_gpu, kern_ms):
+def roofline_entry(name, N, per_gpu, kern_ms, dec, fmt=None):
     """HBM roofline of one decode launch sequence: algorithmic bytes (1.125 N per frame) over
-    the event-timed kernel time; traffic from the committed PMC summary of the same workload."""
+    the event-timed kernel time; traffic from the committed PMC summary of the same workload,
+    used only when that profile is of the code object timed here (its code_key, recorded by
+    tools/prof_decode.py, equals this plan's)."""
     bytes_per_launch = 1.125 * N * per_gpu
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src, prof = None, None, None
-    prof_path = TRAFFIC_PROFILES.get((name, per_gpu))
+    traffic, traffic_src, prof, note = None, None, None, None
+    key = dec.launch_info(per_gpu)["code_key"]
+    prof_path = TRAFFIC_PROFILES.get((name, per_gpu)) if not fmt else None
     if prof_path and os.path.exists(prof_path):
         with open(prof_path) as f:
             prof = json.load(f)
-        if "hbm_read_bytes_corrected" in prof and "hbm_write_bytes" in prof:
+        if prof.get("code_key") != key:
+            note = "profile %s is of code object %s, this run timed %s: traffic not reported" % (
+                os.path.relpath(prof_path, ROOT), prof.get("code_key"), key)
+            prof = None
+        elif "hbm_read_bytes_corrected" in prof and "hbm_write_bytes" in prof:
             traffic = prof["hbm_read_bytes_corrected"] + prof["hbm_write_bytes"]
             traffic_src = os.path.relpath(prof_path, ROOT)
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
-            "traffic_source": traffic_src, "kernel_ms": kern_ms,
-            "algorithmic_bytes_per_launch": bytes_per_launch}, prof
+    ent = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+           "traffic_source": traffic_src, "kernel_ms": kern_ms, "code_key": key,
+           "algorithmic_bytes_per_launch": bytes_per_launch}
+    if note:
+        ent["traffic_note"] = note
+    return ent, prof
 
 
-def secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mask_name, per_gpu, note, rank, world, dev,
-                    stream):
+def secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mask_name, per_gpu, fmt, note, rank, world,
+                    dev, stream):
     """One secondary configuration: resident rotated C-sim batches, a short timed loop (same
     barrier / synchronize / max-over-ranks bracket as the headline), roofline, and a 4-frame
-    bit-exact check against the oracle on rank 0."""
+    bit-exact check against the oracle on rank 0. fmt: polar_sc_config fields that differ from
+    the shipped datapath (par, llr_bits)."""
     import util
     mask = util.mask(mask_name)
     N, K = mask.size, int(mask.sum())
+    cfg = None
+    if fmt:
+        cfg = pkg.default_config()
+        for f, v in fmt.items():
+            setattr(cfg, f, v)
     if per_gpu is None:
         per_gpu = sharding.shard_bounds(512, world, rank)[1]
     counts = [per_gpu]
@@ -264,7 +291,7 @@ def secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mask_name, 
         dist.all_reduce(t)
         counts = [int(v) for v in t.tolist()]
     frame0 = int(sum(counts[:rank]))
-    dec = pkg.Decoder(mask)
+    dec = pkg.Decoder(mask, config=cfg)
     dec.prepare(per_gpu)
     nb = max(1, min(8, -(-ROTATE_BYTES // (per_gpu * N))))
     batches = make_batches(pkg, torch, args, mask, per_gpu, frame0, sum(counts), dev, args.ebn0, nb)
@@ -273,17 +300,17 @@ def secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mask_name, 
     warm = 3
     elapsed, kern_ms = timed_decodes(torch, sharding, dist, coll_dev, dec, batches, outs, steps, warm, stream)
     frames_all = int(sum(counts))
-    ent = {"workload": note, "mask": mask_name, "N": N, "K": K, "frames_per_gpu": per_gpu,
+    ent = {"workload": note, "mask": mask_name, "N": N, "K": K, "datapath": dict(fmt), "frames_per_gpu": per_gpu,
            "frames_all_ranks": frames_all, "steps": steps, "warmup": warm, "rotated_batches": nb,
            "ms_per_step": elapsed / steps * 1e3, "info_bits_per_s": frames_all * steps / elapsed * K,
            "frames_per_sec": frames_all * steps / elapsed, "kernel": kernel_name(dec.stats)}
-    ent["roofline"], _ = roofline_entry(mask_name, N, per_gpu, kern_ms)
+    ent["roofline"], _ = roofline_entry(mask_name, N, per_gpu, kern_ms, dec, fmt)
     if rank == 0 and args.check > 0:
         from oracle import oracle
         last = (steps - 1) % nb
         nchk = min(4, per_gpu)
         got = pkg.unpack_bits(outs[last][:nchk].cpu().numpy(), N)
-        ref = oracle.decode_fsm(mask, batches[last][0][:nchk].cpu().numpy())
+        ref = oracle.decode_fsm(mask, batches[last][0][:nchk].cpu().numpy(), **fmt)
         ent["parity_check"] = {"frames": nchk, "bit_exact": bool((got == ref).all())}
     dec.close()
     del batches, outs
@@ -456,12 +483,18 @@ def main():
         c = [float(v) for v in cnt.cpu().tolist()]
         fer, ber = c[1] / per_gpu, c[2] / (per_gpu * N)
         if dist is not None:
+            # every rank's own counts (reported beside the total, so that the sum can be checked)
+            mine = cnt.to(coll_dev, torch.float64)
+            per_rank = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(per_rank, mine)
             # the job's error totals: device counts summed over the ranks (RCCL all-reduce)
             sharding.sum_over_ranks(cnt, dist, coll_dev)
             t = [int(v) for v in cnt.cpu().tolist()]
             errors_all = {"frames": frames_all, "frame_errors": t[1], "bit_errors": t[2],
                           "bit_errors_mod1024_sum": t[0], "frame_error_rate": t[1] / frames_all,
-                          "bit_error_rate": t[2] / (frames_all * N)}
+                          "bit_error_rate": t[2] / (frames_all * N),
+                          "per_rank": [{"frames": counts[r], "frame_errors": int(v[1].item()),
+                                        "bit_errors": int(v[2].item())} for r, v in enumerate(per_rank)]}
     else:
         xhat = pkg.unpack_bits(out[: min(per_gpu, 4096)].cpu().numpy(), N)
         xs = x[: xhat.shape[0]].cpu().numpy()
@@ -490,14 +523,18 @@ def main():
     secondary = None
     if args.secondary and args.config == "c2" and not args.batch:
         secondary = {}
-        for key, mname, pg, note in SECONDARY:
+        for key, mname, pg, fmt, note in SECONDARY:
             if key == "c5_share64" and world != 1:
                 continue   # at 8 GPUs the c5 entry already is the 64-frame share
-            secondary[key] = secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mname, pg, note, rank,
-                                             world, dev, stream)
+            secondary[key] = secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mname, pg, fmt, note,
+                                             rank, world, dev, stream)
+        if "par16_n16384" in secondary and "par64_n16384" in secondary:
+            # script_tests.sh sweeps PAR 16 and 64 on the same codes: PAR 64's cost relative to 16
+            secondary["par64_over_par16_time"] = (secondary["par64_n16384"]["ms_per_step"] /
+                                                  secondary["par16_n16384"]["ms_per_step"])
 
     if rank == 0:
-        roof, prof = roofline_entry(name, N, per_gpu, kern_ms)
+        roof, prof = roofline_entry(name, N, per_gpu, kern_ms, dec)
         prof_path = TRAFFIC_PROFILES.get((name, per_gpu))
         valu = None
         if prof is not None:

@@ -74,14 +74,17 @@ typedef struct polar_sc_tuning {
     int32_t kernel;           /* 0 = automatic; 1 = the schedule interpreter for every N
                                  (no per-mask / generated-subtree code); 2 = the hybrid
                                  kernel (8-frame groups) for N > 1024; 3 = the pair kernel
-                                 (one frame pair per wave) for N >= 2048 */
+                                 (one frame pair per wave) for N >= 2048 in the shipped
+                                 datapath or PAR 64. A forced kernel or sub_words the plan
+                                 cannot use is an error (-ENOTSUP / -EINVAL), never a
+                                 silent fallback */
     int32_t waves_per_group;  /* interpreter / hybrid launches: waves per 8-frame group, 0 =
                                  automatic (more when the batch cannot fill the GPU), else 1,
                                  2, 4, 8 or 16 (capped at the hybrid kernel's bound) */
     int32_t sub_words;        /* hybrid / pair plans: generated subtree size in 16-LLR words,
                                  0 = automatic (hybrid: 64, 128 from N = 32768; pair:
                                  min(256, N / 32)), else a power of two 2..128 (hybrid) or
-                                 16..256 and <= N / 32 (pair) */
+                                 32..256 and <= N / 32 (pair) */
     int32_t tier_words;       /* hybrid HBM-scratch plans: F / G records of >= this many words
                                  run as grid launches; 0 = automatic, -1 = no grid tier */
     int32_t lds_slots;        /* HBM-scratch plans: stage slots held in LDS, 0 = automatic,
@@ -89,7 +92,10 @@ typedef struct polar_sc_tuning {
     int32_t hybrid_waves;     /* hybrid plans: waves per group of the kernel's launch bound,
                                  0 = automatic (8), else 4 or 8 */
     int32_t chain_max;        /* pair plans: F / G records fused into one descent chain
-                                 (pop_chain), 0 = automatic (3), 1 = no fusion, 2 or 3 */
+                                 (pop_chain), 0 = automatic (3), 1 = no fusion, 2, 3 or 4
+                                 (4 can exceed the register budget of an 8-wave block: the
+                                 launch then runs fewer waves per pair, see
+                                 polar_sc_plan_launch_info) */
     int32_t reserved;         /* must be 0 */
 } polar_sc_tuning;
 
@@ -158,16 +164,25 @@ typedef struct polar_sc_plan_stats {
                                          N <= 1024)                                      */
     uint32_t lds_bytes_per_wave;      /* LDS footprint of one 8-frame group: storage 2:
                                          the staged channel frames; 0: all stage slots and
-                                         partial sums; 1: the lower tree levels          */
+                                         partial sums; 1: the lower tree levels. Pair plans
+                                         (kernel 3): per frame pair, the subtree-root slot
+                                         level only -- the launch puts more levels in LDS
+                                         when the batch leaves room (up to ~129 KB per
+                                         pair; polar_sc_plan_launch_info.lds_bytes)      */
     uint64_t scratch_bytes_per_wave;  /* HBM scratch of one 8-frame group (storage 1:
-                                         upper tree levels + partial sums), else 0       */
+                                         upper tree levels + partial sums), else 0. Pair
+                                         plans: per frame pair (slot rows + partial sums) */
     uint32_t kernel;                  /* decode kernel: 0 = schedule interpreter,
                                          1 = per-mask kernel (N <= 1024), 2 = hybrid
                                          (interpreter for the upper tree levels, generated
-                                         code for every mixed subtree of sub_words)      */
-    uint32_t sub_words;               /* hybrid: subtree size in 16-LLR words, else 0     */
-    uint32_t n_sub_kinds;             /* hybrid: distinct generated subtree decoders      */
-    uint32_t n_sub_calls;             /* hybrid: subtree decoder calls per frame group    */
+                                         code for every mixed subtree of sub_words),
+                                         3 = pair kernel (one frame pair per wave, generated
+                                         subtree decoders, upper levels over stage-slot
+                                         rows; the default for N >= 2048)                */
+    uint32_t sub_words;               /* hybrid / pair: subtree size in 16-LLR words      */
+    uint32_t n_sub_kinds;             /* hybrid / pair: distinct generated subtree decoders */
+    uint32_t n_sub_calls;             /* hybrid / pair: subtree decoder calls per frame
+                                         group / pair                                    */
     uint32_t tier_steps;              /* hybrid, large N: launches per decode of the grid
                                          tier (upper-level F / G over all frame groups +
                                          the schedule segments between them), else 0     */
@@ -251,6 +266,27 @@ int polar_sc_plan_compile(const polar_sc_plan *plan);
 
 /* The generated per-mask kernel source (NUL-terminated, truncated to cap); *len = full size. */
 int polar_sc_plan_kernel_source(const polar_sc_plan *plan, char *buf, size_t cap, size_t *len);
+
+/* Launch shape a polar_sc_decode of `batch` frames would use on a device with `cus` compute
+ * units (0 = 256, MI355X), computed on the host (compiles the generated kernel with hipRTC if
+ * needed; no GPU). The waves of a block must fit the 512 registers per SIMD lane that they
+ * share (VGPRs + AGPRs, from the code object's kernel descriptor); the decode lowers its
+ * waves per frame group / pair until they do, and returns -ENOTSUP when not even one wave
+ * fits (waves_per_block = 0 here). */
+typedef struct polar_sc_launch_info {
+    uint32_t kernel;            /* stats.kernel */
+    uint32_t regs;              /* registers per lane of the decode kernel (allocation
+                                   granule), 0 for the hipcc-built interpreter */
+    uint32_t regs_seg;          /* pair plans with a grid tier: the segment kernel's */
+    uint32_t waves_per_block;   /* waves per frame group / pair; 0: not launchable */
+    uint64_t blocks;            /* workgroups of the decode launch */
+    uint32_t lds_bytes;         /* dynamic LDS per block */
+    uint32_t lds_row0;          /* pair plans: first stage-slot row held in LDS */
+    uint64_t code_key;          /* key of the plan's generated code object in the hipRTC
+                                   cache (lib/rtc_cache/<key>.co), 0 = none */
+} polar_sc_launch_info;
+
+int polar_sc_plan_launch_info(const polar_sc_plan *plan, size_t batch, uint32_t cus, polar_sc_launch_info *info);
 
 /* ---- Frame source and error accounting of the reference testbench ---- */
 

@@ -95,6 +95,12 @@ class polar_sc_plan_stats(ctypes.Structure):
                 ("tier_steps", ctypes.c_uint32), ("tier_words", ctypes.c_uint32)]
 
 
+class polar_sc_launch_info(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_uint32), ("regs", ctypes.c_uint32), ("regs_seg", ctypes.c_uint32),
+                ("waves_per_block", ctypes.c_uint32), ("blocks", ctypes.c_uint64), ("lds_bytes", ctypes.c_uint32),
+                ("lds_row0", ctypes.c_uint32), ("code_key", ctypes.c_uint64)]
+
+
 # exported symbols of include/polar_sc.h (tests check that the library exports all of them)
 EXPORTS = (
     "polar_sc_default_config", "polar_sc_plan_create", "polar_sc_plan_create_tuned", "polar_sc_plan_destroy",
@@ -105,7 +111,7 @@ EXPORTS = (
     "polar_sc_abi_version", "polar_sc_plan_compile", "polar_sc_plan_kernel_source",
     "polar_csim_frames", "polar_csim_states", "polar_count_errors",
     "polar_mask_from_order", "polar_write_frozen_tab", "polar_write_parameters_h", "polar_parse_parameters_h",
-    "polar_sc_trace", "polar_sc_decode_i16", "polar_sc_debug_subtree",
+    "polar_sc_trace", "polar_sc_decode_i16", "polar_sc_debug_subtree", "polar_sc_plan_launch_info",
 )
 
 _lib = None
@@ -146,6 +152,7 @@ def lib():
         "polar_sc_selftest_lanes": [p],
         "polar_sc_debug_subtree": [p, u32, p, p],
         "polar_sc_plan_compile": [p],
+        "polar_sc_plan_launch_info": [p, sz, u32, p],
         "polar_sc_plan_kernel_source": [p, ctypes.c_char_p, sz, ctypes.POINTER(sz)],
         "polar_sc_strerror": [i32],
         "polar_sc_abi_version": [],
@@ -334,6 +341,16 @@ class Decoder:
             return False
         _check("polar_sc_plan_compile", rc)
         return True
+
+    def launch_info(self, batch, cus=0):
+        """Launch shape of a decode of `batch` frames (polar_sc_plan_launch_info, host only:
+        compiles the generated kernel if needed) as a dict; code_key as 16 hex digits."""
+        r = polar_sc_launch_info()
+        _check("polar_sc_plan_launch_info", lib().polar_sc_plan_launch_info(self._plan, int(batch), int(cus),
+                                                                            ctypes.byref(r)))
+        d = {f: getattr(r, f) for f, _ in polar_sc_launch_info._fields_}
+        d["code_key"] = "%016x" % r.code_key
+        return d
 
     def kernel_source(self):
         n = ctypes.c_size_t(0)

@@ -1,0 +1,148 @@
+"""The plans the benchmark and the GPU test suite decode with, compiled ahead into
+lib/rtc_cache/ by __graft_entry__.build() (host only, hipRTC), so that a GPU box loads their
+code objects instead of compiling them (C5's pair kernel alone takes ~2 minutes).
+
+Build tooling, not a decode path: the lists here are data (masks of data/frozen_masks.json,
+structured masks from a seeded generator, datapath formats of the reference's sweep scripts);
+tests/test_pair.py and tests/test_gpu_formats.py parametrise over the same lists.
+"""
+import functools
+import json
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MASKS_JSON = os.path.join(ROOT, "data", "frozen_masks.json")
+
+
+@functools.lru_cache(maxsize=None)
+def _masks():
+    with open(MASKS_JSON) as f:
+        return json.load(f)["masks"]
+
+
+def mask_names():
+    return list(_masks())
+
+
+def mask(name):
+    """Information mask (uint8, 1 = info) of a frozen-table fixture (data/frozen_masks.json)."""
+    m = _masks()[name]
+    b = np.frombuffer(bytes.fromhex(m["hex"]), dtype=np.uint8)
+    return np.unpackbits(b, bitorder="little")[: m["N"]].astype(np.uint8)
+
+
+# ---- pair plans (tests/test_pair.py) ---------------------------------------------------------
+def structured_mask(rng, N, p_special=0.7):
+    """Nodes of random size whose frozen pattern is R0 / R1 / REP / SPC (or random), so that the
+    pruned node ops appear at every level (1 .. N/64 words)."""
+    m = (rng.random(N) < 0.5).astype(np.uint8)
+    pos = 0
+    while pos < N:
+        size = 16 << int(rng.integers(0, 6))
+        size = min(size, N - pos)
+        if rng.random() < p_special:
+            kind = int(rng.integers(0, 4))
+            blk = np.zeros(size, np.uint8)
+            if kind == 1:
+                blk[:] = 1                  # R1
+            elif kind == 2:
+                blk[-1] = 1                 # REP
+            elif kind == 3:
+                blk[:] = 1
+                blk[0] = 0                  # SPC
+            m[pos:pos + size] = blk
+        pos += size
+    return m
+
+
+@functools.lru_cache(maxsize=None)
+def struct_masks(N):
+    rng = np.random.default_rng(N)
+    return tuple(structured_mask(rng, N) for _ in range(3))
+
+
+@functools.lru_cache(maxsize=None)
+def wave_mask():
+    return structured_mask(np.random.default_rng(4242), 16384, 0.9)
+
+
+PARITY_MASKS = [("frozen_n_2048_k_1024", 23), ("FB_N2048_K1024", 8), ("frozen_n_4096_k_2048", 17),
+                ("frozen_n_8192_k_4096", 9), ("frozen_n_16384_k_8192", 7), ("frozen_n_32768_k_29492", 5),
+                ("frozen_n_2048_k_1844", 12), ("frozen_n_16384_k_14746", 6), ("frozen_n_65536_k_32768", 5)]
+STRUCT_SUB_WORDS = (32, 64, 256)
+PAR64_MASKS = [("frozen_n_2048_k_1024", 9), ("frozen_n_16384_k_8192", 5), ("frozen_n_16384_k_14746", 5),
+               ("frozen_n_65536_k_32768", 3)]
+
+
+def struct_sub_words(N):
+    return [sw for sw in STRUCT_SUB_WORDS if sw <= N // 32]   # subtrees of at most half the code
+
+
+def gpu_plans():
+    """(name, mask, tuning) of every pair plan the GPU tests decode with."""
+    out = [(n, mask(n), {"kernel": 3}) for n, _ in PARITY_MASKS]
+    for N in (2048, 8192, 32768):
+        for i, m in enumerate(struct_masks(N)):
+            out += [("struct%d_%d" % (N, i), m, {"kernel": 3, "sub_words": sw}) for sw in struct_sub_words(N)]
+    out += [("frozen_n_2048_k_1024", mask("frozen_n_2048_k_1024"), {"kernel": 3, "sub_words": sw})
+            for sw in (32, 64)]
+    out += [("frozen_n_8192_k_4096", mask("frozen_n_8192_k_4096"), {"kernel": 3, "sub_words": 256}),
+            ("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"), {"kernel": 3, "sub_words": 64}),
+            ("wave_mask", wave_mask(), {"kernel": 3, "sub_words": 64}),
+            ("frozen_n_32768_k_29492", mask("frozen_n_32768_k_29492"),
+             {"kernel": 3, "tier_words": 512, "sub_words": 128}),
+            ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), {"kernel": 3}),
+            ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), {"kernel": 3, "tier_words": 1024})]
+    return out
+
+
+def gpu_par64_plans():
+    """(name, mask, config fields, tuning) of the PAR 64 GPU tests and bench entries."""
+    out = [(n, mask(n), {"par": 64}, {"kernel": 3}) for n, _ in PAR64_MASKS]
+    for N in (8192, 32768):
+        for i, m in enumerate(struct_masks(N)[:2]):
+            out += [("struct%d_%d" % (N, i), m, {"par": 64}, {"kernel": 3, "sub_words": sw}) for sw in (64, 256)]
+    return out
+
+
+def cpu_test_plans():
+    """(name, mask, tuning) of the plans the CPU register-budget test compiles (the round-3
+    dispatch abort's configuration: chain_max = 4 on the structured N = 32768 mask)."""
+    return [("struct32768_0", struct_masks(32768)[0], {"kernel": 3, "sub_words": sw, "chain_max": 4}) for sw in (64, 256)]
+
+
+# ---- datapath formats (tests/test_gpu_formats.py): (PAR, SIGMAG, EXTENDED, LLR_BITS) ---------
+FORMATS = [
+    (16, 0, 1, 6), (16, 0, 1, 8), (16, 0, 0, 6), (16, 1, 0, 6), (16, 1, 1, 9), (16, 0, 1, 9),
+    (32, 1, 1, 6), (32, 0, 1, 6), (64, 1, 1, 6), (64, 1, 1, 8), (64, 0, 1, 6), (64, 1, 0, 6), (64, 0, 0, 8),
+    (64, 1, 1, 9),
+    # PAR 4 / 8 (script_RTL_sim.sh:97-330): PAR words as lane groups of a device word
+    (8, 1, 1, 6), (8, 0, 1, 6), (8, 1, 0, 8), (8, 1, 1, 8), (4, 1, 1, 6), (4, 0, 0, 8), (4, 1, 1, 8),
+    (4, 1, 1, 9),
+]
+
+# the rate-0.9 codes of script_tests.sh:7-9 (QUANT 8)
+RATE09_MASKS = ("frozen_n_2048_k_1844", "frozen_n_4096_k_3686", "frozen_n_8192_k_7372", "frozen_n_16384_k_14746")
+
+
+def prewarm_all(verbose=False):
+    """Compile every plan above (and the reference-config plan of every mask fixture) into
+    lib/rtc_cache/."""
+    import sc_polar_decoder_hls_amd as pkg
+    from sc_polar_decoder_hls_amd import _build
+    _build.prewarm({n: mask(n) for n in mask_names() if mask(n).size >= 32}, verbose=verbose)
+    # the schedule interpreter of every datapath format the GPU tests exercise (LDS and
+    # HBM-scratch storage): its source depends on the format, not on the mask
+    cfgs = []
+    for par, sigmag, ext, q in FORMATS:
+        c = pkg.default_config()
+        c.par, c.sigmag, c.extended, c.llr_bits = par, sigmag, ext, q
+        cfgs.append(c)
+    _build.prewarm({n: mask(n) for n in ("FB_N1024_K512", "frozen_n_16384_k_8192")}, configs=cfgs, verbose=verbose)
+    q8 = pkg.default_config()
+    q8.llr_bits = 8
+    _build.prewarm({n: mask(n) for n in RATE09_MASKS}, configs=[q8], verbose=verbose)
+    _build.prewarm_plans(gpu_plans() + cpu_test_plans(), verbose=verbose)
+    _build.prewarm_items(gpu_par64_plans(), verbose=verbose)

@@ -470,7 +470,7 @@ bool tuning_valid(const polar_sc_tuning &t)
            t.tier_words >= -1 && (t.tier_words <= 0 || pow2(t.tier_words)) &&
            (t.lds_slots == 0 || t.lds_slots == 256 || t.lds_slots == 512 || t.lds_slots == 1024) &&
            (t.hybrid_waves == 0 || t.hybrid_waves == 4 || t.hybrid_waves == 8) && t.chain_max >= 0 &&
-           t.chain_max <= 3 && t.reserved == 0;
+           t.chain_max <= 4 && t.reserved == 0;
 }
 
 int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
@@ -504,14 +504,18 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, DevMode 
         st.simds = 4 * cus;
     }
     if ((p->jit || p->hybrid || p->pair) && mode != DEV_I16) {
-        int rc = polar_host::jit_load(*p, st);
-        if (rc) return rc;
+        // pair plans are traced on the schedule interpreter (trace_common): no pair kernel is
+        // built or loaded for a trace
+        if (!(p->pair && interp)) {
+            int rc = polar_host::jit_load(*p, st);
+            if (rc) return rc;
+        }
         if (p->jit && !interp) {
             *out = &st;
             return 0;
         }
         if ((p->jit || p->pair) && interp && p->cfg.llr_bits != 6) {   // traced plan: hipRTC interpreter at POLAR_Q
-            rc = polar_host::jit_load_interp(*p, st);
+            const int rc = polar_host::jit_load_interp(*p, st);
             if (rc) return rc;
         }
     }
@@ -824,6 +828,15 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // 1.55, N = 16384 x 4096 frames 0.39 -> 0.24, N = 4096 x 16384 0.36 -> 0.23);
     // polar_sc_tuning.kernel = 2 keeps the hybrid kernel
     const bool want_pair = !p->jit && jit_on && !kinds && pair_fmt && p->G >= 128 && (t.kernel == 3 || t.kernel == 0);
+    // an explicit kernel / subtree size that cannot be honoured is an error, not a silent
+    // fallback to another kernel (A/B measurements force them)
+    if ((t.kernel == 3 && !want_pair) ||
+        (t.kernel == 2 && !p->jit && !kinds && dflt && t.sub_words && (!sub_ok || (uint32_t)sub_words >= p->G))) {
+        const int rc = t.kernel == 3 ? -ENOTSUP : -EINVAL;
+        delete p;
+        return rc;
+    }
+    bool use_pair = false;
     if (want_pair) {
         int S = std::min<int>(polar_host::PAIR_SUB_WORDS, (int)p->G / 2);
         if (t.sub_words) {
@@ -853,6 +866,27 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
             }
             p->pair_tier = pair_tier_schedule(p->pair_ops, t.tier_words);
         }
+        // generate the kernel source now: a schedule the generator does not support falls back
+        // to the hybrid kernel here (or fails plan creation when the pair kernel was forced)
+        // instead of failing the first decode
+        try {
+            (void)polar_host::pair_source(*p);
+            use_pair = true;
+        } catch (const std::exception &e) {
+            p->jit_log = e.what();
+            if (t.kernel == 3) {
+                delete p;
+                return -ENOTSUP;
+            }
+            p->pair = 0;
+            p->sub_words = 0;
+            p->subs.clear();
+            p->pair_ops.clear();
+            p->pair_tier = polar_host::PairTier{};
+            s.sub_words = s.n_sub_kinds = s.n_sub_calls = 0;
+        }
+    }
+    if (use_pair) {
         // the schedule interpreter's copy (per-op monitor, int16 channel)
         dev_sched = p->ops;
     } else if (!p->jit && jit_on && !kinds && dflt && sub_ok && (uint32_t)sub_words < p->G) {
@@ -1152,6 +1186,42 @@ int polar_sc_plan_kernel_source(const polar_sc_plan *p, char *buf, size_t cap, s
         std::memcpy(buf, src.data(), n);
         buf[n] = 0;
     }
+    return 0;
+}
+
+int polar_sc_plan_launch_info(const polar_sc_plan *p, size_t batch, uint32_t cus, polar_sc_launch_info *info)
+{
+    if (!p || !info || batch == 0 || batch > (size_t)0x7FFFFFF8) return -EINVAL;
+    polar_sc_launch_info r{};
+    r.kernel = p->stats.kernel;
+    const int simds = 4 * (int)(cus ? cus : 256u);
+    int regs = 0, regs_seg = 0;
+    if (p->jit || p->hybrid || p->pair) {
+        if (const int rc = polar_host::jit_compile(*p)) return rc;
+        polar_host::code_regs(*p, regs, regs_seg);
+        if (regs < 0 || regs_seg < 0) return -EIO;   // kernel missing from the code object
+        r.code_key = polar_host::code_key(*p);
+    }
+    r.regs = (uint32_t)regs;
+    r.regs_seg = (uint32_t)regs_seg;
+    if (p->pair) {
+        const polar_host::PairShape sh = polar_host::pair_shape(*p, (long)batch, simds, regs, regs_seg);
+        r.waves_per_block = (uint32_t)sh.W;
+        r.blocks = (uint64_t)sh.pairs;
+        r.lds_bytes = sh.lds;
+        r.lds_row0 = (uint32_t)sh.lds_row0;
+    } else if (p->jit) {
+        const int wpb = polar_host::MASK_WAVES_PER_BLOCK;
+        r.waves_per_block = polar_host::fit_waves(regs, wpb) == wpb ? (uint32_t)wpb : 0u;
+        r.blocks = ((batch + 7) / 8 + wpb - 1) / wpb;
+    } else {
+        int wpg = waves_per_group(p, batch, simds);
+        if (p->hybrid) wpg = polar_host::fit_waves(regs, wpg);
+        r.waves_per_block = (uint32_t)wpg;
+        r.blocks = (batch + 7) / 8;
+        r.lds_bytes = (uint32_t)p->lds_group_dwords * 4u;
+    }
+    *info = r;
     return 0;
 }
 

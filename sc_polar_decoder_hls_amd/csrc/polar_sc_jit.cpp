@@ -16,10 +16,12 @@
 #include <hip/hiprtc.h>
 
 #include <dlfcn.h>
+#include <elf.h>
 #include <sys/stat.h>
 #include <utime.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <cstdio>
@@ -34,7 +36,7 @@ namespace {
 // slower on the same box and removed: a persistent batch loop (78.9 vs 72.8 us), two batches
 // per wave in straight-line code (80.9 vs 73.6 us), 1 / 2 waves per block (74.2 / 74.7 vs
 // 73.7 us), re-splitting the root from LDS for the root G (77 vs 72 us) -- DESIGN.md 3.1.
-constexpr int MASK_WPB = 4;
+constexpr int MASK_WPB = polar_host::MASK_WAVES_PER_BLOCK;
 constexpr int MASK_MIN_WAVES = 4;
 }  // namespace
 
@@ -618,10 +620,9 @@ std::string cache_dir()
     return (slash == std::string::npos ? std::string(".") : so.substr(0, slash)) + "/rtc_cache";
 }
 
-std::string cache_path(const std::string &src)
+// the cache key: the source, the embedded headers it includes, the options, the hipRTC version
+uint64_t source_key(const std::string &src)
 {
-    const std::string dir = cache_dir();
-    if (dir.empty()) return "";
     uint64_t h = 1469598103934665603ull;
     h = fnv1a(h, src.data(), src.size());
     // the embedded headers the source includes (interp.h and pair.h include device.h only)
@@ -633,8 +634,28 @@ std::string cache_path(const std::string &src)
     hiprtcVersion(&ver_major, &ver_minor);
     h = fnv1a(h, (const char *)&ver_major, sizeof ver_major);
     h = fnv1a(h, (const char *)&ver_minor, sizeof ver_minor);
+    return h;
+}
+
+}  // namespace
+
+uint64_t code_key(const polar_sc_plan &p)
+{
+    if (!p.jit && !p.hybrid && !p.pair) return 0;
+    try {
+        return source_key(jit_source(p));
+    } catch (const std::exception &) {
+        return 0;
+    }
+}
+
+namespace {
+std::string cache_path(const std::string &src)
+{
+    const std::string dir = cache_dir();
+    if (dir.empty()) return "";
     char name[40];
-    std::snprintf(name, sizeof name, "/%016llx.co", (unsigned long long)h);
+    std::snprintf(name, sizeof name, "/%016llx.co", (unsigned long long)source_key(src));
     return dir + name;
 }
 
@@ -740,6 +761,64 @@ int jit_load_interp(const polar_sc_plan &p, DevState &st)
     return 0;
 }
 
+// Registers per lane of kernel `name` in a gfx950 code object, from its kernel descriptor
+// (symbol "<name>.kd", AMDHSA code object v5): compute_pgm_rsrc1 bits 0..5 hold
+// GRANULATED_WORKITEM_VGPR_COUNT, which on gfx90a and later counts the unified VGPR + AGPR
+// allocation in granules of 8. hipRTC can add AGPRs to a 256-VGPR call graph; the hardware
+// then rejects a dispatch whose waves do not fit (HSA_STATUS_ERROR_INVALID_ISA), so the launch
+// shape is checked against this before every launch. -1: no such kernel.
+int kernel_regs(const std::vector<char> &code, const char *name)
+{
+    if (code.size() < sizeof(Elf64_Ehdr) || std::memcmp(code.data(), ELFMAG, SELFMAG) != 0) return -1;
+    Elf64_Ehdr eh;
+    std::memcpy(&eh, code.data(), sizeof eh);
+    if (eh.e_ident[EI_CLASS] != ELFCLASS64 || eh.e_shentsize != sizeof(Elf64_Shdr) ||
+        eh.e_shoff + (uint64_t)eh.e_shnum * sizeof(Elf64_Shdr) > code.size())
+        return -1;
+    std::vector<Elf64_Shdr> sh(eh.e_shnum);
+    std::memcpy(sh.data(), code.data() + eh.e_shoff, sh.size() * sizeof(Elf64_Shdr));
+    const std::string want = std::string(name) + ".kd";
+    for (const Elf64_Shdr &s : sh) {
+        if (s.sh_type != SHT_SYMTAB || s.sh_link >= sh.size() || s.sh_entsize != sizeof(Elf64_Sym)) continue;
+        const Elf64_Shdr &strs = sh[s.sh_link];
+        if (s.sh_offset + s.sh_size > code.size() || strs.sh_offset + strs.sh_size > code.size()) continue;
+        for (uint64_t o = 0; o + sizeof(Elf64_Sym) <= s.sh_size; o += sizeof(Elf64_Sym)) {
+            Elf64_Sym sym;
+            std::memcpy(&sym, code.data() + s.sh_offset + o, sizeof sym);
+            if (sym.st_name >= strs.sh_size) continue;
+            const char *nm = code.data() + strs.sh_offset + sym.st_name;
+            if (std::strncmp(nm, want.c_str(), strs.sh_size - sym.st_name) != 0) continue;
+            if (sym.st_shndx >= sh.size()) return -1;
+            const Elf64_Shdr &sec = sh[sym.st_shndx];   // the descriptor's section (.rodata)
+            const uint64_t off = sec.sh_offset + (sym.st_value - sec.sh_addr);
+            if (sym.st_value < sec.sh_addr || off + 64 > code.size()) return -1;
+            uint32_t rsrc1;
+            std::memcpy(&rsrc1, code.data() + off + 48, 4);   // compute_pgm_rsrc1
+            return (int)((rsrc1 & 63u) + 1u) * 8;
+        }
+    }
+    return -1;
+}
+
+// registers of the plan's decode kernel and (pair plans with a grid tier) its segment kernel,
+// from the compiled code object (jit_compile first)
+void code_regs(const polar_sc_plan &p, int &regs, int &regs_seg)
+{
+    const char *main = p.pair ? "polar_sc_pair_kernel" : (p.hybrid ? "polar_sc_hybrid_kernel" : "polar_sc_mask_kernel");
+    regs = kernel_regs(p.jit_code, main);
+    regs_seg = p.pair && !p.pair_tier.steps.empty() ? kernel_regs(p.jit_code, "polar_sc_pair_seg_kernel") : 0;
+}
+
+// the largest waves-per-block count <= W (halving) whose waves fit the 512 registers per lane
+// of a SIMD (a block's waves are spread over the CU's 4 SIMDs); 0 when not even one wave fits
+int fit_waves(int regs, int W)
+{
+    if (regs <= 0) return W;   // (the hipcc-built interpreter: fixed launch bounds)
+    if (regs > SIMD_REGS) return 0;
+    while (W > 1 && ((W + 3) / 4) * regs > SIMD_REGS) W /= 2;
+    return W;
+}
+
 int jit_load(const polar_sc_plan &p, DevState &st)
 {
     if (st.fn) return 0;
@@ -748,6 +827,15 @@ int jit_load(const polar_sc_plan &p, DevState &st)
         std::fprintf(stderr, "polar_sc: hipRTC build failed (%d)%s%s\n", rc, p.jit_log.empty() ? "" : ":\n",
                      p.jit_log.c_str());
         return rc;
+    }
+    // register budget of the decode kernels (before anything is loaded on the device)
+    {
+        code_regs(p, st.regs, st.regs_seg);
+        if (st.regs > SIMD_REGS || st.regs_seg > SIMD_REGS) {
+            std::fprintf(stderr, "polar_sc: generated kernel needs %d registers per lane (> %d): not launchable\n",
+                         std::max(st.regs, st.regs_seg), SIMD_REGS);
+            return -ENOTSUP;
+        }
     }
     if (hipError_t e = hipModuleLoadData(&st.module, p.jit_code.data()); e != hipSuccess) {
         std::fprintf(stderr, "polar_sc: hipModuleLoadData: %s\n", hipGetErrorString(e));
@@ -779,6 +867,7 @@ int jit_launch(const polar_sc_plan &p, const DevState &st, const int8_t *llr, ui
                int out_stride, void *stream)
 {
     (void)p;
+    if (fit_waves(st.regs, MASK_WPB) != MASK_WPB) return -ENOTSUP;   // (123 registers at C2)
     const long waves = (batch + 7) / 8;   // one 8-frame batch per wave (run_mask)
     const unsigned blocks = (unsigned)((waves + MASK_WPB - 1) / MASK_WPB);
     int b = (int)batch;
@@ -848,24 +937,29 @@ int launch_tier(const polar_sc_plan &p, const DevState &st, const int8_t *llr, u
 }
 
 // Pair plans (polar_sc_pair.h): one block of W waves per frame pair. W grows while the pairs
-// cannot give every SIMD two waves (C3's 2048 pairs: 1; C5's 256 or 32: 8). The stage slots of
-// the smallest levels go to LDS while they fit the share of a CU's 160 KB that one resident
-// pair gets (all-HBM otherwise); with a grid tier they stay below the tier's cut.
-int jit_launch_pair(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
-                    int out_stride, void *stream)
+// cannot give every SIMD two waves (C3's 2048 pairs: 1; C5's 256 or 32: 8), then is capped so
+// that the block's waves fit the register file (kernel_regs). The stage slots of the smallest
+// levels go to LDS while they fit the share of a CU's 160 KB that one resident pair gets
+// (all-HBM otherwise); with a grid tier they stay below the tier's cut.
+PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, int regs_seg)
 {
-    const long pairs = (batch + 1) / 2;
-    const long cus = st.simds > 0 ? st.simds / 4 : 256;
+    PairShape sh;
+    sh.pairs = (batch + 1) / 2;
+    const long cus = simds > 0 ? simds / 4 : 256;
     int W = p.tune.waves_per_group;
     if (W == 0) {
         W = 1;
-        while (W < PAIR_WAVES_MAX && pairs * W < 2 * (st.simds > 0 ? st.simds : 1024)) W *= 2;
+        while (W < PAIR_WAVES_MAX && sh.pairs * W < 2 * (simds > 0 ? simds : 1024)) W *= 2;
     }
     if (W > PAIR_WAVES_MAX) W = PAIR_WAVES_MAX;
     const bool tier = !p.pair_tier.steps.empty();
+    W = fit_waves(regs, W);
+    if (tier) W = std::min(W, fit_waves(regs_seg, W));
+    sh.W = W;
+    if (W == 0) return sh;
+    const long per_cu = (sh.pairs + cus - 1) / cus;
     // LDS: levels of nodes S .. L words (32 (2 L - S) bytes) + the SPC exchange (3 W rows of 256 B)
-    const long per_cu = (pairs + cus - 1) / cus;
-    const long budget = 160l * 1024l / (per_cu > 0 ? per_cu : 1) - 3l * W * 256l;
+    const long budget = CU_LDS_BYTES / (per_cu > 0 ? per_cu : 1) - 3l * W * 256l;
     const int S = p.sub_words, G = (int)p.G;
     int L = 0;
     for (int w = S; w <= G / 2; w *= 2) {
@@ -873,15 +967,25 @@ int jit_launch_pair(const polar_sc_plan &p, const DevState &st, const int8_t *ll
         if (32l * (2l * w - S) <= budget) L = w;
     }
     const int lds_rows = L ? (2 * L - S) / 4 : 0;
-    int lds_row0 = p.pair_slot_rows - lds_rows;
-    const unsigned lds = (unsigned)(lds_rows * 128 + 3 * W * 256);
-    int N = (int)p.N, b = (int)batch, pd = p.pair_dwords, sr = p.pair_slot_rows;
+    sh.lds_row0 = p.pair_slot_rows - lds_rows;
+    sh.lds = (unsigned)(lds_rows * 128 + 3 * W * 256);
+    return sh;
+}
+
+int jit_launch_pair(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
+                    int out_stride, void *stream)
+{
+    const PairShape sh = pair_shape(p, batch, st.simds, st.regs, st.regs_seg);
+    if (sh.W == 0) return -ENOTSUP;
+    const bool tier = !p.pair_tier.steps.empty();
+    int N = (int)p.N, b = (int)batch, pd = p.pair_dwords, sr = p.pair_slot_rows, lds_row0 = sh.lds_row0;
+    const long pairs = sh.pairs;
     void *scratch = st.scratch;
     auto segment = [&](hipFunction_t fn, int seg) {
         void *args[] = {(void *)&llr, (void *)&out, (void *)&scratch, (void *)&N, (void *)&b, (void *)&out_stride,
                         (void *)&pd, (void *)&sr, (void *)&lds_row0, (void *)&seg};
-        return hipModuleLaunchKernel(fn, (unsigned)pairs, 1, 1, (unsigned)(64 * W), 1, 1, lds, (hipStream_t)stream,
-                                     args, nullptr);
+        return hipModuleLaunchKernel(fn, (unsigned)pairs, 1, 1, (unsigned)(64 * sh.W), 1, 1, sh.lds,
+                                     (hipStream_t)stream, args, nullptr);
     };
     if (!tier) return segment(st.fn, 0) == hipSuccess ? 0 : -EIO;
     int cw = TIER_CW;
@@ -906,6 +1010,8 @@ int jit_launch_pair(const polar_sc_plan &p, const DevState &st, const int8_t *ll
 int jit_launch_hybrid(const polar_sc_plan &p, const DevState &st, const int8_t *llr, uint16_t *out, long batch,
                       int out_stride, int wpg, void *stream, unsigned long long *trace)
 {
+    wpg = fit_waves(st.regs, wpg);   // the block's waves must fit the register file
+    if (wpg == 0) return -ENOTSUP;
     if (!trace && !p.tiers.empty()) return launch_tier(p, st, llr, out, batch, out_stride, wpg, stream);
     return launch_interp_fn(trace ? st.fn_trace : st.fn, p, st, llr, out, batch, out_stride, wpg, stream, trace);
 }

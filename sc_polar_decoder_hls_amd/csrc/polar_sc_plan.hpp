@@ -31,6 +31,10 @@ struct DevState {
     hipFunction_t fn16 = nullptr;
     void *ops16 = nullptr;              //   and its schedule when it differs from `ops`
     int simds = 0;                // SIMDs of the device (4 per CU), for launch sizing
+    // registers per lane (VGPR + AGPR allocation, kernel descriptor) of the generated decode
+    // kernel and of the pair segment kernel: the launch shape is capped so that a block's
+    // waves fit (kernel_regs, fit_waves); 0 = not a generated kernel
+    int regs = 0, regs_seg = 0;
 };
 
 enum JitMode { JIT_OFF = 0, JIT_AUTO = 1 };
@@ -65,7 +69,7 @@ struct TierPlan {
 constexpr uint32_t FB_EXACT = 1u << 19;
 
 // hybrid kernels: by default at most 8 waves per 8-frame group (one 512-thread block, the
-// kernel's launch bound); POLAR_SC_HYBRID_WAVES (4 or 8) at plan creation changes it.
+// kernel's launch bound); polar_sc_tuning.hybrid_waves (4 or 8) changes it.
 // Measured (tools/wpg_sweep.py): C5 (512 frames) 6.50 -> 5.99 ms from 4 to 8 waves, C3
 // (4096 frames, which keeps 4 waves per group) unchanged; 16 waves (1024-thread blocks with
 // spilled subtree code) failed to launch (HSA_STATUS_ERROR_INVALID_ISA).
@@ -75,6 +79,18 @@ constexpr int HYBRID_MAX_WAVES = 8;
 // <= 256 VGPRs per wave), subtrees of at most PAIR_SUB_WORDS words in registers
 constexpr int PAIR_WAVES_MAX = 8;
 constexpr int PAIR_SUB_WORDS = 256;
+// unified register file per SIMD lane (VGPRs + AGPRs) shared by the waves on the SIMD
+constexpr int SIMD_REGS = 512;
+// one CU's LDS (gfx950)
+constexpr long CU_LDS_BYTES = 160l * 1024l;
+
+// launch shape of a pair plan for one batch (jit_launch_pair, polar_sc_plan_launch_info)
+struct PairShape {
+    int W = 0;            // waves per frame pair (0: the kernel does not fit, -ENOTSUP)
+    long pairs = 0;       // blocks
+    int lds_row0 = 0;     // first stage-slot row held in LDS
+    unsigned lds = 0;     // dynamic LDS bytes per block
+};
 
 // grid tier of a pair plan: `seg_ops` is the upper schedule with POLAR_OP_SEGEND where the grid
 // launches of `steps` (grid records) run; steps alternate with the segment kernel's cases
@@ -158,4 +174,10 @@ int launch_interp_fn(hipFunction_t fn, const polar_sc_plan &p, const DevState &s
                      long batch, int out_stride, int wpg, void *stream, unsigned long long *trace,
                      const void *ops = nullptr);   // schedule: nullptr = st.ops
 bool jit_supported(uint32_t N);
+int kernel_regs(const std::vector<char> &code, const char *name);   // -1: no such kernel
+int fit_waves(int regs, int W);
+void code_regs(const polar_sc_plan &p, int &regs, int &regs_seg);
+constexpr int MASK_WAVES_PER_BLOCK = 4;   // per-mask kernel launch (polar_sc_jit.cpp MASK_WPB)
+PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, int regs_seg);
+uint64_t code_key(const polar_sc_plan &p);   // rtc cache key of the plan's generated source (0: none)
 }  // namespace polar_host

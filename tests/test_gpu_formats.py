@@ -9,19 +9,11 @@ import numpy as np
 import pytest
 
 import util
+from sc_polar_decoder_hls_amd._plansets import FORMATS   # (par, sigmag, extended, llr_bits); build() prewarms them
 from test_gpu_parity import _assert_same
 
 pytestmark = pytest.mark.gpu
 
-# (par, sigmag, extended, llr_bits)
-FORMATS = [
-    (16, 0, 1, 6), (16, 0, 1, 8), (16, 0, 0, 6), (16, 1, 0, 6), (16, 1, 1, 9), (16, 0, 1, 9),
-    (32, 1, 1, 6), (32, 0, 1, 6), (64, 1, 1, 6), (64, 1, 1, 8), (64, 0, 1, 6), (64, 1, 0, 6), (64, 0, 0, 8),
-    (64, 1, 1, 9),
-    # PAR 4 / 8 (script_RTL_sim.sh:97-330): PAR words as lane groups of a device word
-    (8, 1, 1, 6), (8, 0, 1, 6), (8, 1, 0, 8), (8, 1, 1, 8), (4, 1, 1, 6), (4, 0, 0, 8), (4, 1, 1, 8),
-    (4, 1, 1, 9),
-]
 CONFIGS = ((2, 1, 1, 1, 0, 0, 1), (1, 1, 1, 1, 1, 1, 0), (0, 0, 0, 0, 0, 0, 0), (2, 1, 1, 1, 1, 1, 0))
 
 

@@ -7,8 +7,6 @@ GPU tests: bit-exact against the oracle (literal my_module FSM) on reference mas
 structured masks that put R0 / R1 / REP / SPC nodes at every size (the cross-row steps of the
 nodes of 1, 2 and 4 words), for every waves-per-pair count, subtree size, LDS / HBM slot
 placement and with the grid tier."""
-import functools
-
 import numpy as np
 import pytest
 
@@ -20,77 +18,9 @@ def pair(pkg, mask, **tuning):
     return pkg.Decoder(mask, tuning=dict(tuning, kernel=3))
 
 
-def structured_mask(rng, N, p_special=0.7):
-    """Nodes of random size whose frozen pattern is R0 / R1 / REP / SPC (or random), so that the
-    pruned node ops appear at every level (1 .. N/64 words)."""
-    m = (rng.random(N) < 0.5).astype(np.uint8)
-    pos = 0
-    while pos < N:
-        size = 16 << int(rng.integers(0, 6))
-        size = min(size, N - pos)
-        if rng.random() < p_special:
-            kind = int(rng.integers(0, 4))
-            blk = np.zeros(size, np.uint8)
-            if kind == 1:
-                blk[:] = 1                  # R1
-            elif kind == 2:
-                blk[-1] = 1                 # REP
-            elif kind == 3:
-                blk[:] = 1
-                blk[0] = 0                  # SPC
-            m[pos:pos + size] = blk
-        pos += size
-    return m
-
-
-@functools.lru_cache(maxsize=None)
-def struct_masks(N):
-    rng = np.random.default_rng(N)
-    return tuple(structured_mask(rng, N) for _ in range(3))
-
-
-@functools.lru_cache(maxsize=None)
-def wave_mask():
-    return structured_mask(np.random.default_rng(4242), 16384, 0.9)
-
-
-PARITY_MASKS = [("frozen_n_2048_k_1024", 23), ("FB_N2048_K1024", 8), ("frozen_n_4096_k_2048", 17),
-                ("frozen_n_8192_k_4096", 9), ("frozen_n_16384_k_8192", 7), ("frozen_n_32768_k_29492", 5),
-                ("frozen_n_2048_k_1844", 12), ("frozen_n_16384_k_14746", 6), ("frozen_n_65536_k_32768", 5)]
-STRUCT_SUB_WORDS = (32, 64, 256)
-
-
-def struct_sub_words(N):
-    return [sw for sw in STRUCT_SUB_WORDS if sw <= N // 32]   # subtrees of at most half the code
-
-
-def gpu_plans():
-    """(name, mask, tuning) of every plan the GPU tests below decode with: their hipRTC code
-    objects are compiled ahead by __graft_entry__.build() (the GPU box loads them from the
-    in-tree cache instead of compiling)."""
-    out = [(n, util.mask(n), {"kernel": 3}) for n, _ in PARITY_MASKS]
-    for N in (2048, 8192, 32768):
-        for i, m in enumerate(struct_masks(N)):
-            out += [("struct%d_%d" % (N, i), m, {"kernel": 3, "sub_words": sw}) for sw in struct_sub_words(N)]
-    out += [("frozen_n_2048_k_1024", util.mask("frozen_n_2048_k_1024"), {"kernel": 3, "sub_words": sw})
-            for sw in (32, 64)]
-    out += [("frozen_n_8192_k_4096", util.mask("frozen_n_8192_k_4096"), {"kernel": 3, "sub_words": 256}),
-            ("frozen_n_16384_k_8192", util.mask("frozen_n_16384_k_8192"), {"kernel": 3, "sub_words": 64}),
-            ("wave_mask", wave_mask(), {"kernel": 3, "sub_words": 64}),
-            ("frozen_n_32768_k_29492", util.mask("frozen_n_32768_k_29492"),
-             {"kernel": 3, "tier_words": 512, "sub_words": 128}),
-            ("frozen_n_262144_k_131072", util.mask("frozen_n_262144_k_131072"), {"kernel": 3}),
-            ("frozen_n_262144_k_131072", util.mask("frozen_n_262144_k_131072"), {"kernel": 3, "tier_words": 1024})]
-    return out
-
-
-def gpu_par64_plans():
-    """(name, mask, config fields, tuning) of the PAR 64 GPU tests (prewarmed by build())."""
-    out = [(n, util.mask(n), {"par": 64}, {"kernel": 3}) for n, _ in PAR64_MASKS]
-    for N in (8192, 32768):
-        for i, m in enumerate(struct_masks(N)[:2]):
-            out += [("struct%d_%d" % (N, i), m, {"par": 64}, {"kernel": 3, "sub_words": sw}) for sw in (64, 256)]
-    return out
+# the plan lists live in the package's build tooling (build() compiles them ahead)
+from sc_polar_decoder_hls_amd._plansets import (PAR64_MASKS, PARITY_MASKS, gpu_par64_plans, gpu_plans,  # noqa: F401
+                                                struct_masks, struct_sub_words, structured_mask, wave_mask)
 
 
 def run(pkg, torch, dec, llr):
@@ -244,28 +174,45 @@ def test_pair_misaligned_channel(pkg, cuda, oracle_mod, name):
     _assert_same(pkg.unpack_bits(out.cpu().numpy(), mask.size), oracle_mod.decode_fsm(mask, llr), "misaligned " + name)
 
 
-def test_pair_register_budget(pkg, tmp_path, monkeypatch):
-    """hipRTC code objects of the largest pair plans fit the registers of a 512-thread launch
-    (VGPRs + AGPRs <= 256 per lane at two waves per SIMD): a generated call graph that needs
-    more is spilled into AGPRs by hipRTC and the dispatch is rejected on the device
-    (HSA_STATUS_ERROR_INVALID_ISA)."""
+def test_pair_register_budget(pkg):
+    """The launch guard (polar_sc_jit.cpp kernel_regs / fit_waves, polar_sc_plan_launch_info):
+    the registers of a generated kernel come from its kernel descriptor (granulated VGPR +
+    AGPR count, equal to the ELF metadata's unified .vgpr_count rounded to 8), and a launch
+    never puts more waves of a block on a SIMD than its 512 registers per lane hold. Checked on
+    C5 and on the chain_max = 4 plans of the structured N = 32768 mask -- the configuration of
+    the round-3 dispatch abort -- which hipRTC compiles to exactly 256 registers (the
+    512-thread launch bound), so the full 8-wave block still fits."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import check_rtc_registers as cr
-    monkeypatch.setenv("POLAR_SC_RTC_CACHE", str(tmp_path))
-    for m, tun in ((util.mask("frozen_n_262144_k_131072"), {}), (struct_masks(32768)[0], {"sub_words": 64})):
-        assert pair(pkg, m, **tun).compile()
-    cos = list(tmp_path.glob("*.co"))
-    assert len(cos) == 2
-    for co in cos:
-        for name, vgpr, agpr, wg in cr.kernels(str(co)):
-            over, total = cr.over_budget(vgpr, agpr, wg)
-            assert not over, "%s: %s vgpr %d agpr %d for %d threads" % (co.name, name, vgpr, agpr, wg)
+    cache = os.path.join(os.path.dirname(pkg._build.LIB), "rtc_cache")
+    plans = [(util.mask("frozen_n_262144_k_131072"), {}), (struct_masks(32768)[0], {"sub_words": 64, "chain_max": 4}),
+             (struct_masks(32768)[0], {"sub_words": 256, "chain_max": 4})]
+    for m, tun in plans:
+        dec = pair(pkg, m, **tun)
+        for batch in (9, 64, 4096, 40001):
+            info = dec.launch_info(batch)
+            W, regs = info["waves_per_block"], info["regs"]
+            assert 0 < regs <= 512 and W >= 1, info
+            assert -(-W // 4) * regs <= 512, info
+        meta = {name: (vgpr, wg) for name, vgpr, _, wg in cr.kernels(os.path.join(cache, info["code_key"] + ".co"))}
+        vgpr, wg = meta["polar_sc_pair_kernel"]
+        assert regs == -(-vgpr // 8) * 8, (regs, vgpr)
+        assert not cr.over_budget(vgpr, 0, wg)[0]
+    # an automatic 8-wave launch (small batch) of the chain_max = 4 kernel: 2 waves of 256
+    # registers per SIMD
+    info = pair(pkg, struct_masks(32768)[0], sub_words=64, chain_max=4).launch_info(9)
+    assert (info["regs"], info["waves_per_block"]) == (256, 8), info
 
 
-PAR64_MASKS = [("frozen_n_2048_k_1024", 9), ("frozen_n_16384_k_8192", 5), ("frozen_n_16384_k_14746", 5),
-               ("frozen_n_65536_k_32768", 3)]
+def test_forced_kernel_errors(pkg):
+    """A forced kernel / subtree size the plan cannot use is an error, not a silent fallback."""
+    with pytest.raises(pkg.PolarError):
+        pkg.Decoder(util.mask("FB_N1024_K512"), tuning={"kernel": 3})     # N < 2048: no pair kernel
+    with pytest.raises(pkg.PolarError):
+        pkg.Decoder(util.mask("frozen_n_8192_k_4096"), tuning={"kernel": 2, "sub_words": 256})   # hybrid <= 128
+    assert pkg.Decoder(util.mask("frozen_n_8192_k_4096"), tuning={"kernel": 2, "sub_words": 128}).stats["kernel"] == 2
 
 
 def par64_config(pkg, q=6):

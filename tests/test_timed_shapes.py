@@ -1,0 +1,73 @@
+"""The launch shapes bench.py times, decoded whole.
+
+The pair kernel's launch depends on the batch: waves per frame pair W, which stage-slot levels
+sit in LDS and whether F-descent chains run (W = 1 only). The other GPU tests decode a few
+frames, i.e. W = 8 with several LDS levels; these decode the full timed batches through the
+default plan -- C3: 4096 frames of frozen_n_65536_k_32768 (W = 1, 8 pairs per CU, only the
+subtree-root level in LDS, chains of 3); C5: 512 and 64 frames of frozen_n_262144_k_131072
+(W = 8) -- and check every frame: a noiseless round trip (random information bits, LLR
+magnitudes 1..31 with the codeword's signs: SC recovers x exactly) on all frames but 8, and
+equality with the oracle's literal FSM on 8 AWGN frames placed across the same launch (first,
+middle and last pairs, both halves)."""
+import numpy as np
+import pytest
+
+import util
+from test_gpu_parity import _assert_same
+
+# (mask, frames per GPU, waves per frame pair of the launch)
+SHAPES = [("frozen_n_65536_k_32768", 4096, 1), ("frozen_n_262144_k_131072", 512, 8),
+          ("frozen_n_262144_k_131072", 64, 8)]
+
+
+def noiseless_batch(torch, mask, batch, seed):
+    """[batch, N] int8 LLRs on the GPU: x = u F^{(x)n} for random information bits u, LLR sign
+    from x (bit 1 -> negative), magnitude uniform in 1..31; and x as [batch, N] uint8."""
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    N = mask.size
+    m = torch.from_numpy(mask.astype(np.uint8)).cuda()
+    x = torch.randint(0, 2, (batch, N), generator=g, device="cuda", dtype=torch.uint8) & m
+    h = 1
+    while h < N:
+        v = x.view(batch, N // (2 * h), 2, h)
+        v[:, :, 0, :] ^= v[:, :, 1, :]
+        h *= 2
+    mag = torch.randint(1, 32, (batch, N), generator=g, device="cuda", dtype=torch.int16)
+    llr = torch.where(x.bool(), -mag, mag).to(torch.int8)
+    return llr, x
+
+
+def awgn_rows(batch):
+    """8 frame indices spread over the launch: the first, middle and last pairs (both frames)
+    plus one odd-pair high frame."""
+    mid = (batch // 4) * 2
+    return np.array(sorted({0, 1, mid, mid + 1, batch - 2, batch - 1, 5, batch // 3 * 2 + 1}))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,batch,W", SHAPES)
+def test_timed_shape_full_batch(pkg, cuda, oracle_mod, name, batch, W):
+    torch = cuda
+    mask = util.mask(name)
+    N = mask.size
+    dec = pkg.Decoder(mask)
+    info = dec.launch_info(batch)
+    # the shape bench.py times: one block per pair, W waves per pair
+    assert (info["kernel"], info["waves_per_block"], info["blocks"]) == (3, W, batch // 2), info
+    if W == 1:
+        # C3: only the subtree-root level in LDS, F-descent chains in the generated kernel
+        S = dec.stats["sub_words"]
+        assert info["lds_bytes"] == S // 4 * 128 + 3 * 256, info
+        assert "pop_chain<3" in dec.kernel_source()
+    llr, x = noiseless_batch(torch, mask, batch, seed=batch)
+    rows = awgn_rows(batch)
+    noisy, _ = util.synth_frames(mask, rows.size, ebn0_db=1.0, seed=batch + 7)
+    llr[torch.from_numpy(rows).cuda()] = torch.from_numpy(noisy).cuda()
+    out = dec.decode(llr)
+    torch.cuda.synchronize()
+    got = pkg.unpack_bits(out.cpu().numpy(), N)
+    keep = np.ones(batch, bool)
+    keep[rows] = False
+    _assert_same(got[keep], x.cpu().numpy()[keep], "%s x %d: noiseless round trip" % (name, batch))
+    _assert_same(got[rows], oracle_mod.decode_fsm(mask, noisy), "%s x %d: AWGN frames vs oracle" % (name, batch))

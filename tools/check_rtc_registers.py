@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Register budget of every hipRTC code object in lib/rtc_cache (CPU only).
 
-A kernel whose VGPRs + AGPRs exceed what its launch bound allows (512 unified registers per
-SIMD lane, shared by the waves of a workgroup that land on one SIMD) is rejected at dispatch
-(HSA_STATUS_ERROR_INVALID_ISA): hipRTC can add AGPRs to a 256-VGPR call graph. This lists
-every kernel with its counts and exits 1 when one is over budget.
+A kernel whose registers (VGPRs + AGPRs, unified) exceed what its launch bound allows (512
+registers per SIMD lane, shared by the waves of a workgroup that land on one SIMD) cannot be
+dispatched at that block size. This lists every kernel with its counts and exits 1 when one
+is over budget at its launch bound (the library itself caps the waves per block at launch,
+polar_sc_jit.cpp fit_waves).
 
 usage: python tools/check_rtc_registers.py [cache dir]
 """
@@ -32,9 +33,13 @@ def kernels(path):
 
 
 def over_budget(vgpr, agpr, wg):
-    # unified register file of 512 per lane and SIMD; VGPRs are padded to 4 before the AGPRs
-    waves_per_simd = max(1, -(-wg // 64) // 4)
-    total = (-(-vgpr // 4) * 4 if agpr else vgpr) + agpr
+    # unified register file of 512 per lane and SIMD. On gfx90a and later the metadata's
+    # .vgpr_count is already the unified total (architected VGPRs padded to 4, then the
+    # AGPRs: LLVM's getTotalNumVGPRs); .agpr_count is the AGPR part of it. The kernel
+    # descriptor's granulated count (polar_sc_jit.cpp kernel_regs) rounds it up to 8.
+    waves = -(-wg // 64)
+    waves_per_simd = max(1, -(-waves // 4))
+    total = -(-vgpr // 8) * 8
     return total * waves_per_simd > 512, total
 
 

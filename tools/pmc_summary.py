@@ -41,6 +41,16 @@ def load_trace(d, kre):
     return durs
 
 
+def load_launch_info(d):
+    """The 'launch_info {...}' line tools/prof_decode.py prints (any pass's log), or None."""
+    for f in sorted(glob.glob(os.path.join(d, "*.log"))):
+        with open(f, errors="replace") as fh:
+            for line in fh:
+                if line.startswith("launch_info "):
+                    return json.loads(line[len("launch_info "):])
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -58,6 +68,11 @@ def main():
     else:
         d = durs[a.skip_first:] if len(durs) > a.skip_first else durs
     res = {"kernel_regex": a.kernel, "dispatches": len(durs), "counters": c}
+    info = load_launch_info(a.dir)
+    if info:
+        # the profiled plan's launch shape and code-object key (tools/prof_decode.py)
+        res["launch_info"] = info
+        res["code_key"] = info["code_key"]
     if a.reps > 0:
         res["per_decode_of_reps"] = a.reps
     if d:

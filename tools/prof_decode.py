@@ -2,6 +2,7 @@
 """Decode-only driver for rocprofv3 runs: generates frames once, then launches the decode
 kernel `--reps` times (no other kernels in the loop)."""
 import argparse
+import json
 import os
 import sys
 
@@ -29,6 +30,10 @@ def main():
     tun = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, a.tuning.split(",")))}
     dec = pkg.Decoder(mask, tuning=tun or None)
     dec.prepare(a.batch)
+    # the launch shape and code object being profiled (tools/pmc_summary.py copies it into the
+    # summary; bench.py uses a profile's traffic only for the code object it times)
+    print("launch_info " + json.dumps(dict(dec.launch_info(a.batch), mask=a.mask, batch=a.batch, tuning=tun)),
+          flush=True)
     nb = a.rotate if a.rotate > 0 else max(1, min(8, -(-bench.ROTATE_BYTES // (a.batch * mask.size))))
     llrs = [bench.gen_frames_torch(torch, mask, a.batch, a.ebn0, 0xF0 + b, dev)[0] for b in range(nb)]
     out = torch.empty((a.batch, dec.words), dtype=torch.int64, device=dev)

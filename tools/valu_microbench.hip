@@ -35,12 +35,26 @@ __device__ __forceinline__ void op(unsigned &r, unsigned k)
     if constexpr (OP == 12) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
     if constexpr (OP == 13) asm volatile("v_xor_b32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
     if constexpr (OP == 14) asm volatile("v_min3_u32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+    // encoding-size probes: the same simple op as VOP2 (4 B), VOP2 + literal (8 B), VOP2 with an
+    // SGPR operand (4 B) and the VOP3 form (8 B); a 4 B / 8 B alternation
+    if constexpr (OP == 15) asm volatile("v_and_b32_e32 %0, 0x7fff7fff, %0" : "+v"(r));
+    if constexpr (OP == 16) asm volatile("v_and_b32_e32 %0, %1, %0" : "+v"(r) : "s"(k));
+    if constexpr (OP == 17) asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 18) asm volatile("v_pk_add_u16 %0, %1, %0" : "+v"(r) : "s"(k));
+    if constexpr (OP == 19) asm volatile("v_add_u32 %0, %0, %1\n\tv_pk_add_u16 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 20) asm volatile("v_lshlrev_b32_e32 %0, 3, %0" : "+v"(r));
+    if constexpr (OP == 21) asm volatile("v_bfi_b32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 22) asm volatile("v_add_u32 %0, %0, %1\n\tv_xor_b32 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 23) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(r) : "v"(k));
 }
 static const char *names[] = {"v_add_u32", "v_xor_b32", "v_pk_add_u16", "v_pk_min_u16", "v_bitop3_b32",
                               "v_mov_b32_dpp row_ror", "v_add_u32_dpp row_ror", "v_and_or_b32",
                               "v_pk_ashrrev_i16", "v_add_f32", "v_fma_f32", "v_pk_mad_u16", "v_perm_b32",
-                              "v_xor_b32_dpp quad_perm", "v_min3_u32"};
-constexpr int NOPS = 15;
+                              "v_xor_b32_dpp quad_perm", "v_min3_u32", "v_and_b32_e32 literal (8 B)",
+                              "v_and_b32_e32 sgpr (4 B)", "v_add_u32_e64 (VOP3, 8 B)", "v_pk_add_u16 sgpr",
+                              "v_add_u32 + v_pk_add_u16 (pair)", "v_lshlrev_b32_e32 inline const",
+                              "v_bfi_b32", "v_add_u32 + v_xor_b32 (pair)", "v_cndmask_b32_e32 vcc"};
+constexpr int NOPS = 24;
 
 // CHAINS independent accumulators per wave; stamps[wave] = {memtime delta, memrealtime delta}
 template <int OP, int CHAINS>
@@ -98,15 +112,18 @@ void one(unsigned *buf, unsigned long long *st, int cus, int wps)
 }
 
 template <int OP>
-void all(unsigned *buf, unsigned long long *st, int cus)
+void all(unsigned *buf, unsigned long long *st, int cus, int from)
 {
-    for (int wps : {1, 2, 4, 8}) one<OP, 8>(buf, st, cus, wps);
-    one<OP, 1>(buf, st, cus, 1);
-    if constexpr (OP + 1 < NOPS) all<OP + 1>(buf, st, cus);
+    if (OP >= from)
+        for (int wps : {1, 2, 4, 8}) one<OP, 8>(buf, st, cus, wps);
+    if (OP >= from) one<OP, 1>(buf, st, cus, 1);
+    if constexpr (OP + 1 < NOPS) all<OP + 1>(buf, st, cus, from);
 }
 
-int main()
+// usage: valu_mb [first op index]   (the encoding-size probes start at 15)
+int main(int argc, char **argv)
 {
+    const int from = argc > 1 ? std::atoi(argv[1]) : 0;
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, 0);
     const int cus = prop.multiProcessorCount;
@@ -114,7 +131,7 @@ int main()
     unsigned long long *st;
     hipMalloc(&buf, (size_t)cus * 8 * 256 * 4);
     hipMalloc(&st, (size_t)cus * 8 * 4 * 2 * 8);
-    all<0>(buf, st, cus);
+    all<0>(buf, st, cus, from);
     hipFree(buf);
     hipFree(st);
     return 0;
