@@ -46,6 +46,28 @@ __device__ __forceinline__ void op(unsigned &r, unsigned k)
     if constexpr (OP == 21) asm volatile("v_bfi_b32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
     if constexpr (OP == 22) asm volatile("v_add_u32 %0, %0, %1\n\tv_xor_b32 %0, %0, %1" : "+v"(r) : "v"(k));
     if constexpr (OP == 23) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(r) : "v"(k));
+    // which operand forms dual-issue (round 4): shift amount / constant in a VGPR vs inline,
+    // VOP1, 16-bit VOP2, 3-source VOP3, SGPR masks, permlane
+    if constexpr (OP == 24) asm volatile("v_lshlrev_b32_e32 %0, %1, %0" : "+v"(r) : "v"(k));
+    if constexpr (OP == 25) asm volatile("v_and_b32_e32 %0, %1, %0" : "+v"(r) : "v"(k));
+    if constexpr (OP == 26) asm volatile("v_or3_b32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 27) asm volatile("v_sub_u32_e32 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 28) asm volatile("v_lshrrev_b32_e32 %0, 16, %0" : "+v"(r));
+    if constexpr (OP == 29) asm volatile("v_not_b32_e32 %0, %0" : "+v"(r));
+    if constexpr (OP == 30) asm volatile("v_min_u32_e32 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 31) asm volatile("v_min_u16_e32 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 32) asm volatile("v_add_u16_e32 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 33) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[4:5]" : "+v"(r) : "v"(k));
+    if constexpr (OP == 34) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 35) asm volatile("v_and_b32_e32 %0, 15, %0" : "+v"(r));
+    if constexpr (OP == 36) asm volatile("v_xor_b32_e32 %0, 0x80008000, %0" : "+v"(r));
+    if constexpr (OP == 37) asm volatile("v_add_u32_e32 %0, 5, %0" : "+v"(r));
+    if constexpr (OP == 38) asm volatile("v_permlane16_swap_b32 %0, %0" : "+v"(r));
+    if constexpr (OP == 39) asm volatile("v_mov_b32_e32 %0, %1" : "=v"(r) : "v"(k));
+    if constexpr (OP == 40) asm volatile("v_ashrrev_i32_e32 %0, %1, %0" : "+v"(r) : "v"(k));
+    if constexpr (OP == 41) asm volatile("v_pk_sub_u16 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 42) asm volatile("v_sub_u32_e64 %0, %0, %1" : "+v"(r) : "v"(k));
+    if constexpr (OP == 43) asm volatile("v_max_i16_e32 %0, %0, %1" : "+v"(r) : "v"(k));
 }
 static const char *names[] = {"v_add_u32", "v_xor_b32", "v_pk_add_u16", "v_pk_min_u16", "v_bitop3_b32",
                               "v_mov_b32_dpp row_ror", "v_add_u32_dpp row_ror", "v_and_or_b32",
@@ -53,8 +75,14 @@ static const char *names[] = {"v_add_u32", "v_xor_b32", "v_pk_add_u16", "v_pk_mi
                               "v_xor_b32_dpp quad_perm", "v_min3_u32", "v_and_b32_e32 literal (8 B)",
                               "v_and_b32_e32 sgpr (4 B)", "v_add_u32_e64 (VOP3, 8 B)", "v_pk_add_u16 sgpr",
                               "v_add_u32 + v_pk_add_u16 (pair)", "v_lshlrev_b32_e32 inline const",
-                              "v_bfi_b32", "v_add_u32 + v_xor_b32 (pair)", "v_cndmask_b32_e32 vcc"};
-constexpr int NOPS = 24;
+                              "v_bfi_b32", "v_add_u32 + v_xor_b32 (pair)", "v_cndmask_b32_e32 vcc",
+                              "v_lshlrev_b32_e32 vgpr shift", "v_and_b32_e32 vgpr", "v_or3_b32",
+                              "v_sub_u32_e32 vgpr", "v_lshrrev_b32_e32 inline 16", "v_not_b32 (VOP1)",
+                              "v_min_u32_e32", "v_min_u16_e32", "v_add_u16_e32", "v_cndmask_b32_e64 sgpr mask",
+                              "v_lshl_or_b32", "v_and_b32_e32 inline 15", "v_xor_b32_e32 literal",
+                              "v_add_u32_e32 inline 5", "v_permlane16_swap_b32", "v_mov_b32_e32 vgpr",
+                              "v_ashrrev_i32_e32 vgpr", "v_pk_sub_u16", "v_sub_u32_e64 (VOP3)", "v_max_i16_e32"};
+constexpr int NOPS = 44;
 
 // CHAINS independent accumulators per wave; stamps[wave] = {memtime delta, memrealtime delta}
 template <int OP, int CHAINS>
