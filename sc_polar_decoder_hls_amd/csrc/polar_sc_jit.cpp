@@ -94,6 +94,13 @@ struct Gen {
               << pos / 16 << "]);\n";
         }
     }
+    // the same from a full mask per half (0xFFFF / 0: every bit of a half equal, as the leaf
+    // and REP decisions are): the bits land in place without a shift or an AND
+    void put_mask(int pos, int n, const std::string &m)
+    {
+        if (n >= 16) o << "    bw[" << pos / 16 << "] = " << m << ";\n";
+        else o << "    bw[" << pos / 16 << "] = bsel(" << hexmask(pos, n) << ", " << m << ", bw[" << pos / 16 << "]);\n";
+    }
     // G-type ops: loop over n words with partial sums from upos (or zero)
     void ucache(int upos, int i)
     {
@@ -301,7 +308,7 @@ struct Gen {
                   << "    const u32 S_ = plane_mask<0>(" << P(sd, 1) << ") ^ (xm_ & ~pk_sra(d_, 15));\n";
             }
             o << "    const u32 x_ = leaf_ms<0x" << std::hex << op.fb << std::dec << "u, 0, 16>(M_, S_, ln);\n";
-            put(op.pos, 1, "x_ & 0x00010001u");
+            put_mask(op.pos, 1, "x_");
             o << "  }\n";
             if (f) clobber_parent(sd, 1);
             break;
@@ -322,7 +329,7 @@ struct Gen {
                   << ", FS_[" << i / 16 << "]), ln), acc_, 0u);\n";
             // two's complement or SM16: the hard decision is bit 15 / 31 either way
             o << "    }\n    full_ = pk_sra(acc_, 15);\n";
-            for (int j = 0; j < n; j += 16) put(op.pos + j, n < 16 ? n : 16, "full_");
+            for (int j = 0; j < n; j += 16) put_mask(op.pos + j, n < 16 ? n : 16, "full_");
             o << "  }\n";
             clobber_parent(sd, n);
             break;
@@ -483,10 +490,14 @@ struct Gen {
             for (int c = 0; c < (LPF + 63) / 64; c++) {
                 // the LDS row of lane i is base + 16 i whatever its global address, so a frame
                 // of fewer than 64 chunks (N < 1024) loads with the other lanes masked off
+                // the frame index clamped to the batch is wave-uniform: readfirstlane keeps it
+                // (and the frame address) in SGPRs -- computed per lane it cost ~150 VALU and
+                // 16 v_cndmask per wave
                 const std::string ch = "(" + std::to_string(c * 64) + " + lane)";
-                o << "    if (" << (LPF - c * 64 >= 64 ? std::string("true") : "lane < " + std::to_string(LPF - c * 64))
-                  << ") { const long fr_ = f0_ + " << f << " < batch ? f0_ + " << f << " : (long)batch - 1;\n"
-                  << "      __builtin_amdgcn_global_load_lds((gas_t)(lla_ + fr_ * " << N << " + " << ch
+                o << "    { const int fr_ = __builtin_amdgcn_readfirstlane((int)(f0_ + " << f << " < batch ? f0_ + " << f
+                  << " : (long)batch - 1));\n"
+                  << "      if (" << (LPF - c * 64 >= 64 ? std::string("true") : "lane < " + std::to_string(LPF - c * 64))
+                  << ") __builtin_amdgcn_global_load_lds((gas_t)(lla_ + (long)fr_ * " << N << " + " << ch
                   << " * 16), (las_t)(st_ + " << f * FS + c * 1024 << "), 16, 0, 0); }\n";
             }
         // Lane-derived values are recomputed after the fetch (the empty asm makes the lane

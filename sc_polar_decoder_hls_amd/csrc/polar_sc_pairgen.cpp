@@ -69,6 +69,12 @@ struct PairGen {
             o << "    bw[" << l / 16 << "] = bsel(" << hexmask(l, cnt) << ", (" << acc << ") << " << l % 16 << ", bw["
               << l / 16 << "]);\n";
     }
+    // the same from a full mask per half (leaf / REP decisions): no shift, no AND
+    void put_mask(int l, int cnt, const std::string &m)
+    {
+        if (cnt >= 16) o << "    bw[" << l / 16 << "] = " << m << ";\n";
+        else o << "    bw[" << l / 16 << "] = bsel(" << hexmask(l, cnt) << ", " << m << ", bw[" << l / 16 << "]);\n";
+    }
     std::string var(const char *p) { return std::string(p) + std::to_string(nvar++) + "_"; }
     void fence() { o << "  __builtin_amdgcn_sched_barrier(0);\n"; }
     void chunk_fence(int i, int n)
@@ -176,7 +182,7 @@ struct PairGen {
                 o << "      acc_ = rep_sm_rows(acc_, F_split_sm<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i)
                   << ", FS_[" << i / 16 << "]), ln);\n";
             o << "    }\n    const u32 full_ = pk_sra(acc_, 15);\n";
-            for (int j = 0; j < n4; j += 16) put(l0 + j, n4 < 16 ? n4 : 16, "full_");
+            for (int j = 0; j < n4; j += 16) put_mask(l0 + j, n4 < 16 ? n4 : 16, "full_");
             o << "  }\n";
             clobber_parent(pd, n4);
             break;
@@ -356,7 +362,7 @@ struct PairGen {
                 o << "  { // " << (h ? "H" : "H0") << " n 2\n    const u32 w_ = " << R;
                 if (h) o << " ^ (" << small2.at(op.pos) << " & row_lo2(c.row))";
                 o << ";\n";
-                put(op.pos / 4, 1, "w_ & 0x00010001u");
+                put_mask(op.pos / 4, 1, "w_");
                 o << "  }\n";
             }
             break;
