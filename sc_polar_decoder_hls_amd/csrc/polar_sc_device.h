@@ -363,6 +363,46 @@ __device__ __forceinline__ u32 sm8_of_byte(u32 b)
     const u32 m = (t < QP - t ? t : QP - t) & QMAG;
     return (t >= QP / 2u + 1u ? 0x80u : 0u) | m;
 }
+// wrapper_in + qconv_format on four channel bytes at once (LLR_BITS <= 7; SWAR within the
+// bytes, every step a plain 32-bit VALU op): t = byte & (2^Q - 1); |LLR| = min(t, 2^Q - t)
+// & (2^(Q-1) - 1) (so -2^(Q-1) -> +0); negative iff t > 2^(Q-1). Returns the magnitudes in
+// bits 0..Q-2 of each byte; sb receives the sign flags at bits 7, 15, 23, 31.
+//   sign: t + (127 - 2^(Q-1)) reaches bit 7 iff t > 2^(Q-1) (no carry out of a byte);
+//   2^Q - t = (t ^ (2^Q - 1)) + 1, the complement mask built from the sign bit.
+// (only called for LLR_BITS <= 7: at 8 the per-byte sums overflow)
+__device__ __forceinline__ u32 qconv4(u32 raw, u32 &sb)
+{
+    constexpr u32 B1 = 0x01010101u, QM = (1u << QB) - 1u;
+    const u32 t = raw & (QM * B1);
+    sb = (t + (127u - (1u << (QB - 1))) * B1) & 0x80808080u;
+    const u32 lsb = sb >> 7;
+    const u32 m = (sb >> (QB <= 7 ? 7 - QB : 0)) - lsb;   // 2^Q - 1 in the negative bytes
+    return ((t ^ m) + lsb) & (QMAG * B1);
+}
+
+// Byte transpose inside a quad of lanes (the four lanes of positions 4q .. 4q + 3 of a word,
+// which lane_pos keeps together): lane k of the quad holds the dword of those positions of
+// "combination" k (frame, word, ...); afterwards byte c of every lane is combination c's byte
+// at the lane's own position. Two quad-perm DPP moves and two v_perm with per-lane selectors.
+struct QuadSel {
+    u32 s1, s2;
+    __device__ __forceinline__ void init(u32 pl)
+    {
+        const u32 k = pl & 3u, m = lane_pos(pl) & 3u;
+        // round 1: [x_k[m], x_k^1[m], x_k[m ^ 2], x_k^1[m ^ 2]] from (own = bytes 0..3, partner = 4..7)
+        s1 = m | ((4u + m) << 8) | ((m ^ 2u) << 16) | ((4u + (m ^ 2u)) << 24);
+        // round 2: byte k <- y[0], k ^ 1 <- y[1], k ^ 2 <- partner y[2] (6), k ^ 3 <- partner y[3] (7)
+        s2 = (0u << (8 * k)) | (1u << (8 * (k ^ 1u))) | (6u << (8 * (k ^ 2u))) | (7u << (8 * (k ^ 3u)));
+    }
+};
+__device__ __forceinline__ u32 quad_transpose(u32 x, const QuadSel &q)
+{
+    const u32 t1 = __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+    const u32 y = __builtin_amdgcn_perm(t1, x, q.s1);
+    const u32 t2 = __builtin_amdgcn_update_dpp(0u, y, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    return __builtin_amdgcn_perm(t2, y, q.s2);
+}
+
 // two SM8 bytes (low byte of lo, low byte of hi) -> SM16 pair: duplicate each byte into both
 // bytes of its half, keep bit 15 and bits 0..4
 __device__ __forceinline__ u32 sm8_pair(u32 lo, u32 hi)

@@ -323,31 +323,22 @@ __device__ __forceinline__ T *uniform_ptr(T *p)
 struct ChanQ {
     const g_u8 *base;   // frame lo, byte 0 (wave-uniform)
     u32 off;            // this lane's combination at row 0, positions 4 q .. (bytes from base)
-    u32 s1, s2;         // v_perm selectors of the two transpose rounds
+    QuadSel sel;        // v_perm selectors of the two transpose rounds (polar_sc_device.h)
     bool al;            // frames 4-byte aligned (else the byte-load path)
 };
 __device__ __forceinline__ ChanQ chan_quad(const PairCtx &c)
 {
-    const u32 lane = threadIdx.x & 63u, pl = lane & 15u, k = pl & 3u, m = lane_pos(pl) & 3u;
+    const u32 lane = threadIdx.x & 63u, pl = lane & 15u, k = pl & 3u;
     ChanQ q;
     // chl = frame lo + 16 row + pos; chh - chl = (hi frame - lo frame) N (uniform)
     q.base = uniform_ptr(c.chl - (16u * (lane >> 4) + lane_pos(pl)));
     const u32 dhi = __builtin_amdgcn_readfirstlane((u32)(c.chh - c.chl));
     q.off = 16u * (lane >> 4) + (pl & ~3u) + 64u * (k & 1u) + ((k & 2u) ? dhi : 0u);
-    // round 1: [x_k[m], x_k^1[m], x_k[m ^ 2], x_k^1[m ^ 2]] from (own = bytes 0..3, partner = 4..7)
-    q.s1 = m | ((4u + m) << 8) | ((m ^ 2u) << 16) | ((4u + (m ^ 2u)) << 24);
-    // round 2: byte k <- y[0], k ^ 1 <- y[1], k ^ 2 <- partner y[2] (6), k ^ 3 <- partner y[3] (7)
-    q.s2 = (0u << (8 * k)) | (1u << (8 * (k ^ 1u))) | (6u << (8 * (k ^ 2u))) | (7u << (8 * (k ^ 3u)));
+    q.sel.init(pl);
     q.al = ((u32)(unsigned long)q.base & 3u) == 0u;
     return q;
 }
-__device__ __forceinline__ u32 quad_transpose(u32 x, const ChanQ &q)
-{
-    const u32 t1 = __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
-    const u32 y = __builtin_amdgcn_perm(t1, x, q.s1);
-    const u32 t2 = __builtin_amdgcn_update_dpp(0u, y, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
-    return __builtin_amdgcn_perm(t2, y, q.s2);
-}
+__device__ __forceinline__ u32 quad_transpose(u32 x, const ChanQ &q) { return quad_transpose(x, q.sel); }
 __device__ __forceinline__ u32 chan_conv(u32 raw)
 {
     if constexpr (PAIR_SWAR) return conv4(raw);

@@ -1,5 +1,6 @@
 """CPU check of the byte-parallel (SWAR) stage arithmetic of the pair kernels' upper levels
-(polar_sc_pair.h: F4, G4, conv4, ubits4, prow, ppack), restated line for line on numpy uint32
+(polar_sc_pair.h: F4, G4, conv4, ubits4, prow, ppack) and of the per-mask kernel's channel
+presplit (polar_sc_device.h: qconv4, QuadSel / quad_transpose), restated line for line on numpy uint32
 and compared exhaustively with the per-value SM16 definitions the register code uses
 (polar_sc_device.h F_sm / G_sm<GSAT> / conv_pair, in turn pinned to the oracle): every pair of
 SM8 values and flip flag in every byte position, the other three bytes random, for Q = 6 and 7
@@ -178,6 +179,63 @@ def test_swar_conv_exhaustive(Q):
     for pos in range(4):
         d = spread(rng, raw, pos)
         assert (byte(conv4(d, Q), pos) == ref_conv(raw, Q)).all(), "conv4 byte %d" % pos
+
+
+def qconv4(raw, Q):
+    """polar_sc_device.h qconv4: (magnitudes, sign bits at 7 / 15 / 23 / 31)"""
+    QMAG, _ = consts(Q)
+    QM = (1 << Q) - 1
+    t = raw & U(QM * B_ONE)
+    sb = ((t + U((127 - (1 << (Q - 1))) * B_ONE)) & U(M32)) & U(0x80808080)
+    lsb = sb >> U(7)
+    m = sub32(sb >> U(7 - Q), lsb)
+    return (((t ^ m) + lsb) & U(M32)) & U(QMAG * B_ONE), sb
+
+
+@pytest.mark.parametrize("Q", [5, 6, 7])
+def test_qconv4_exhaustive(Q):
+    """every channel byte in every byte position, the other three random: magnitude and sign
+    equal the qconv_format table of the byte path (sm8_of_byte)"""
+    rng = np.random.default_rng(30 + Q)
+    raw = np.arange(256, dtype=np.int64)
+    for pos in range(4):
+        d = spread(rng, raw, pos)
+        mag, sb = qconv4(d, Q)
+        got = byte(mag, pos) | byte(sb, pos)
+        assert (got == ref_conv(raw, Q)).all(), "qconv4 byte %d" % pos
+
+
+def lane_pos(pl):
+    return pl ^ (3 if pl & 4 else 0)   # POLAR_LANE_REMAP
+
+
+def test_quad_transpose():
+    """QuadSel / quad_transpose on a 16-lane row: lane k of a quad holds the four position
+    bytes of combination k; afterwards byte c of lane l is combination c at lane_pos(l)."""
+    rng = np.random.default_rng(4)
+    comb = rng.integers(0, 256, size=(4, 16))          # comb[c][position]
+    x = np.zeros(16, np.int64)
+    for pl in range(16):
+        q, k = pl >> 2, pl & 3
+        for b in range(4):
+            x[pl] |= int(comb[k][4 * q + b]) << (8 * b)
+    def dpp_quad(v, pat):   # quad_perm: lane i of a quad reads lane pat[i]
+        return np.array([v[(l & ~3) + pat[l & 3]] for l in range(16)])
+    def vperm(s0, s1, sel):
+        return np.array([int(perm(U(int(s0[l])), U(int(s1[l])), int(sel[l]))) for l in range(16)])
+    s1 = np.zeros(16, np.int64)
+    s2 = np.zeros(16, np.int64)
+    for pl in range(16):
+        k, m = pl & 3, lane_pos(pl) & 3
+        s1[pl] = m | ((4 + m) << 8) | ((m ^ 2) << 16) | ((4 + (m ^ 2)) << 24)
+        s2[pl] = (0 << (8 * k)) | (1 << (8 * (k ^ 1))) | (6 << (8 * (k ^ 2))) | (7 << (8 * (k ^ 3)))
+    t1 = dpp_quad(x, (1, 0, 3, 2))
+    y = vperm(t1, x, s1)
+    t2 = dpp_quad(y, (2, 3, 0, 1))
+    out = vperm(t2, y, s2)
+    for pl in range(16):
+        for c in range(4):
+            assert (out[pl] >> (8 * c)) & 0xFF == comb[c][lane_pos(pl)], (pl, c)
 
 
 @pytest.mark.parametrize("Q", [6, 7, 8])

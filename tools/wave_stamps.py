@@ -43,6 +43,7 @@ int main()
     for (int b = 0; b < NB; b++) hipMemcpy(llr + (size_t)b * h.size(), h.data(), h.size(), hipMemcpyHostToDevice);
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     float ms = 0.f;
+    std::vector<double> lms;
     for (int it = 0; it < 40; it++) {
         hipMemset(st, 0, (size_t)waves * NS * 8);
         hipEventRecord(e0);
@@ -50,7 +51,19 @@ int main()
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         hipEventElapsedTime(&ms, e0, e1);
+        if (it >= 10) lms.push_back(ms * 1e3);
     }
+    // back-to-back launches without the stamp reset in between (the bench's loop shape)
+    hipEventRecord(e0);
+    for (int it = 0; it < 50; it++)
+        polar_sc_mask_kernel<<<waves / 4, 256>>>(llr + (size_t)(it % NB) * h.size(), out, batch, G, st);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float bb = 0.f;
+    hipEventElapsedTime(&bb, e0, e1);
+    std::sort(lms.begin(), lms.end());
+    printf("launch median over 30: %.2f us; 50 back-to-back launches: %.2f us each\n", lms[lms.size() / 2],
+           bb * 1e3 / 50);
     std::vector<unsigned long long> s((size_t)waves * NS);
     hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost);
     auto q = [](std::vector<double> v, double p) { std::sort(v.begin(), v.end()); return v[(size_t)(p * (v.size() - 1))]; };
@@ -139,6 +152,8 @@ def build(out_name="wave_stamps", src=None):
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "build":
-        build()
+        # optional: an output name and a saved per-mask kernel source (same-box A/B of variants)
+        name = sys.argv[2] if len(sys.argv) > 2 else "wave_stamps"
+        build(name, open(sys.argv[3]).read() if len(sys.argv) > 3 else None)
     else:
-        sys.exit("usage: tools/wave_stamps.py build   (then run build_tools/wave_stamps on the GPU box)")
+        sys.exit("usage: tools/wave_stamps.py build [name [kernel source]]   (then run build_tools/<name> on the GPU box)")
