@@ -363,23 +363,6 @@ __device__ __forceinline__ u32 sm8_of_byte(u32 b)
     const u32 m = (t < QP - t ? t : QP - t) & QMAG;
     return (t >= QP / 2u + 1u ? 0x80u : 0u) | m;
 }
-// wrapper_in + qconv_format on four channel bytes at once (LLR_BITS <= 7; SWAR within the
-// bytes, every step a plain 32-bit VALU op): t = byte & (2^Q - 1); |LLR| = min(t, 2^Q - t)
-// & (2^(Q-1) - 1) (so -2^(Q-1) -> +0); negative iff t > 2^(Q-1). Returns the magnitudes in
-// bits 0..Q-2 of each byte; sb receives the sign flags at bits 7, 15, 23, 31.
-//   sign: t + (127 - 2^(Q-1)) reaches bit 7 iff t > 2^(Q-1) (no carry out of a byte);
-//   2^Q - t = (t ^ (2^Q - 1)) + 1, the complement mask built from the sign bit.
-// (only called for LLR_BITS <= 7: at 8 the per-byte sums overflow)
-__device__ __forceinline__ u32 qconv4(u32 raw, u32 &sb)
-{
-    constexpr u32 B1 = 0x01010101u, QM = (1u << QB) - 1u;
-    const u32 t = raw & (QM * B1);
-    sb = (t + (127u - (1u << (QB - 1))) * B1) & 0x80808080u;
-    const u32 lsb = sb >> 7;
-    const u32 m = (sb >> (QB <= 7 ? 7 - QB : 0)) - lsb;   // 2^Q - 1 in the negative bytes
-    return ((t ^ m) + lsb) & (QMAG * B1);
-}
-
 // Byte transpose inside a quad of lanes (the four lanes of positions 4q .. 4q + 3 of a word,
 // which lane_pos keeps together): lane k of the quad holds the dword of those positions of
 // "combination" k (frame, word, ...); afterwards byte c of every lane is combination c's byte

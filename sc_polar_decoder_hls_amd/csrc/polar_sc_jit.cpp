@@ -64,7 +64,6 @@ struct Gen {
     // F / G word. C2: 158 -> 126 VGPRs, 3 -> 4 waves per SIMD, 76.7 -> 72.7 / 75.5 us on one
     // box
     bool pack = false;
-    int FS_ = 0;   // per-mask kernels: LDS frame stride of the staged channel
     Gen(const std::vector<polar_sc_op> &ops_, int lg) : ops(ops_), LG(lg) {}
 
     // Partial sums: u32 bw[max(1, G / 16)], dword j = groups 16 j .. 16 j + 15, low frame in
@@ -201,40 +200,16 @@ struct Gen {
     }
 
     // Per-mask kernels: wrapper_in + qconv_format (wrapper_in.h:26-44, scalar.h:229-239) once
-    // per frame. Every channel word becomes a magnitude pair m<LG>[w] and a bit of the sign
+    // per frame. (Tried in round 4 and reverted: one ds_read_b32 per root register + quad byte
+    // transpose + SWAR conversion instead of the 12 byte / table reads: 236 more VALU per wave,
+    // 84.0 vs 83.4 us on one box, profiles/r04_ab/c2_presplit_ab.txt -- the presplit is not
+    // LDS-bound.) Every channel word becomes a magnitude pair m<LG>[w] and a bit of the sign
     // plane s<LG>[w / 16] (two LDS tables give |LLR| and the sign of a channel byte), so the
     // root F / G are the split-word ops of every other level (F: 1 VALU per word instead of
     // 10, G: 10 instead of 18) for a conversion of about 3 VALU per word.
-    // LLR_BITS <= 7: the presplit reads the staged channel by dwords and converts four bytes
-    // at once (qconv4) instead of 12 byte loads / table lookups per packed root register
-    bool swar_chan = false;
     void root_presplit(int words)
     {
         for (int k = 0; k < planes(words); k++) o << "  s" << LG << "[" << k << "] = 0u;\n";
-        if (pack && swar_chan) {
-            // lane k of each quad loads the dword of its quad's four positions of combination
-            // k = (frame row / row + 4, word i / i + G/2); the quad transpose gives every lane
-            // [a0, b0, a1, b1] at its own position -- the packed root register's byte order --
-            // and qconv4 converts the four bytes. Per register: 1 ds_read_b32, 4 + 9 VALU, the
-            // sign planes 2 x 3 (the byte loads + LDS tables of the other path: 12 LDS reads,
-            // whose dependent chains made the presplit of the first dispatch round LDS-bound,
-            // profiles/r04_c2_wave_timeline.txt)
-            const int h = words / 2;
-            o << "  { QuadSel qs_; qs_.init((u32)pl);\n"
-              << "    const u32 qk_ = (u32)pl & 3u;\n"
-              << "    const unsigned char *qb_ = st_ + (row + 4 * (int)(qk_ >> 1)) * " << FS_ << " + 4 * (pl >> 2) + "
-              << "(int)(qk_ & 1u) * " << 16 * h << ";\n";
-            for (int i = 0; i < h; i++) {
-                const int j = i + h;
-                o << "    { u32 sb_; pr[" << i << "] = qconv4(quad_transpose(*(const u32 *)(qb_ + " << 16 * i
-                  << "), qs_), sb_);\n"
-                  << "      s" << LG << "[" << i / 16 << "] |= ((sb_ >> 7) & 0x00010001u) << " << i % 16 << ";\n"
-                  << "      s" << LG << "[" << j / 16 << "] |= ((sb_ >> 15) & 0x00010001u) << " << j % 16 << "; }\n";
-                chunk_fence(i, h);
-            }
-            o << "  }\n";
-            return;
-        }
         if (pack) {
             const int h = words / 2;
             for (int i = 0; i < h; i++) {
@@ -488,8 +463,6 @@ struct Gen {
         const int wpb = MASK_WPB;
         presplit = true;
         pack = G >= 2;
-        FS_ = FS;
-        swar_chan = p.cfg.llr_bits <= 7;
         o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
           << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
           << "typedef const __attribute__((address_space(1))) void *gas_t;\n"
@@ -497,13 +470,11 @@ struct Gen {
           << "extern \"C\" __global__ void __launch_bounds__(" << 64 * wpb << ", " << MASK_MIN_WAVES
           << ") polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
-          << "  __shared__ uint4 stage_[" << wpb << " * 8 * " << FS / 16 << "];\n";
-        if (!swar_chan)   // (LLR_BITS 8: LDS tables of qconv_format; qconv4 below otherwise)
-            o << "  __shared__ unsigned char tabm_[256], tabs_[256];   // channel byte -> |LLR|, sign (qconv_format)\n"
-              << "  for (u32 t_ = threadIdx.x; t_ < 256u; t_ += " << 64 * wpb << "u) { const u32 v_ = sm8_of_byte(t_);\n"
-              << "    tabm_[t_] = (unsigned char)(v_ & QMAG); tabs_[t_] = (unsigned char)(v_ >> 7); }\n"
-              << "  __syncthreads();\n";
-        o
+          << "  __shared__ uint4 stage_[" << wpb << " * 8 * " << FS / 16 << "];\n"
+          << "  __shared__ unsigned char tabm_[256], tabs_[256];   // channel byte -> |LLR|, sign (qconv_format)\n"
+          << "  for (u32 t_ = threadIdx.x; t_ < 256u; t_ += " << 64 * wpb << "u) { const u32 v_ = sm8_of_byte(t_);\n"
+          << "    tabm_[t_] = (unsigned char)(v_ & QMAG); tabs_[t_] = (unsigned char)(v_ >> 7); }\n"
+          << "  __syncthreads();\n"
           << "  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR batch indices\n"
           << "  const long nw_ = ((long)batch + 7) / 8;\n"
           << "  long wave = (long)blockIdx.x * " << wpb << " + wib;\n"

@@ -1,6 +1,6 @@
 """CPU check of the byte-parallel (SWAR) stage arithmetic of the pair kernels' upper levels
-(polar_sc_pair.h: F4, G4, conv4, ubits4, prow, ppack) and of the per-mask kernel's channel
-presplit (polar_sc_device.h: qconv4, QuadSel / quad_transpose), restated line for line on numpy uint32
+(polar_sc_pair.h: F4, G4, conv4, ubits4, prow, ppack) and the quad byte transpose of the
+channel reads (polar_sc_device.h QuadSel / quad_transpose), restated line for line on numpy uint32
 and compared exhaustively with the per-value SM16 definitions the register code uses
 (polar_sc_device.h F_sm / G_sm<GSAT> / conv_pair, in turn pinned to the oracle): every pair of
 SM8 values and flip flag in every byte position, the other three bytes random, for Q = 6 and 7
@@ -179,30 +179,6 @@ def test_swar_conv_exhaustive(Q):
     for pos in range(4):
         d = spread(rng, raw, pos)
         assert (byte(conv4(d, Q), pos) == ref_conv(raw, Q)).all(), "conv4 byte %d" % pos
-
-
-def qconv4(raw, Q):
-    """polar_sc_device.h qconv4: (magnitudes, sign bits at 7 / 15 / 23 / 31)"""
-    QMAG, _ = consts(Q)
-    QM = (1 << Q) - 1
-    t = raw & U(QM * B_ONE)
-    sb = ((t + U((127 - (1 << (Q - 1))) * B_ONE)) & U(M32)) & U(0x80808080)
-    lsb = sb >> U(7)
-    m = sub32(sb >> U(7 - Q), lsb)
-    return (((t ^ m) + lsb) & U(M32)) & U(QMAG * B_ONE), sb
-
-
-@pytest.mark.parametrize("Q", [5, 6, 7])
-def test_qconv4_exhaustive(Q):
-    """every channel byte in every byte position, the other three random: magnitude and sign
-    equal the qconv_format table of the byte path (sm8_of_byte)"""
-    rng = np.random.default_rng(30 + Q)
-    raw = np.arange(256, dtype=np.int64)
-    for pos in range(4):
-        d = spread(rng, raw, pos)
-        mag, sb = qconv4(d, Q)
-        got = byte(mag, pos) | byte(sb, pos)
-        assert (got == ref_conv(raw, Q)).all(), "qconv4 byte %d" % pos
 
 
 def lane_pos(pl):

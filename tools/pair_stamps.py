@@ -81,7 +81,23 @@ int main()
 NAMES = {1: "F", 2: "G", 5: "REP", 6: "R1", 7: "SPC", 8: "H", 9: "H0", 13: "SUB"}
 
 
-def build(mask_name, batch, tuning):
+def drop_subtree_fences(src):
+    """A/B variant: the generated subtree decoders without their scheduling fences (the
+    sched_barrier before every op and every 8 registers), so that the machine scheduler can
+    overlap an op's independent prefix with the previous op's dependent tail."""
+    out, inside = [], False
+    for line in src.split("\n"):
+        if line.startswith("__device__ __noinline__ void polar_psub_"):
+            inside = True
+        elif line.startswith("}"):
+            inside = False
+        if inside and line.strip() == "__builtin_amdgcn_sched_barrier(0);":
+            continue
+        out.append(line)
+    return "\n".join(out)
+
+
+def build(mask_name, batch, tuning, variant=""):
     import sc_polar_decoder_hls_amd as pkg
     import util
     mask = util.mask(mask_name)
@@ -89,26 +105,14 @@ def build(mask_name, batch, tuning):
     st = dec.stats
     assert st["kernel"] == 3 and st["tier_steps"] == 0, "pair plan without grid tier expected"
     src = dec.kernel_source()
+    if variant == "nofence":
+        src = drop_subtree_fences(src)
     N, G, S = mask.size, mask.size // 16, st["sub_words"]
-    # launch shape of jit_launch_pair (polar_sc_jit.cpp): waves per pair, LDS slot levels
-    pairs, simds, cus = (batch + 1) // 2, 1024, 256
-    W = tuning.get("waves_per_group", 0)
-    if not W:
-        W = 1
-        while W < 8 and pairs * W < 2 * simds:
-            W *= 2
+    # launch shape of the library's own decision (polar_sc_plan_launch_info)
+    info = dec.launch_info(batch)
+    W, lds_row0, lds = info["waves_per_block"], info["lds_row0"], info["lds_bytes"]
     slot_rows = (G - S) // 4
-    pair_dwords = slot_rows * 32 + (G // 64) * 64
-    per_cu = -(-pairs // cus)
-    budget = 160 * 1024 // per_cu - 3 * W * 256
-    L, w = 0, S
-    while w <= G // 2:
-        if 32 * (2 * w - S) <= budget:
-            L = w
-        w *= 2
-    lds_rows = (2 * L - S) // 4 if L else 0
-    lds_row0 = slot_rows - lds_rows
-    lds = lds_rows * 128 + 3 * W * 256
+    pair_dwords = st["scratch_bytes_per_wave"] // 4
     # stamp segment 0: after pair_init, after every op
     head = "int lds_row0, int seg)\n{\n"
     k = src.index("polar_sc_pair_kernel(")
@@ -147,10 +151,11 @@ def build(mask_name, batch, tuning):
     tab = ("static const char *LABEL[] = {%s};\nstatic const char *CLASS[] = {%s};\n"
            % (", ".join('"%s"' % s for s in labels), ", ".join('"%s"' % s for s in classes)))
     os.makedirs(OUT, exist_ok=True)
-    path = os.path.join(OUT, "pair_stamps_%s_b%d.hip" % (mask_name, batch))
+    tag = "pair_stamps_%s_b%d%s" % (mask_name, batch, "_" + variant if variant else "")
+    path = os.path.join(OUT, tag + ".hip")
     with open(path, "w") as f:
         f.write("#include <hip/hip_runtime.h>\n" + defs + src + tab + DRIVER)
-    exe = os.path.join(OUT, "pair_stamps_%s_b%d" % (mask_name, batch))
+    exe = os.path.join(OUT, tag)
     subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", CSRC, "-o", exe, path])
     print(exe, "ops", n, "W", W, "lds_row0", lds_row0, "of", slot_rows)
 
@@ -161,6 +166,7 @@ if __name__ == "__main__":
     ap.add_argument("--mask", default="frozen_n_65536_k_32768")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--tuning", default="")
+    ap.add_argument("--variant", default="", choices=["", "nofence"])
     a = ap.parse_args()
     tun = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, a.tuning.split(",")))}
-    build(a.mask, a.batch, tun)
+    build(a.mask, a.batch, tun, a.variant)
