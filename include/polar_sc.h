@@ -88,7 +88,9 @@ typedef struct polar_sc_tuning {
     int32_t tier_words;       /* hybrid HBM-scratch plans: F / G records of >= this many words
                                  run as grid launches; 0 = automatic, -1 = no grid tier */
     int32_t lds_slots;        /* HBM-scratch plans: stage slots held in LDS, 0 = automatic,
-                                 else 256, 512 or 1024 */
+                                 else 256, 512 or 1024; pair plans: the levels of nodes of
+                                 up to this many words sit in LDS whatever the batch (the
+                                 default fits them to the LDS share of the resident pairs) */
     int32_t hybrid_waves;     /* hybrid plans: waves per group of the kernel's launch bound,
                                  0 = automatic (8), else 4 or 8 */
     int32_t chain_max;        /* pair plans: F / G records fused into one descent chain

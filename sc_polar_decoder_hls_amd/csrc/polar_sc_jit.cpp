@@ -980,6 +980,13 @@ PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, in
         if (tier && w >= p.pair_tier.tw) break;
         if (32l * (2l * w - S) <= budget) L = w;
     }
+    // polar_sc_tuning.lds_slots: the levels of nodes up to this many words in LDS whatever
+    // the batch (fewer pairs then fit a CU: the A/B of keeping more levels on chip)
+    if (const int want = p.tune.lds_slots) {
+        L = 0;
+        for (int w = S; w <= G / 2 && w <= want; w *= 2)
+            if (!(tier && w >= p.pair_tier.tw) && 32l * (2l * w - S) + 3l * W * 256l <= CU_LDS_BYTES) L = w;
+    }
     const int lds_rows = L ? (2 * L - S) / 4 : 0;
     sh.lds_row0 = p.pair_slot_rows - lds_rows;
     sh.lds = (unsigned)(lds_rows * 128 + 3 * W * 256);

@@ -76,11 +76,13 @@ struct PairGen {
         else o << "    bw[" << l / 16 << "] = bsel(" << hexmask(l, cnt) << ", " << m << ", bw[" << l / 16 << "]);\n";
     }
     std::string var(const char *p) { return std::string(p) + std::to_string(nvar++) + "_"; }
-    void fence() { o << "  __builtin_amdgcn_sched_barrier(0);\n"; }
-    void chunk_fence(int i, int n)
-    {
-        if ((i & 7) == 7 && i + 1 < n) fence();
-    }
+    // No scheduling fences in the subtree decoders (the per-mask kernel keeps them for its
+    // register budget): the machine scheduler may then overlap an op's independent prefix
+    // with the previous op's dependent tail. Same box, two rounds (tools/pair_stamps.py
+    // --variant nofence, profiles/r04_ab/subtree_fence_ab_stamps.txt): C5 64-frame share
+    // 1326 / 1335 vs 1345 / 1350 us (subtrees -1.5 %), C3 unchanged (980 / 979 vs 989 / 975).
+    void fence() {}
+    void chunk_fence(int, int) {}
     // after an F-type op the parent words stay live until the matching G: an empty asm that
     // redefines them keeps the F op's intermediates from being carried across the left subtree
     void clobber_parent(int sd, int n4)

@@ -124,6 +124,23 @@ def test_pair_waves_per_pair(pkg, cuda, oracle_mod, wpg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lds_slots,batch", [(256, 300), (1024, 4096)])
+def test_pair_forced_lds_levels(pkg, cuda, oracle_mod, lds_slots, batch):
+    """polar_sc_tuning.lds_slots on a pair plan: the slot levels of nodes up to that many
+    words sit in LDS whatever the batch -- fewer than the default at 300 frames (W = 8, where
+    every level fits), more at 4096 (W = 1, 8 pairs per CU: the default keeps one level)."""
+    mask = util.mask("frozen_n_65536_k_32768")
+    llr, _ = util.synth_frames(mask, batch, ebn0_db=1.0, seed=lds_slots)
+    dec = pair(pkg, mask, lds_slots=lds_slots)
+    info, dflt = dec.launch_info(batch), pair(pkg, mask).launch_info(batch)
+    assert info["lds_row0"] != dflt["lds_row0"], (info, dflt)
+    got = run(pkg, cuda, dec, llr)
+    _assert_same(got, run(pkg, cuda, pair(pkg, mask), llr), "lds_slots %d vs default" % lds_slots)
+    idx = np.r_[0:3, batch - 3:batch]
+    _assert_same(got[idx], oracle_mod.decode_fsm(mask, llr[idx]), "lds_slots %d vs oracle" % lds_slots)
+
+
+@pytest.mark.gpu
 def test_pair_all_hbm_slots_large_batch(pkg, cuda, oracle_mod):
     """A batch large enough that no slot level fits the LDS share of a pair (every level in
     HBM): equal to the hybrid kernel on every frame and to the oracle on a sample."""
