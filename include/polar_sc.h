@@ -322,8 +322,9 @@ int polar_count_errors(const uint64_t *xhat_dev, const uint64_t *xref_dev, uint3
  * The analogue of the reference's latency monitor (sc_monitor.h:50-140 over my_module's
  * Fct_ID / N_value ports, my_module.h:21-30): one synchronous decode of `batch` resident
  * frames (hard_bits_dev receives the same x^ as polar_sc_decode) with the schedule
- * interpreter instrumented (hybrid plans: the hybrid kernel; per-mask plans are profiled
- * on the interpreter, which runs the same schedule). For every device op, the shader-clock
+ * interpreter instrumented (hybrid plans: the hybrid kernel; per-mask and pair plans are
+ * profiled on the interpreter, which runs the same schedule, and the pair kernel is not
+ * compiled for it; tools/pair_stamps.py stamps the pair kernel itself). For every device op, the shader-clock
  * cycles from its start to the next op's start, measured on the lead wave of frame group 0
  * while the rest of the batch runs. recs == NULL: only *count (the number of device ops,
  * END included) is returned. Device ops are the schedule of polar_sc_plan_get_schedule plus,
