@@ -32,10 +32,10 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # bytes they report (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
 # roofline.traffic when the benchmarked (mask, frames per GPU) is the profiled one.
 TRAFFIC_PROFILES = {
-    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r04_v1_c2_pmc.json"),
-    ("frozen_n_65536_k_32768", 4096): os.path.join(ROOT, "profiles", "r04_v1_c3_pmc.json"),
-    ("frozen_n_262144_k_131072", 512): os.path.join(ROOT, "profiles", "r04_v1_c5_pmc.json"),
-    ("frozen_n_262144_k_131072", 64): os.path.join(ROOT, "profiles", "r04_v1_c5b64_pmc.json"),
+    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r04_v2_c2_pmc.json"),
+    ("frozen_n_65536_k_32768", 4096): os.path.join(ROOT, "profiles", "r04_v2_c3_pmc.json"),
+    ("frozen_n_262144_k_131072", 512): os.path.join(ROOT, "profiles", "r04_v2_c5_pmc.json"),
+    ("frozen_n_262144_k_131072", 64): os.path.join(ROOT, "profiles", "r04_v2_c5b64_pmc.json"),
 }
 # Rotated input: the timed loop cycles through distinct resident batches of at least this
 # many bytes in total, so the LLR reads come from HBM and not from the 256 MB Infinity Cache
@@ -241,8 +241,8 @@ SECONDARY = (
 def roofline_entry(name, N, per_gpu, kern_ms, dec, fmt=None):
     """HBM roofline of one decode launch sequence: algorithmic bytes (1.125 N per frame) over
     the event-timed kernel time; traffic from the committed PMC summary of the same workload,
-    used only when that profile is of the code object timed here (its code_key, recorded by
-    tools/prof_decode.py, equals this plan's)."""
+    used only when that profile is of the machine code timed here (its code_key -- the hash of
+    the kernels' instructions and descriptors, polar_sc_plan_launch_info -- equals this plan's)."""
     bytes_per_launch = 1.125 * N * per_gpu
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src, prof, note = None, None, None, None

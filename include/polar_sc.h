@@ -43,8 +43,10 @@ extern "C" {
  *     (script/parser.sh:15,43);
  *   * extended 1/0 (config.h:14: exact or saturating leaves);
  *   * par 4, 8, 16, 32 or 64 (script_tests.sh:11 runs 16 and 64, script_RTL_sim.sh 4..64).
- * The shipped datapath (sigmag 1, par 16, extended 1, llr_bits <= 8) runs the specialised
- * kernels; every other format runs the schedule interpreter compiled for it. elag_rare = 1
+ * The shipped datapath (sigmag 1, par 16, llr_bits <= 8; either extended, every pruning level
+ * and elag combination) runs the generated kernels, and so does PAR 64 (sigmag 1, extended 1,
+ * llr_bits <= 8, pruning_level 0 / 2) for N >= 2048; every other format runs the schedule
+ * interpreter compiled for it. elag_rare = 1
  * (does not compile in the reference, my_module.h:255 vs :1511) is rejected with -ENOTSUP.
  */
 typedef struct polar_sc_config {
@@ -74,8 +76,8 @@ typedef struct polar_sc_tuning {
     int32_t kernel;           /* 0 = automatic; 1 = the schedule interpreter for every N
                                  (no per-mask / generated-subtree code); 2 = the hybrid
                                  kernel (8-frame groups) for N > 1024; 3 = the pair kernel
-                                 (one frame pair per wave) for N >= 2048 in the shipped
-                                 datapath or PAR 64. A forced kernel or sub_words the plan
+                                 (one frame pair per wave) for N >= 2048 in the generated
+                                 datapaths above. A forced kernel or sub_words the plan
                                  cannot use is an error (-ENOTSUP / -EINVAL), never a
                                  silent fallback */
     int32_t waves_per_group;  /* interpreter / hybrid launches: waves per 8-frame group, 0 =
@@ -284,8 +286,10 @@ typedef struct polar_sc_launch_info {
     uint64_t blocks;            /* workgroups of the decode launch */
     uint32_t lds_bytes;         /* dynamic LDS per block */
     uint32_t lds_row0;          /* pair plans: first stage-slot row held in LDS */
-    uint64_t code_key;          /* key of the plan's generated code object in the hipRTC
-                                   cache (lib/rtc_cache/<key>.co), 0 = none */
+    uint64_t code_key;          /* identity of the machine code: hash of the instructions
+                                   and kernel descriptors of the plan's compiled code
+                                   object (equal code -> equal key whatever the source
+                                   text), 0 = none */
 } polar_sc_launch_info;
 
 int polar_sc_plan_launch_info(const polar_sc_plan *plan, size_t batch, uint32_t cus, polar_sc_launch_info *info);

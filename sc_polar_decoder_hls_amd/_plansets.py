@@ -126,6 +126,75 @@ FORMATS = [
 # the rate-0.9 codes of script_tests.sh:7-9 (QUANT 8)
 RATE09_MASKS = ("frozen_n_2048_k_1844", "frozen_n_4096_k_3686", "frozen_n_8192_k_7372", "frozen_n_16384_k_14746")
 
+# ---- pruning / ELAG sweep (tests/test_gpu_configs.py, test_gpu_formats.py) -------------------
+# (pruning_level, elag_r1, elag_rep, elag_spc, elag_rep2, elag_spc2, elag_h0): the loop of
+# script/script_tests.sh:103-122, then REP2 / SPC2 / H0 switched at PRUNING_LEVEL 2
+PRUNING_SWEEP = (
+    (0, 0, 0, 0, 0, 0, 0), (1, 0, 0, 0, 0, 0, 0), (1, 1, 0, 0, 0, 0, 0), (1, 1, 1, 0, 0, 0, 0),
+    (1, 1, 1, 1, 0, 0, 0), (1, 1, 1, 1, 1, 0, 0), (1, 1, 1, 1, 1, 1, 0), (2, 0, 0, 0, 0, 0, 1),
+    (2, 1, 0, 0, 0, 0, 1), (2, 1, 1, 0, 0, 0, 1), (2, 1, 1, 1, 0, 0, 1),
+    (2, 1, 1, 1, 0, 0, 0), (2, 1, 1, 1, 1, 1, 1),
+)
+SHIPPED_C7 = (2, 1, 1, 1, 0, 0, 1)   # config.h
+SWEEP_MASKS = ("FB_N128_K64", "FB_N1024_K512", "frozen_n_2048_k_1024", "frozen_n_8192_k_4096")
+PLANTED_N = (32, 256, 1024, 4096)
+FORMAT_C7 = ((2, 1, 1, 1, 0, 0, 1), (1, 1, 1, 1, 1, 1, 0), (0, 0, 0, 0, 0, 0, 0), (2, 1, 1, 1, 1, 1, 0))
+QBITS_MASKS = ("FB_N128_K64", "FB_N1024_K512", "frozen_n_4096_k_2048")
+
+
+def planted_mask(rng, N, par=16):
+    """Random mask with PAR groups of every pruned class (R0 / R1 / REP / SPC / REP2 / SPC2)."""
+    all1 = (1 << par) - 1
+    pats = [0, all1, 1 << (par - 1), all1 & ~1, 3 << (par - 2), all1 & ~3]
+    m = (rng.random(N) < 0.5).astype(np.uint8)
+    for g in range(N // par):
+        if rng.random() < 0.6:
+            p = int(rng.choice(pats))
+            m[par * g:par * g + par] = [(p >> k) & 1 for k in range(par)]
+    return m
+
+
+def sweep_planted_mask(N):
+    return planted_mask(np.random.default_rng(800 + N), N)
+
+
+def format_seed(fmt):
+    par, sigmag, ext, q = fmt
+    return par * 7 + sigmag * 3 + ext + q * 11
+
+
+def format_masks(fmt):
+    """(name, mask) of the format test: LDS (N <= 4096) and HBM-scratch (N = 16384) storage."""
+    par = fmt[0]
+    return [("FB_N1024_K512", mask("FB_N1024_K512")),
+            ("planted_4096", planted_mask(np.random.default_rng(format_seed(fmt)), 4096, par)),
+            ("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"))]
+
+
+def c7_fields(c7):
+    keys = ("pruning_level", "elag_r1", "elag_rep", "elag_spc", "elag_rep2", "elag_spc2", "elag_h0")
+    return dict(zip(keys, c7))
+
+
+def sweep_items():
+    """(name, mask, config fields, tuning) of every plan the pruning / format sweeps decode."""
+    out = []
+    for c7 in PRUNING_SWEEP:
+        out += [(n, mask(n), c7_fields(c7), None) for n in SWEEP_MASKS]
+        out += [("planted%d" % N, sweep_planted_mask(N), c7_fields(c7), None) for N in PLANTED_N]
+    # script_tests.sh:105-106's loop at PAR 16, QUANT 8 on the default (pair) kernel
+    out += [("frozen_n_32768_k_29492", mask("frozen_n_32768_k_29492"), dict(c7_fields(c7), llr_bits=8), None)
+            for c7 in PRUNING_SWEEP]
+    for q in (5, 7, 8):
+        for c7 in (SHIPPED_C7, (1, 1, 1, 1, 1, 1, 0)):
+            out += [(n, mask(n), dict(c7_fields(c7), llr_bits=q), None) for n in QBITS_MASKS]
+    for fmt in FORMATS:
+        par, sigmag, ext, q = fmt
+        for n, m in format_masks(fmt):
+            out += [(n, m, dict(c7_fields(c7), par=par, sigmag=sigmag, extended=ext, llr_bits=q), None)
+                    for c7 in FORMAT_C7]
+    return out
+
 
 def prewarm_all(verbose=False):
     """Compile every plan above (and the reference-config plan of every mask fixture) into
@@ -146,3 +215,7 @@ def prewarm_all(verbose=False):
     _build.prewarm({n: mask(n) for n in RATE09_MASKS}, configs=[q8], verbose=verbose)
     _build.prewarm_plans(gpu_plans() + cpu_test_plans(), verbose=verbose)
     _build.prewarm_items(gpu_par64_plans(), verbose=verbose)
+    # the pruning / ELAG / format sweeps: PRUNING_LEVEL 1 leaf decoders and EXTENDED 0 run the
+    # generated kernels (one code object per mask and configuration); the interpreter formats
+    # share one per format
+    _build.prewarm_items(sweep_items(), verbose=verbose)

@@ -430,9 +430,33 @@ __device__ __forceinline__ u32 leaf_ms(u32 M, u32 S, const Lanes &ln)
         const u32 x = opaque(SF ^ xorlane<H>(xa));
         const u32 lt = opaque(pk_sra(pk_sub(PM, M), 15));
         // magnitude: signs differ -> max - min, else max + min  (min = the F magnitude)
-        const u32 Mb = pk_mad_u16(Mf, x | 0x00010001u, pk_max_u16(M, PM));
+        // (EXTENDED = 0: Function_G's clamp inside the leaf too, as leaf_dp)
+        u32 Mb = pk_mad_u16(Mf, x | 0x00010001u, pk_max_u16(M, PM));
+        if constexpr (!EXT) Mb = pk_min(Mb, GSAT2);
         const u32 xb = leaf_ms<FB, B + H, H>(Mb, S ^ (x & ~lt), ln);
         return bselo(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
+    }
+}
+
+// A generated leaf record (polar_sc_op.fb: frozen pattern in bits 0..15, PRUNING_LEVEL 1
+// decoder in bits 16..18): the plain leaf, or the REP / SPC / REP2 / SPC2 row decoders of the
+// interpreter (leaf_kind_dp, SIGMAG) on the SM16 word of the split operands. Same output
+// convention as leaf_ms (16-bit masks).
+template <u32 FB>
+__device__ __forceinline__ u32 leaf_gen(u32 M, u32 S, const Lanes &ln)
+{
+    constexpr u32 KIND = (FB >> 16) & 7u;
+    static_assert(KIND <= 4, "POLAR_LEAF_R1 is a CA2 decoder");
+    if constexpr (KIND == 0) {
+        return leaf_ms<FB & 0xFFFFu, 0, 16>(M, S, ln);
+    } else {
+        const u32 L = M | (S & SGN);
+        u32 x;
+        if constexpr (KIND == 1) x = leaf_rep(L, ln);
+        else if constexpr (KIND == 2) x = leaf_spc<false>(L, ln);
+        else if constexpr (KIND == 3) x = leaf_rep2(L, ln);
+        else x = leaf_spc<true>(L, ln);
+        return pk_sra(x, 15);
     }
 }
 

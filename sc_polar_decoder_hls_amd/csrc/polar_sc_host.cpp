@@ -457,9 +457,17 @@ bool config_supported(const polar_sc_config &c)
 // the shipped datapath (SIGMAG, PAR 16, EXTENDED, int8-range LLRs): the only one the per-mask
 // and generated-subtree kernels implement; every other format runs the schedule interpreter
 // compiled by hipRTC with its POLAR_* switches
+// the datapath of the generated kernels (per-mask, hybrid, pair): SIGMAG, PAR 16, LLR_BITS <= 8,
+// EXTENDED 0 or 1 (POLAR_EXT of the generated source)
 bool default_format(const polar_sc_config &c)
 {
-    return c.sigmag == 1 && c.par == 16 && c.extended == 1 && c.llr_bits <= 8;
+    return c.sigmag == 1 && c.par == 16 && c.llr_bits <= 8;
+}
+// the datapath the hipcc-built schedule interpreter is compiled for; every other format's
+// interpreter (per-op monitor, fallbacks) is compiled by hipRTC with its POLAR_* switches
+bool builtin_format(const polar_sc_config &c)
+{
+    return c.sigmag == 1 && c.par == 16 && c.extended == 1 && c.llr_bits == 6;
 }
 
 bool tuning_valid(const polar_sc_tuning &t)
@@ -514,7 +522,7 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, DevMode 
             *out = &st;
             return 0;
         }
-        if ((p->jit || p->pair) && interp && p->cfg.llr_bits != 6) {   // traced plan: hipRTC interpreter at POLAR_Q
+        if ((p->jit || p->pair) && interp && !builtin_format(p->cfg)) {   // traced plan: hipRTC interpreter of its format
             const int rc = polar_host::jit_load_interp(*p, st);
             if (rc) return rc;
         }
@@ -624,8 +632,8 @@ int trace_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size_
     if (!rc) {
         if (p->hybrid) {
             rc = polar_host::jit_launch_hybrid(*p, *st, llr, out, (long)batch, out_stride, wpg, nullptr, dtrace);
-        } else if ((p->jit || p->pair) && p->cfg.llr_bits != 6) {
-            // per-mask plan at another LLR_BITS: the hipRTC interpreter of its POLAR_Q
+        } else if ((p->jit || p->pair) && !builtin_format(p->cfg)) {
+            // per-mask / pair plan of another format: the hipRTC interpreter of its POLAR_* switches
             if (wpg > polar_host::HYBRID_MAX_WAVES) wpg = polar_host::HYBRID_MAX_WAVES;
             rc = polar_host::launch_interp_fn(st->ifn_trace, *p, *st, llr, out, (long)batch, out_stride, wpg, nullptr,
                                               dtrace);
@@ -802,10 +810,12 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // subtree decoders of sub_words words, default 64 / 128). polar_sc_tuning.kernel = 1
     // selects the plain schedule interpreter for every N.
     const bool jit_on = t.kernel != 1;
-    // PRUNING_LEVEL 1 leaf decoders other than the plain leaf run on the interpreter only
+    // PRUNING_LEVEL 1 leaf decoders: the 16-LLR REP / SPC / REP2 / SPC2 leaves run in the
+    // generated kernels too (leaf_gen); the PAR-word decoders of PAR > 16 (OP_PLEAF) and the
+    // CA2 R1 leaf on the interpreter only
     bool kinds = false;
     for (const polar_sc_op &o : p->ops)
-        if (((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && ((o.fb >> 16) & 7u)) ||
+        if (((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && ((o.fb >> 16) & 7u) > POLAR_LEAF_SPC2) ||
             o.code == polar_host::POLAR_OP_PLEAF)
             kinds = true;
     const bool dflt = default_format(c);
@@ -903,7 +913,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         s.n_sub_calls = sc.calls;
     } else {
         dev_sched = p->ops;
-        if (!p->jit && (c.llr_bits != 6 || !dflt)) {
+        if (!p->jit && !builtin_format(c)) {
             // the hipcc-built interpreter is the shipped datapath; other formats run the same
             // interpreter compiled by hipRTC with their POLAR_* switches (a hybrid kernel
             // without subtrees)

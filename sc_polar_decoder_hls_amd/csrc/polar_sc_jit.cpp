@@ -310,7 +310,7 @@ struct Gen {
                   << ")), GSAT2);\n"
                   << "    const u32 S_ = plane_mask<0>(" << P(sd, 1) << ") ^ (xm_ & ~pk_sra(d_, 15));\n";
             }
-            o << "    const u32 x_ = leaf_ms<0x" << std::hex << op.fb << std::dec << "u, 0, 16>(M_, S_, ln);\n";
+            o << "    const u32 x_ = leaf_gen<0x" << std::hex << (op.fb & 0x7FFFFu) << std::dec << "u>(M_, S_, ln);\n";
             put_mask(op.pos, 1, "x_");
             o << "  }\n";
             if (f) clobber_parent(sd, 1);
@@ -463,8 +463,9 @@ struct Gen {
         const int wpb = MASK_WPB;
         presplit = true;
         pack = G >= 2;
-        o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits
-          << "\n#include \"polar_sc_device.h\"\nusing namespace polar;\n"
+        o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits << "\n"
+          << (p.cfg.extended ? "" : "#define POLAR_EXT 0\n")   // EXTENDED = 0: saturating leaves
+          << "#include \"polar_sc_device.h\"\nusing namespace polar;\n"
           << "typedef const __attribute__((address_space(1))) void *gas_t;\n"
           << "typedef __attribute__((address_space(3))) void *las_t;\n"
           << "extern \"C\" __global__ void __launch_bounds__(" << 64 * wpb << ", " << MASK_MIN_WAVES
@@ -653,14 +654,35 @@ uint64_t source_key(const std::string &src)
 
 }  // namespace
 
+// Identity of the machine code a plan runs: FNV-1a over the executable sections and .rodata
+// (the kernel descriptors) of its compiled code object. Two code objects with equal
+// instructions and descriptors get the same key whatever the source text they came from
+// (hipRTC names a module-unique symbol after the source, so the whole file differs);
+// profiles record it and bench.py reuses their counters only for the same machine code.
 uint64_t code_key(const polar_sc_plan &p)
 {
-    if (!p.jit && !p.hybrid && !p.pair) return 0;
-    try {
-        return source_key(jit_source(p));
-    } catch (const std::exception &) {
+    const std::vector<char> &code = p.jit_code;
+    if ((!p.jit && !p.hybrid && !p.pair) || code.size() < sizeof(Elf64_Ehdr) ||
+        std::memcmp(code.data(), ELFMAG, SELFMAG) != 0)
         return 0;
+    Elf64_Ehdr eh;
+    std::memcpy(&eh, code.data(), sizeof eh);
+    if (eh.e_ident[EI_CLASS] != ELFCLASS64 || eh.e_shentsize != sizeof(Elf64_Shdr) || eh.e_shstrndx >= eh.e_shnum ||
+        eh.e_shoff + (uint64_t)eh.e_shnum * sizeof(Elf64_Shdr) > code.size())
+        return 0;
+    std::vector<Elf64_Shdr> sh(eh.e_shnum);
+    std::memcpy(sh.data(), code.data() + eh.e_shoff, sh.size() * sizeof(Elf64_Shdr));
+    const Elf64_Shdr &names = sh[eh.e_shstrndx];
+    uint64_t h = 1469598103934665603ull;
+    for (const Elf64_Shdr &s : sh) {
+        if (s.sh_type != SHT_PROGBITS || s.sh_offset + s.sh_size > code.size() || s.sh_name >= names.sh_size ||
+            names.sh_offset + names.sh_size > code.size())
+            continue;
+        const char *nm = code.data() + names.sh_offset + s.sh_name;
+        if ((s.sh_flags & SHF_EXECINSTR) || std::strncmp(nm, ".rodata", names.sh_size - s.sh_name) == 0)
+            h = fnv1a(h, code.data() + s.sh_offset, s.sh_size);
     }
+    return h;
 }
 
 namespace {

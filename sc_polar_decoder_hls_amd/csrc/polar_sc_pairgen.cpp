@@ -299,7 +299,7 @@ struct PairGen {
                                          : "    const u32 M_ = pk_min(bsel(xm_, pk_abs_i16(d_), pk_add(m_.a, m_.b)), GSAT2);\n")
                   << "    const u32 S_ = plane_mask<0>(s_.b) ^ (xm_ & ~pk_sra(d_, 15));\n";
             }
-            o << "    " << x << " = leaf_ms<0x" << std::hex << (op.fb & 0xFFFFu) << std::dec << "u, 0, 16>(M_, S_, ln);\n  }\n";
+            o << "    " << x << " = leaf_gen<0x" << std::hex << (op.fb & 0x7FFFFu) << std::dec << "u>(M_, S_, ln);\n  }\n";
             small1[op.pos] = x;
             break;
         }
@@ -528,7 +528,8 @@ std::string pair_source(const polar_sc_plan &p)
 {
     std::ostringstream o;
     o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits << "\n#define POLAR_LPAR " << (p.cfg.par == 64 ? 6 : 4)
-      << "\n#include \"polar_sc_pair.h\"\n"
+      << "\n" << (p.cfg.extended ? "" : "#define POLAR_EXT 0\n")   // EXTENDED = 0: saturating leaves
+      << "#include \"polar_sc_pair.h\"\n"
       << "namespace polar {\n" << kPairCH;
     int lg = 0;
     while ((1 << lg) < p.sub_words) lg++;

@@ -179,5 +179,5 @@ int fit_waves(int regs, int W);
 void code_regs(const polar_sc_plan &p, int &regs, int &regs_seg);
 constexpr int MASK_WAVES_PER_BLOCK = 4;   // per-mask kernel launch (polar_sc_jit.cpp MASK_WPB)
 PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, int regs_seg);
-uint64_t code_key(const polar_sc_plan &p);   // rtc cache key of the plan's generated source (0: none)
+uint64_t code_key(const polar_sc_plan &p);   // hash of the compiled kernels' instructions + descriptors (0: none)
 }  // namespace polar_host

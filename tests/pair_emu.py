@@ -303,6 +303,13 @@ def leaf_ms(FB, B, W, M, S, ln):
     return bsel(ln.a[H], xa ^ xorlane(H, xb), xb)
 
 
+def leaf_gen(FB, M, S, ln):
+    """polar_sc_device.h leaf_gen: the plain leaf (PRUNING_LEVEL 1 decoders are not emulated)."""
+    if (FB >> 16) & 7:
+        raise NotImplementedError("PRUNING_LEVEL 1 leaf decoders")
+    return leaf_ms(FB & 0xFFFF, 0, 16, M, S, ln)
+
+
 def sm8_pair(l, h):
     l, h = V(l).astype(np.int64), V(h).astype(np.int64)
     b0, b1 = l & 0xFF, h & 0xFF

@@ -9,24 +9,12 @@ import numpy as np
 import pytest
 
 import util
-from sc_polar_decoder_hls_amd._plansets import FORMATS   # (par, sigmag, extended, llr_bits); build() prewarms them
+# FORMATS: (par, sigmag, extended, llr_bits); build() prewarms every plan decoded here
+from sc_polar_decoder_hls_amd._plansets import FORMATS, FORMAT_C7 as CONFIGS, format_seed, planted_mask, \
+    PRUNING_SWEEP
 from test_gpu_parity import _assert_same
 
 pytestmark = pytest.mark.gpu
-
-CONFIGS = ((2, 1, 1, 1, 0, 0, 1), (1, 1, 1, 1, 1, 1, 0), (0, 0, 0, 0, 0, 0, 0), (2, 1, 1, 1, 1, 1, 0))
-
-
-def _planted_mask(rng, N, par):
-    """Random mask with PAR groups of every pruned class (R0 / R1 / REP / SPC / REP2 / SPC2)."""
-    all1 = (1 << par) - 1
-    pats = [0, all1, 1 << (par - 1), all1 & ~1, 3 << (par - 2), all1 & ~3]
-    mask = (rng.random(N) < 0.5).astype(np.uint8)
-    for g in range(N // par):
-        if rng.random() < 0.6:
-            p = int(rng.choice(pats))
-            mask[par * g:par * g + par] = [(p >> k) & 1 for k in range(par)]
-    return mask
 
 
 def _decoder(pkg, mask, fmt, c7):
@@ -40,9 +28,9 @@ def _decoder(pkg, mask, fmt, c7):
 @pytest.mark.parametrize("fmt", FORMATS, ids=lambda f: "p%d_%s_e%d_q%d" % (f[0], "sm" if f[1] else "ca2", f[2], f[3]))
 def test_formats_vs_oracle(pkg, cuda, oracle_mod, fmt):
     par, sigmag, ext, q = fmt
-    rng = np.random.default_rng(par * 7 + sigmag * 3 + ext + q * 11)
+    rng = np.random.default_rng(format_seed(fmt))
     amp = (1 << (q - 1)) - 1
-    masks = [("FB_N1024_K512", util.mask("FB_N1024_K512")), ("planted_4096", _planted_mask(rng, 4096, par)),
+    masks = [("FB_N1024_K512", util.mask("FB_N1024_K512")), ("planted_4096", planted_mask(rng, 4096, par)),
              ("frozen_n_16384_k_8192", util.mask("frozen_n_16384_k_8192"))]
     for name, mask in masks:
         B = 24 if mask.size <= 4096 else 9
@@ -58,6 +46,8 @@ def test_formats_vs_oracle(pkg, cuda, oracle_mod, fmt):
             got = pkg.unpack_bits(out.cpu().numpy(), mask.size)
             ref = oracle_mod.decode_fsm(mask, llr, config=c7, llr_bits=q, par=par, sigmag=sigmag, extended=ext)
             _assert_same(got, ref, "%s fmt %s cfg %s storage %d" % (name, fmt, c7, dec.stats["storage"]))
+            if par == 16 and sigmag == 1 and q <= 8:   # EXTENDED 0: the generated kernels
+                assert dec.stats["kernel"] in (1, 3), (name, fmt, c7, dec.stats["kernel"])
 
 
 @pytest.mark.parametrize("q", [6, 9])
@@ -132,6 +122,22 @@ def test_script_tests_pruning_sweep(pkg, cuda, oracle_mod, par):
         cuda.cuda.synchronize()
         got = pkg.unpack_bits(out.cpu().numpy(), mask.size)
         _assert_same(got, oracle_mod.decode_fsm(mask, llr, config=c7, llr_bits=8, par=par), "PAR %d %s" % (par, c7))
+
+
+def test_script_tests_pruning_sweep_pair_kernel(pkg, cuda, oracle_mod):
+    """The same loop at PAR 16 on the kernel the plans select by default: the generated pair
+    kernel for every configuration, PRUNING_LEVEL 1's REP / SPC / REP2 / SPC2 leaves included."""
+    mask = util.mask("frozen_n_32768_k_29492")
+    awgn, _ = util.synth_frames(mask, 8, ebn0_db=3.5, seed=16)
+    llr = np.clip(awgn.astype(np.int32) * 4, -127, 127).astype(np.int8)
+    t = cuda.from_numpy(llr).cuda()
+    for c7 in PRUNING_SWEEP:
+        dec = pkg.Decoder(mask, config=_sweep_cfg(pkg, c7, 16))
+        assert dec.stats["kernel"] == 3, c7
+        out = dec.decode(t)
+        cuda.cuda.synchronize()
+        got = pkg.unpack_bits(out.cpu().numpy(), mask.size)
+        _assert_same(got, oracle_mod.decode_fsm(mask, llr, config=c7, llr_bits=8), "pair %s" % (c7,))
 
 
 @pytest.mark.parametrize("par", [16, 64])

@@ -213,7 +213,9 @@ def test_pair_register_budget(pkg):
             W, regs = info["waves_per_block"], info["regs"]
             assert 0 < regs <= 512 and W >= 1, info
             assert -(-W // 4) * regs <= 512, info
-        meta = {name: (vgpr, wg) for name, vgpr, _, wg in cr.kernels(os.path.join(cache, info["code_key"] + ".co"))}
+        co = cr.find_code(cache, info["code_key"])   # (also checks the key's Python restatement)
+        assert co, info["code_key"]
+        meta = {name: (vgpr, wg) for name, vgpr, _, wg in cr.kernels(co)}
         vgpr, wg = meta["polar_sc_pair_kernel"]
         assert regs == -(-vgpr // 8) * 8, (regs, vgpr)
         assert not cr.over_budget(vgpr, 0, wg)[0]

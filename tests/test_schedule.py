@@ -165,12 +165,14 @@ def test_unsupported_configs(pkg):
     c.par = 64
     with pytest.raises(pkg.PolarError):
         pkg.Decoder(np.ones(64, np.uint8), config=c)
-    for field, val in (("llr_bits", 9), ("par", 64), ("par", 32), ("par", 8), ("par", 4), ("sigmag", 0),
-                       ("extended", 0)):
+    for field, val in (("llr_bits", 9), ("par", 64), ("par", 32), ("par", 8), ("par", 4), ("sigmag", 0)):
         c = pkg.default_config()
         setattr(c, field, val)
         dec = pkg.Decoder(mask, config=c)
         assert dec.stats["kernel"] == 2   # the interpreter compiled for the format
+    c = pkg.default_config()
+    c.extended = 0                        # EXTENDED 0: the per-mask kernel with saturating leaves
+    assert pkg.Decoder(mask, config=c).stats["kernel"] == 1
 
 
 @pytest.mark.parametrize("par", [32, 64])

@@ -32,6 +32,32 @@ def kernels(path):
     return out
 
 
+def code_key(path):
+    """polar_sc_jit.cpp code_key restated: FNV-1a (64-bit) over the PROGBITS sections that are
+    executable or named .rodata, in section order, as 16 hex digits."""
+    import struct
+    data = open(path, "rb").read()
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    names = secs[shstrndx]
+    h = 1469598103934665603
+    for name, typ, flags, _, off, size, *_ in secs:
+        nm = data[names[4] + name:].split(b"\0", 1)[0]
+        if typ == 1 and (flags & 4 or nm == b".rodata"):
+            for b in data[off:off + size]:
+                h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return "%016x" % h
+
+
+def find_code(cache, key):
+    """The code object in `cache` whose machine code has this code_key."""
+    for co in sorted(glob.glob(os.path.join(cache, "*.co")), key=os.path.getmtime, reverse=True):
+        if code_key(co) == key:
+            return co
+    return None
+
+
 def over_budget(vgpr, agpr, wg):
     # unified register file of 512 per lane and SIMD. On gfx90a and later the metadata's
     # .vgpr_count is already the unified total (architected VGPRs padded to 4, then the
