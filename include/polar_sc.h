@@ -100,7 +100,11 @@ typedef struct polar_sc_tuning {
                                  (4 can exceed the register budget of an 8-wave block: the
                                  launch then runs fewer waves per pair, see
                                  polar_sc_plan_launch_info) */
-    int32_t reserved;         /* must be 0 */
+    int32_t sub_inline;       /* pair plans: how the kernel runs its generated subtree
+                                 decoders. 0 = automatic, 1 = as calls (one __noinline__
+                                 function per distinct subtree), 2 = inlined into the kernel
+                                 at every call site (no call frame: no callee-saved register
+                                 stores; longer hipRTC compile) */
 } polar_sc_tuning;
 
 /* Immutable decode plan: N, config, frozen mask, compiled decode schedule and its device

@@ -55,8 +55,8 @@ class polar_sc_config(ctypes.Structure):
 class polar_sc_tuning(ctypes.Structure):
     """Kernel selection / launch shape of a plan (include/polar_sc.h); all 0 = automatic."""
     _fields_ = [(n, ctypes.c_int32) for n in (
-        "kernel", "waves_per_group", "sub_words", "tier_words", "lds_slots", "hybrid_waves", "chain_max")] + [
-        ("reserved", ctypes.c_int32)]
+        "kernel", "waves_per_group", "sub_words", "tier_words", "lds_slots", "hybrid_waves", "chain_max",
+        "sub_inline")]
 
 
 def make_tuning(tuning):
@@ -67,7 +67,7 @@ def make_tuning(tuning):
     for k, v in dict(tuning).items():
         if k == "kernel" and isinstance(v, str):
             v = {"auto": 0, "interp": 1}[v]
-        if k not in [f for f, _ in polar_sc_tuning._fields_ if f != "reserved"]:
+        if k not in [f for f, _ in polar_sc_tuning._fields_]:
             raise KeyError("unknown tuning field %r" % k)
         setattr(t, k, int(v))
     return t

@@ -478,7 +478,7 @@ bool tuning_valid(const polar_sc_tuning &t)
            t.tier_words >= -1 && (t.tier_words <= 0 || pow2(t.tier_words)) &&
            (t.lds_slots == 0 || t.lds_slots == 256 || t.lds_slots == 512 || t.lds_slots == 1024) &&
            (t.hybrid_waves == 0 || t.hybrid_waves == 4 || t.hybrid_waves == 8) && t.chain_max >= 0 &&
-           t.chain_max <= 4 && t.reserved == 0;
+           t.chain_max <= 4 && t.sub_inline >= 0 && t.sub_inline <= 2;
 }
 
 int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }

@@ -390,11 +390,13 @@ struct PairGen {
 
     // subtree decoder `id`: root words from the slot dwords at src_ (rows j, j + 1: CH), partial sums to
     // the pair's bit dwords from local word l0
-    void sub_function(int id)
+    // inl: inlined at its call sites (polar_sc_tuning.sub_inline = 2) instead of a call
+    void sub_function(int id, bool inl)
     {
         const int words = 1 << LG, R = regs(LG), nbw = words / 4 >= 16 ? words / 64 : 1;
         // (plain arguments: a PairCtx passed by reference would live on the private stack)
-        o << "__device__ __noinline__ void polar_psub_" << id << "(const u32 *src_, g_u32 *hb_, int l0)\n{\n"
+        o << "__device__ " << (inl ? "__forceinline__" : "__noinline__") << " void polar_psub_" << id
+          << "(const u32 *src_, g_u32 *hb_, int l0)\n{\n"
           << "  const u32 lane_ = threadIdx.x & 63u;\n  Lanes ln; ln.init(lane_ & 15u);\n"
           << "  struct { u32 row; } c; c.row = lane_ >> 4;\n  u32 bw[" << nbw << "] = {};\n";
         bool split_root = false;   // REP / R1 / SPC children of the root read split root words
@@ -535,7 +537,7 @@ std::string pair_source(const polar_sc_plan &p)
     while ((1 << lg) < p.sub_words) lg++;
     for (size_t id = 0; id < p.subs.size(); id++) {
         PairGen g(p.subs[id], lg);
-        g.sub_function((int)id);
+        g.sub_function((int)id, p.tune.sub_inline == 2);
         o << g.o.str();
     }
     o << "}  // namespace polar\nusing namespace polar;\n";

@@ -42,7 +42,7 @@ def test_tuning_validation_and_no_environment(pkg, monkeypatch):
     m = util.mask("FB_N1024_K512")
     for bad in ({"kernel": 4}, {"waves_per_group": 3}, {"waves_per_group": 32}, {"sub_words": 512},
                 {"tier_words": -2}, {"tier_words": 1000}, {"lds_slots": 300}, {"hybrid_waves": 16},
-                {"chain_max": 5}, {"chain_max": -1}):
+                {"chain_max": 5}, {"chain_max": -1}, {"sub_inline": 3}, {"sub_inline": -1}):
         with pytest.raises(pkg.PolarError) as e:
             pkg.Decoder(m, tuning=bad)
         assert e.value.rc == -22, bad
