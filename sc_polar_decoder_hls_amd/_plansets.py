@@ -98,12 +98,18 @@ def gpu_plans():
     return out
 
 
+PAIR_PARS = (32, 64)   # PAR > 16 on the pair kernel (script_tests.sh:11,124 sweeps 64)
+
+
 def gpu_par64_plans():
-    """(name, mask, config fields, tuning) of the PAR 64 GPU tests and bench entries."""
-    out = [(n, mask(n), {"par": 64}, {"kernel": 3}) for n, _ in PAR64_MASKS]
-    for N in (8192, 32768):
-        for i, m in enumerate(struct_masks(N)[:2]):
-            out += [("struct%d_%d" % (N, i), m, {"par": 64}, {"kernel": 3, "sub_words": sw}) for sw in (64, 256)]
+    """(name, mask, config fields, tuning) of the PAR 32 / 64 pair-kernel GPU tests and bench
+    entries."""
+    out = []
+    for par in PAIR_PARS:
+        out += [(n, mask(n), {"par": par}, {"kernel": 3}) for n, _ in PAR64_MASKS]
+        for N in (8192, 32768):
+            for i, m in enumerate(struct_masks(N)[:2]):
+                out += [("struct%d_%d" % (N, i), m, {"par": par}, {"kernel": 3, "sub_words": sw}) for sw in (64, 256)]
     return out
 
 

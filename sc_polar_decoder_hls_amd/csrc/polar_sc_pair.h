@@ -92,31 +92,45 @@ __device__ __forceinline__ u32 G_split_x(u32 ma, u32 mb, u32 X, u32 &LT)
 }
 
 // PAR 64 (POLAR_LPAR 6): a PAR word is four device words = the four rows of one register of a
-// node (and one slot row); PAR 16: one device word = one row
-constexpr bool PAIR_P64 = LPAR == 6;
-static_assert(LPAR == 4 || LPAR == 6, "pair plans: PAR 16 or 64");
+// node (and one slot row); PAR 32 (5): two device words = rows (0, 1) / (2, 3) of a register;
+// PAR 16: one device word = one row
+constexpr bool PAIR_P64 = LPAR == 6, PAIR_P32 = LPAR == 5;
+static_assert(LPAR >= 4 && LPAR <= 6, "pair plans: PAR 16, 32 or 64");
 __device__ __forceinline__ u32 bitrev2(u32 r) { return ((r & 1u) << 1) | (r >> 1); }
-// SPC key bits below the word index (bits 0..5): the tie order of equal magnitudes inside a
-// register -- PAR 16: (word = row, then bitrev4(position)); PAR 64: bitrev6(position in the PAR
-// word) = (bitrev4(position), then bitrev2(row)) (polar_sc_interp.h spc_key)
+// SPC key bits below the register index (bits 0..5): the tie order of equal magnitudes inside a
+// register -- PAR 16: (word = row, then bitrev4(position)); PAR 32: (PAR word row / 2, then
+// bitrev5(position in it) = (bitrev4(position), row & 1)); PAR 64: bitrev6(position in the PAR
+// word) = (bitrev4(position), then bitrev2(row)) (polar_sc_interp.h spc_word_key / spc_lane_key)
 __device__ __forceinline__ u32 spc_sub(u32 row, const Lanes &ln)
 {
-    return PAIR_P64 ? (ln.br << 2) | bitrev2(row) : (row << 4) | ln.br;
+    if constexpr (PAIR_P64) return (ln.br << 2) | bitrev2(row);
+    else if constexpr (PAIR_P32) return ((row >> 1) << 5) | (ln.br << 1) | (row & 1u);
+    else return (row << 4) | ln.br;
+}
+// the same for a node of two words (row r holds word r & 1): PAR 16 two PAR words, PAR 32 one
+__device__ __forceinline__ u32 spc_sub2(u32 row, const Lanes &ln)
+{
+    return PAIR_P32 ? (ln.br << 1) | (row & 1u) : ((row & 1u) << 4) | ln.br;
 }
 // REP accumulation of one register's four row totals (row_sum_biased values, +8192 per half):
-// PAR 16 -- four PAR words in order (word 4 i + row); PAR 64 -- one PAR word, its exact total
+// PAR 16 -- four PAR words in order (word 4 i + row); PAR 32 -- two PAR words, the exact totals
+// of rows (0, 1) and (2, 3); PAR 64 -- one PAR word, its exact total
 __device__ __forceinline__ u32 rep_acc_rows(u32 acc, u32 t0, u32 t1, u32 t2, u32 t3)
 {
     if constexpr (PAIR_P64) {
         const u32 t = pk_sub(pk_add(pk_add(t0, t1), pk_add(t2, t3)), 0x60006000u);   // 4 x 8192 -> 8192
         return rep_acc(acc, t);
+    } else if constexpr (PAIR_P32) {
+        acc = rep_acc(acc, pk_sub(pk_add(t0, t1), 0x20002000u));                      // 2 x 8192 -> 8192
+        return rep_acc(acc, pk_sub(pk_add(t2, t3), 0x20002000u));
     } else {
         return rep_acc(rep_acc(rep_acc(rep_acc(acc, t0), t1), t2), t3);
     }
 }
 // the exact SM chain (rep_any_zero fallback) over one register: SM16 per lane v (row r = word
 // 4 i + r) -> the ADD_TREE of each PAR word (PAR 64: words (0, 2), (1, 3), then the halves,
-// then the positions -- rep_add_tree's order), accumulated with the REP clamp
+// then the positions; PAR 32: words (0, 1), then the positions -- rep_add_tree's order),
+// accumulated with the REP clamp
 __device__ __forceinline__ u32 rep_sm_rows(u32 acc, u32 v, const Lanes &ln)
 {
     if constexpr (PAIR_P64) {
@@ -124,12 +138,37 @@ __device__ __forceinline__ u32 rep_sm_rows(u32 acc, u32 v, const Lanes &ln)
         const u32 v1 = G_sm<0>(q.a, q.b, 0u);
         const X2 r = swap16(v1);
         return G_sm<REPSAT>(row_add_tree(G_sm<0>(r.a, r.b, 0u), ln), acc, 0u);
+    } else if constexpr (PAIR_P32) {
+        const X2 q = swap16(v);
+        const X4 t = rows4(row_add_tree(G_sm<0>(q.a, q.b, 0u), ln));
+        acc = G_sm<REPSAT>(t.t0, acc, 0u);
+        return G_sm<REPSAT>(t.t2, acc, 0u);
     } else {
         const X4 t = rows4(row_add_tree(v, ln));
         acc = G_sm<REPSAT>(t.t0, acc, 0u);
         acc = G_sm<REPSAT>(t.t1, acc, 0u);
         acc = G_sm<REPSAT>(t.t2, acc, 0u);
         return G_sm<REPSAT>(t.t3, acc, 0u);
+    }
+}
+
+// REP of a node of two words (row r holds word r & 1): the biased row sums t -> accumulator
+// (PAR 16: two PAR words in order; PAR 32: one PAR word, its exact total)
+__device__ __forceinline__ u32 rep2_acc(u32 t)
+{
+    const X2 q = swap16(t);
+    if constexpr (PAIR_P32) return rep_acc(0u, pk_sub(pk_add(q.a, q.b), 0x20002000u));
+    else return rep_acc(rep_acc(0u, q.a), q.b);
+}
+// its exact SM chain from the SM16 word per lane
+__device__ __forceinline__ u32 rep2_sm(u32 v, const Lanes &ln)
+{
+    if constexpr (PAIR_P32) {
+        const X2 r = swap16(v);
+        return G_sm<REPSAT>(row_add_tree(G_sm<0>(r.a, r.b, 0u), ln), 0u, 0u);
+    } else {
+        const X2 r = swap16(row_add_tree(v, ln));
+        return G_sm<REPSAT>(r.b, G_sm<REPSAT>(r.a, 0u, 0u), 0u);
     }
 }
 

@@ -308,11 +308,12 @@ struct PairGen {
             o << "  u32 " << x << ";\n  { // REP n " << n << "\n    const X2 m_ = " << sw << "(" << M(pd, 0)
               << "), s_ = " << sw << "(s" << pd << "[0]);\n    const u32 FS_ = s_.a ^ s_.b;\n"
               << "    const u32 t_ = row_sum_biased(F_split_biased<0>(m_.a, m_.b, FS_));\n";
+            // (2 words: two PAR 16 words in order, or one PAR 32 word -- rep2_acc / rep2_sm)
             if (n == 1) o << "    u32 acc_ = rep_acc(0u, t_);\n";
-            else o << "    const X2 q_ = swap16(t_);\n    u32 acc_ = rep_acc(rep_acc(0u, q_.a), q_.b);\n";
-            o << "    if (rep_any_zero(acc_)) {\n      const u32 e_ = row_add_tree(F_split_sm<0>(m_.a, m_.b, FS_), ln);\n";
-            if (n == 1) o << "      acc_ = G_sm<REPSAT>(e_, 0u, 0u);\n";
-            else o << "      const X2 r_ = swap16(e_);\n      acc_ = G_sm<REPSAT>(r_.b, G_sm<REPSAT>(r_.a, 0u, 0u), 0u);\n";
+            else o << "    u32 acc_ = rep2_acc(t_);\n";
+            o << "    if (rep_any_zero(acc_)) {\n";
+            if (n == 1) o << "      acc_ = G_sm<REPSAT>(row_add_tree(F_split_sm<0>(m_.a, m_.b, FS_), ln), 0u, 0u);\n";
+            else o << "      acc_ = rep2_sm(F_split_sm<0>(m_.a, m_.b, FS_), ln);\n";
             o << "    }\n    " << x << " = pk_sra(acc_, 15);\n  }\n";
             (n == 1 ? small1 : small2)[op.pos] = x;
             break;
@@ -331,17 +332,18 @@ struct PairGen {
                 o << "    const u32 l_ = G_split<0>(m_.a, m_.b, X_, LT_);\n"
                   << "    const u32 h_ = plane_mask<0>(s_.b ^ (X_ & ~LT_));\n"
                   << "    u32 par_ = row_xor(h_);\n";
-                const std::string wk = n == 1 ? "0u" : "((c.row & 1u) << 4)";
-                o << "    u32 klo_ = row_min_u32(((l_ & 0xFFu) << 24) | " << wk << " | ln.br);\n"
-                  << "    u32 khi_ = row_min_u32((((l_ >> 16) & 0xFFu) << 24) | " << wk << " | ln.br);\n";
+                // key bits below the magnitude: bitrev4(position), and for 2 words the word
+                // (PAR 16: above it; PAR 32: below it, spc_sub2)
+                const std::string wk = n == 1 ? "ln.br" : "spc_sub2(c.row, ln)";
+                o << "    u32 klo_ = row_min_u32(((l_ & 0xFFu) << 24) | " << wk << ");\n"
+                  << "    u32 khi_ = row_min_u32((((l_ >> 16) & 0xFFu) << 24) | " << wk << ");\n";
                 if (n == 2)
                     o << "    { const X2 p_ = swap16(par_); par_ = p_.a ^ p_.b;\n"
                          "      const X2 a_ = swap16(klo_), b_ = swap16(khi_);\n"
                          "      klo_ = __builtin_elementwise_min(a_.a, a_.b); khi_ = __builtin_elementwise_min(b_.a, b_.b); }\n";
-                const std::string wsel_lo = n == 1 ? "true" : "((klo_ >> 4) & 1u) == (c.row & 1u)";
-                const std::string wsel_hi = n == 1 ? "true" : "((khi_ >> 4) & 1u) == (c.row & 1u)";
-                o << "    const bool flo_ = land(land(par_ & 0x8000u, (klo_ & 15u) == ln.br), " << wsel_lo << ");\n"
-                  << "    const bool fhi_ = land(land(par_ & 0x80000000u, (khi_ & 15u) == ln.br), " << wsel_hi << ");\n"
+                const std::string kb = n == 1 ? "15u" : "31u";
+                o << "    const bool flo_ = land(par_ & 0x8000u, (klo_ & " << kb << ") == " << wk << ");\n"
+                  << "    const bool fhi_ = land(par_ & 0x80000000u, (khi_ & " << kb << ") == " << wk << ");\n"
                   << "    " << x << " = h_ ^ sel(flo_, 0xFFFFu, 0u) ^ sel(fhi_, 0xFFFF0000u, 0u);\n  }\n";
             }
             (n == 1 ? small1 : small2)[op.pos] = x;
@@ -529,7 +531,8 @@ void pair_kernel(std::ostringstream &o, const char *name, const std::vector<pola
 std::string pair_source(const polar_sc_plan &p)
 {
     std::ostringstream o;
-    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits << "\n#define POLAR_LPAR " << (p.cfg.par == 64 ? 6 : 4)
+    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits << "\n#define POLAR_LPAR "
+      << (p.cfg.par == 64 ? 6 : p.cfg.par == 32 ? 5 : 4)
       << "\n" << (p.cfg.extended ? "" : "#define POLAR_EXT 0\n")   // EXTENDED = 0: saturating leaves
       << "#include \"polar_sc_pair.h\"\n"
       << "namespace polar {\n" << kPairCH;

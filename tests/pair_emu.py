@@ -197,6 +197,21 @@ def rep_sm_rows(acc, v, ln):
     return acc
 
 
+def spc_sub2(row, ln):
+    """two-word nodes, PAR 16: (row & 1, bitrev4(position))"""
+    return ((V(row) & 1) << 4) | ln.br
+
+
+def rep2_acc(t):
+    q = swap16(t)
+    return rep_acc(rep_acc(V(0), q.a), q.b)
+
+
+def rep2_sm(v, ln):
+    r = swap16(row_add_tree(v, ln))
+    return G_sm(REPSAT, r.b, G_sm(REPSAT, r.a, 0, 0), 0)
+
+
 def F_split_biased(I, ma, mb, FS):
     m, s = pk_min(ma, mb), plane_mask(I, FS)
     return pk_add(pk_sub(m ^ s, s), 0x02000200)

@@ -19,7 +19,7 @@ def pair(pkg, mask, **tuning):
 
 
 # the plan lists live in the package's build tooling (build() compiles them ahead)
-from sc_polar_decoder_hls_amd._plansets import (PAR64_MASKS, PARITY_MASKS, gpu_par64_plans, gpu_plans,  # noqa: F401
+from sc_polar_decoder_hls_amd._plansets import (PAR64_MASKS, PAIR_PARS, PARITY_MASKS, gpu_par64_plans, gpu_plans,  # noqa: F401
                                                 struct_masks, struct_sub_words, structured_mask, wave_mask)
 
 
@@ -234,9 +234,9 @@ def test_forced_kernel_errors(pkg):
     assert pkg.Decoder(util.mask("frozen_n_8192_k_4096"), tuning={"kernel": 2, "sub_words": 128}).stats["kernel"] == 2
 
 
-def par64_config(pkg, q=6):
+def par64_config(pkg, q=6, par=64):
     c = pkg.default_config()
-    c.par, c.llr_bits = 64, q
+    c.par, c.llr_bits = par, q
     return c
 
 
@@ -248,34 +248,39 @@ def test_pair_par64_plan(pkg):
     assert (s["kernel"], s["sub_words"]) == (3, 256) and s["n_sub_calls"] > 0
     src = d.kernel_source()
     assert "#define POLAR_LPAR 6" in src and "G_split_x" in src
+    d = pkg.Decoder(util.mask("frozen_n_65536_k_32768"), config=par64_config(pkg, par=32))
+    assert d.stats["kernel"] == 3 and "#define POLAR_LPAR 5" in d.kernel_source()
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("par", PAIR_PARS)
 @pytest.mark.parametrize("name,batch", PAR64_MASKS)
-def test_pair_par64_parity(pkg, cuda, oracle_mod, name, batch):
-    """PAR 64 on the pair kernel against the oracle's literal FSM at PAR 64: REP over the PAR
-    word's exact ADD_TREE (words (0, 2), (1, 3), halves, positions) with the 2^(Q+5)-1 clamp,
-    SPC ties by (PAR word, bitrev6(position)), G_extended inside the PAR word."""
+def test_pair_par64_parity(pkg, cuda, oracle_mod, name, batch, par):
+    """PAR 32 / 64 on the pair kernel against the oracle's literal FSM at that PAR: REP over the
+    PAR word's exact ADD_TREE (PAR 64: words (0, 2), (1, 3), halves, positions; PAR 32: words
+    (0, 1), positions) with the 2^(Q+LPAR-1)-1 clamp, SPC ties by (PAR word, bitrev_LPAR
+    (position)), G_extended inside the PAR word."""
     mask = util.mask(name)
     llr, _ = util.synth_frames(mask, batch, ebn0_db=1.0, seed=batch)
     edge = np.random.default_rng(batch).choice(np.array([0, 0, 1, -1, 31, -31, -32, 5], np.int8), size=(2, mask.size))
     llr = np.concatenate([llr, edge])
-    dec = pkg.Decoder(mask, config=par64_config(pkg))
+    dec = pkg.Decoder(mask, config=par64_config(pkg, par=par))
     assert dec.stats["kernel"] == 3
-    _assert_same(run(pkg, cuda, dec, llr), oracle_mod.decode_fsm(mask, llr, par=64), "PAR 64 " + name)
+    _assert_same(run(pkg, cuda, dec, llr), oracle_mod.decode_fsm(mask, llr, par=par), "PAR %d %s" % (par, name))
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("par", PAIR_PARS)
 @pytest.mark.parametrize("N", [8192, 32768])
-def test_pair_par64_structured(pkg, cuda, oracle_mod, N):
-    """PAR 64 on structured masks (R0 / R1 / REP / SPC nodes of every size), subtrees of 64
-    and 256 words, AWGN and edge LLRs."""
+def test_pair_par64_structured(pkg, cuda, oracle_mod, N, par):
+    """PAR 32 / 64 on structured masks (R0 / R1 / REP / SPC nodes of every size), subtrees of
+    64 and 256 words, AWGN and edge LLRs."""
     rng = np.random.default_rng(N + 64)
     for rep, mask in enumerate(struct_masks(N)[:2]):
         llr, _ = util.synth_frames(mask, 4, ebn0_db=0.5, seed=rep)
         edge = rng.choice(np.array([0, 0, 1, -1, 31, -31, -32, 5], np.int8), size=(3, N))
         llr = np.concatenate([llr, edge])
-        ref = oracle_mod.decode_fsm(mask, llr, par=64)
+        ref = oracle_mod.decode_fsm(mask, llr, par=par)
         for sw in (64, 256):
-            dec = pkg.Decoder(mask, config=par64_config(pkg), tuning={"kernel": 3, "sub_words": sw})
-            _assert_same(run(pkg, cuda, dec, llr), ref, "PAR 64 N=%d rep %d S=%d" % (N, rep, sw))
+            dec = pkg.Decoder(mask, config=par64_config(pkg, par=par), tuning={"kernel": 3, "sub_words": sw})
+            _assert_same(run(pkg, cuda, dec, llr), ref, "PAR %d N=%d rep %d S=%d" % (par, N, rep, sw))
