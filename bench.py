@@ -32,10 +32,10 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # bytes they report (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
 # roofline.traffic when the benchmarked (mask, frames per GPU) is the profiled one.
 TRAFFIC_PROFILES = {
-    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r04_v2_c2_pmc.json"),
-    ("frozen_n_65536_k_32768", 4096): os.path.join(ROOT, "profiles", "r04_v2_c3_pmc.json"),
-    ("frozen_n_262144_k_131072", 512): os.path.join(ROOT, "profiles", "r04_v2_c5_pmc.json"),
-    ("frozen_n_262144_k_131072", 64): os.path.join(ROOT, "profiles", "r04_v2_c5b64_pmc.json"),
+    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r04_v6_c2_pmc.json"),
+    ("frozen_n_65536_k_32768", 4096): os.path.join(ROOT, "profiles", "r04_v6_c3_pmc.json"),
+    ("frozen_n_262144_k_131072", 512): os.path.join(ROOT, "profiles", "r04_v6_c5_pmc.json"),
+    ("frozen_n_262144_k_131072", 64): os.path.join(ROOT, "profiles", "r04_v6_c5b64_pmc.json"),
 }
 # Rotated input: the timed loop cycles through distinct resident batches of at least this
 # many bytes in total, so the LLR reads come from HBM and not from the 256 MB Infinity Cache
