@@ -4,6 +4,7 @@ The shared library is the product: HIP kernels (csrc/polar_sc_kernels.hip) + hos
 schedule compiler / C ABI (csrc/polar_sc_host.cpp) behind include/polar_sc.h.
 """
 import os
+import shutil
 import subprocess
 import sys
 
@@ -67,7 +68,12 @@ def build(force=False, verbose=False):
         with open(os.path.join(GEN_DIR, inc), "w") as f:
             f.write("static const char " + name + "[] = R\"POLARSRC(" + src + ")POLARSRC\";\n")
     tmp = LIB + ".tmp.%d" % os.getpid()
+    # the ROCm clang driver next to this hipcc: whole-module compiles of generated kernels
+    # (polar_sc_jit.cpp offline_compile)
+    hc = shutil.which(hipcc()) or hipcc()
+    clang = os.path.join(os.path.dirname(os.path.dirname(os.path.realpath(hc))), "lib", "llvm", "bin", "clang++")
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           '-DPOLAR_ROCM_CLANG="%s"' % clang,
            "-I" + os.path.join(ROOT, "include"), "-I" + GEN_DIR] + SOURCES + ["-o", tmp, "-lhiprtc"]
     if verbose:
         print(" ".join(cmd))

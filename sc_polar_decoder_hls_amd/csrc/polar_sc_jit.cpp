@@ -15,9 +15,14 @@
 
 #include <hip/hiprtc.h>
 
+#include <dirent.h>
 #include <dlfcn.h>
 #include <elf.h>
+#include <fcntl.h>
+#include <spawn.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
+extern char **environ;   // (POSIX: the environment handed to the spawned compiler)
 #include <utime.h>
 #include <unistd.h>
 
@@ -728,8 +733,108 @@ void cache_store(const std::string &path, const std::vector<char> &code)
     if (std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
 }
 
-int rtc_compile(const std::string &src, std::vector<char> &code, std::string &log)
+// ---- generated kernels compiled by the ROCm toolchain's clang driver ----------------------
+// hipRTC is resolved by soname, and a process that imported torch first (the Python package
+// does, to share torch's HIP runtime) gets torch's bundled hipRTC / comgr, an older LLVM than
+// the system ROCm's. Its code is worse for these kernels: the pair kernel's noinline subtree
+// decoders and slot loops get a 128-VGPR budget plus AGPR spill slots (86 AGPRs, ~3000
+// accvgpr moves at C5; the system ROCm 7.2 compiler: 248 VGPRs, no AGPRs), and the per-mask
+// kernel 0.75 % fewer VALU but slower code. Same sources, same box, cache files swapped
+// (profiles/r04_ab/compiler_ab.txt): C2 70.75 / 70.76 vs 71.99 / 71.93 us, C3 0.876 / 0.867 vs
+// 0.902 / 0.907 ms, the C5 64-frame share 1.326 / 1.328 vs 1.362 / 1.360 ms. So every generated
+// kernel is compiled by the clang driver of the toolchain the library was built with (a child
+// process, its own cache key), when it exists and this process has no GPU open (a compile after
+// the GPU runtime started is left to hipRTC; prewarmed plans never compile at decode time).
+bool gpu_open()
 {
+    DIR *d = opendir("/proc/self/fd");
+    if (!d) return true;
+    bool open = false;
+    char path[64], target[64];
+    while (dirent *e = readdir(d)) {
+        std::snprintf(path, sizeof path, "/proc/self/fd/%s", e->d_name);
+        const ssize_t n = readlink(path, target, sizeof target - 1);
+        if (n <= 0) continue;
+        target[n] = 0;
+        if (std::strcmp(target, "/dev/kfd") == 0) open = true;
+    }
+    closedir(d);
+    return open;
+}
+
+// the ROCm clang driver of the toolchain this library was built with (_build.py defines the
+// path); "" when it is not installed here
+std::string rocm_clang()
+{
+#ifdef POLAR_ROCM_CLANG
+    if (access(POLAR_ROCM_CLANG, X_OK) == 0) return POLAR_ROCM_CLANG;
+#endif
+    return "";
+}
+
+bool write_file(const std::string &path, const char *data, size_t n)
+{
+    std::ofstream f(path, std::ios::binary);
+    f.write(data, (std::streamsize)n);
+    return (bool)f;
+}
+
+int offline_compile(const std::string &src, std::vector<char> &code, std::string &log)
+{
+    const std::string clang = rocm_clang();
+    if (clang.empty() || gpu_open()) return -ENOENT;
+    char tmpl[] = "/tmp/polar_sc_rtc_XXXXXX";
+    if (!mkdtemp(tmpl)) return -EIO;
+    const std::string dir = tmpl, in = dir + "/k.hip", out = dir + "/k.co", lg = dir + "/log";
+    const std::string text = "#include <hip/hip_runtime.h>\n" + src;
+    bool ok = write_file(in, text.data(), text.size()) &&
+              write_file(dir + "/polar_sc_device.h", kPolarDeviceSrc, sizeof kPolarDeviceSrc - 1) &&
+              write_file(dir + "/polar_sc_pair.h", kPolarPairSrc, sizeof kPolarPairSrc - 1) &&
+              write_file(dir + "/polar_sc_interp.h", kPolarInterpSrc, sizeof kPolarInterpSrc - 1);
+    int rc = -EIO;
+    if (ok) {
+        const std::string inc = "-I" + dir;
+        const char *argv[] = {clang.c_str(), "-x", "hip", "--offload-arch=gfx950", "--cuda-device-only",
+                              "--no-gpu-bundle-output", "-O3", "-std=c++17", "-w", inc.c_str(), "-c", "-o",
+                              out.c_str(), in.c_str(), nullptr};
+        posix_spawn_file_actions_t fa;
+        posix_spawn_file_actions_init(&fa);
+        posix_spawn_file_actions_addopen(&fa, 1, lg.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        posix_spawn_file_actions_adddup2(&fa, 1, 2);
+        pid_t pid;
+        if (posix_spawn(&pid, clang.c_str(), &fa, nullptr, (char *const *)argv, environ) == 0) {
+            int status = 0;
+            if (waitpid(pid, &status, 0) == pid && WIFEXITED(status) && WEXITSTATUS(status) == 0) {
+                std::ifstream f(out, std::ios::binary);
+                std::vector<char> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+                if (buf.size() >= 4 && std::memcmp(buf.data(), "\x7f" "ELF", 4) == 0) {
+                    code.swap(buf);
+                    rc = 0;
+                }
+            }
+        }
+        posix_spawn_file_actions_destroy(&fa);
+        std::ifstream lf(lg);
+        log.assign((std::istreambuf_iterator<char>(lf)), std::istreambuf_iterator<char>());
+    }
+    for (const char *f : {"/k.hip", "/k.co", "/log", "/polar_sc_device.h", "/polar_sc_pair.h", "/polar_sc_interp.h"})
+        std::remove((dir + f).c_str());
+    rmdir(dir.c_str());
+    return rc;
+}
+
+// whole: a generated kernel source (compiled by the clang driver when available, under its own
+// cache key); otherwise, and for the interpreter sources, hipRTC
+int rtc_compile(const std::string &src, std::vector<char> &code, std::string &log, bool whole = false)
+{
+    if (whole) {
+        const std::string opath = cache_path(src + "\n// offline clang driver\n");
+        if (cache_load(opath, code)) return 0;
+        if (offline_compile(src, code, log) == 0) {
+            cache_store(opath, code);
+            return 0;
+        }
+    }
     const std::string cpath = cache_path(src);
     if (cache_load(cpath, code)) return 0;
     hiprtcProgram prog;
@@ -780,7 +885,7 @@ int jit_compile(const polar_sc_plan &p)
         p.jit_log = e.what();
         return -ENOTSUP;
     }
-    return rtc_compile(src, p.jit_code, p.jit_log);
+    return rtc_compile(src, p.jit_code, p.jit_log, true);
 }
 
 // Per-mask plans whose LLR_BITS is not the hipcc-built 6: the per-op monitor runs the schedule
