@@ -32,10 +32,10 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # bytes they report (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
 # roofline.traffic when the benchmarked (mask, frames per GPU) is the profiled one.
 TRAFFIC_PROFILES = {
-    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r04_v6_c2_pmc.json"),
-    ("frozen_n_65536_k_32768", 4096): os.path.join(ROOT, "profiles", "r04_v6_c3_pmc.json"),
-    ("frozen_n_262144_k_131072", 512): os.path.join(ROOT, "profiles", "r04_v6_c5_pmc.json"),
-    ("frozen_n_262144_k_131072", 64): os.path.join(ROOT, "profiles", "r04_v6_c5b64_pmc.json"),
+    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r04_v8_c2_pmc.json"),
+    ("frozen_n_65536_k_32768", 4096): os.path.join(ROOT, "profiles", "r04_v8_c3_pmc.json"),
+    ("frozen_n_262144_k_131072", 512): os.path.join(ROOT, "profiles", "r04_v8_c5_pmc.json"),
+    ("frozen_n_262144_k_131072", 64): os.path.join(ROOT, "profiles", "r04_v8_c5b64_pmc.json"),
 }
 # Rotated input: the timed loop cycles through distinct resident batches of at least this
 # many bytes in total, so the LLR reads come from HBM and not from the 256 MB Infinity Cache
@@ -66,16 +66,16 @@ CONFIGS = {
 def kernel_name(stats):
     """The kernel that carries the decode of a plan (polar_sc_plan_stats.kernel / .storage)."""
     if stats["kernel"] == 1:
-        return "polar_sc_mask_kernel (per-mask hipRTC kernel)"
+        return "polar_sc_mask_kernel (per-mask generated kernel)"
     if stats["kernel"] == 3:
-        k = ("polar_sc_pair_kernel (hipRTC: one frame pair per wave, %d generated %d-LLR subtree decoders, "
+        k = ("polar_sc_pair_kernel (generated: one frame pair per wave, %d generated %d-LLR subtree decoders, "
              "upper levels over stage-slot rows)" % (stats["n_sub_kinds"], 16 * stats["sub_words"]))
         if stats.get("tier_steps"):
             k += " + grid tier (%d launches per decode)" % stats["tier_steps"]
         return k
     store = "HBM-scratch" if stats["storage"] == 1 else "LDS"
     if stats["kernel"] == 2:
-        k = ("polar_sc_hybrid_kernel (hipRTC: %s interpreter + %d generated %d-LLR subtree decoders)"
+        k = ("polar_sc_hybrid_kernel (generated: %s interpreter + %d generated %d-LLR subtree decoders)"
              % (store, stats["n_sub_kinds"], 16 * stats["sub_words"]))
         if stats.get("tier_steps"):
             k = ("grid tier: polar_sc_tier_kernel (upper-level F / G over all frame groups) + segments of "
