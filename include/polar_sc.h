@@ -45,7 +45,7 @@ extern "C" {
  *   * par 4, 8, 16, 32 or 64 (script_tests.sh:11 runs 16 and 64, script_RTL_sim.sh 4..64).
  * The shipped datapath (sigmag 1, par 16, llr_bits <= 8; either extended, every pruning level
  * and elag combination) runs the generated kernels, and so do PAR 32 and 64 (sigmag 1,
- * extended 1, llr_bits <= 8, pruning_level 0 / 2) for N >= 2048; every other format runs the schedule
+ * either extended, llr_bits <= 8, pruning_level 0 / 2) for N >= 2048; every other format runs the schedule
  * interpreter compiled for it. elag_rare = 1
  * (does not compile in the reference, my_module.h:255 vs :1511) is rejected with -ENOTSUP.
  */

@@ -334,7 +334,7 @@ class Decoder:
                 for o in arr]
 
     def compile(self):
-        """Build the per-mask kernel now (host-only hipRTC); False if the plan uses the
+        """Build the plan's generated kernel now (host only); False if the plan uses the
         schedule interpreter instead."""
         rc = lib().polar_sc_plan_compile(self._plan)
         if rc == -95:

@@ -122,7 +122,7 @@ def cpu_test_plans():
 # ---- datapath formats (tests/test_gpu_formats.py): (PAR, SIGMAG, EXTENDED, LLR_BITS) ---------
 FORMATS = [
     (16, 0, 1, 6), (16, 0, 1, 8), (16, 0, 0, 6), (16, 1, 0, 6), (16, 1, 1, 9), (16, 0, 1, 9),
-    (32, 1, 1, 6), (32, 0, 1, 6), (64, 1, 1, 6), (64, 1, 1, 8), (64, 0, 1, 6), (64, 1, 0, 6), (64, 0, 0, 8),
+    (32, 1, 1, 6), (32, 0, 1, 6), (32, 1, 0, 8), (64, 1, 1, 6), (64, 1, 1, 8), (64, 0, 1, 6), (64, 1, 0, 6), (64, 0, 0, 8),
     (64, 1, 1, 9),
     # PAR 4 / 8 (script_RTL_sim.sh:97-330): PAR words as lane groups of a device word
     (8, 1, 1, 6), (8, 0, 1, 6), (8, 1, 0, 8), (8, 1, 1, 8), (4, 1, 1, 6), (4, 0, 0, 8), (4, 1, 1, 8),

@@ -819,9 +819,10 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
             o.code == polar_host::POLAR_OP_PLEAF)
             kinds = true;
     const bool dflt = default_format(c);
-    // pair plans also take PAR 64 (the PAR word = one register of four device words; the host
-    // expands its leaf into F / G_extended / 16-LLR leaf records, par_expand)
-    const bool pair_fmt = dflt || ((c.par == 32 || c.par == 64) && c.sigmag == 1 && c.extended == 1 && c.llr_bits <= 8);
+    // pair plans also take PAR 32 / 64 (the PAR word = one register of two / four device words;
+    // the host expands its leaf into F / G / 16-LLR leaf records, par_expand: G_extended when
+    // EXTENDED, the saturating G and POLAR_EXT 0 leaves when not)
+    const bool pair_fmt = dflt || ((c.par == 32 || c.par == 64) && c.sigmag == 1 && c.llr_bits <= 8);
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR
     // level's F / G / H then run inside the straight-line code instead of as interpreter ops

@@ -779,7 +779,19 @@ bool write_file(const std::string &path, const char *data, size_t n)
     return (bool)f;
 }
 
-int offline_compile(const std::string &src, std::vector<char> &code, std::string &log)
+// POLAR_SC_CLANG_FLAGS: extra clang driver arguments (whitespace separated) for compiler A/Bs;
+// part of the cache key, and never satisfied by hipRTC
+std::vector<std::string> extra_clang_flags()
+{
+    std::vector<std::string> out;
+    const char *e = getenv("POLAR_SC_CLANG_FLAGS");
+    std::istringstream in(e ? e : "");
+    for (std::string w; in >> w;) out.push_back(w);
+    return out;
+}
+
+int offline_compile(const std::string &src, std::vector<char> &code, std::string &log,
+                    const std::vector<std::string> &extra)
 {
     const std::string clang = rocm_clang();
     if (clang.empty() || gpu_open()) return -ENOENT;
@@ -794,15 +806,17 @@ int offline_compile(const std::string &src, std::vector<char> &code, std::string
     int rc = -EIO;
     if (ok) {
         const std::string inc = "-I" + dir;
-        const char *argv[] = {clang.c_str(), "-x", "hip", "--offload-arch=gfx950", "--cuda-device-only",
-                              "--no-gpu-bundle-output", "-O3", "-std=c++17", "-w", inc.c_str(), "-c", "-o",
-                              out.c_str(), in.c_str(), nullptr};
+        std::vector<const char *> argv = {clang.c_str(), "-x", "hip", "--offload-arch=gfx950", "--cuda-device-only",
+                                          "--no-gpu-bundle-output", "-O3", "-std=c++17", "-w", inc.c_str()};
+        for (const std::string &w : extra) argv.push_back(w.c_str());
+        for (const char *w : {"-c", "-o", out.c_str(), in.c_str()}) argv.push_back(w);
+        argv.push_back(nullptr);
         posix_spawn_file_actions_t fa;
         posix_spawn_file_actions_init(&fa);
         posix_spawn_file_actions_addopen(&fa, 1, lg.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
         posix_spawn_file_actions_adddup2(&fa, 1, 2);
         pid_t pid;
-        if (posix_spawn(&pid, clang.c_str(), &fa, nullptr, (char *const *)argv, environ) == 0) {
+        if (posix_spawn(&pid, clang.c_str(), &fa, nullptr, (char *const *)argv.data(), environ) == 0) {
             int status = 0;
             if (waitpid(pid, &status, 0) == pid && WIFEXITED(status) && WEXITSTATUS(status) == 0) {
                 std::ifstream f(out, std::ios::binary);
@@ -828,11 +842,18 @@ int offline_compile(const std::string &src, std::vector<char> &code, std::string
 int rtc_compile(const std::string &src, std::vector<char> &code, std::string &log, bool whole = false)
 {
     if (whole) {
-        const std::string opath = cache_path(src + "\n// offline clang driver\n");
+        const std::vector<std::string> extra = extra_clang_flags();
+        std::string key = src + "\n// offline clang driver\n";
+        for (const std::string &w : extra) key += "// " + w + "\n";
+        const std::string opath = cache_path(key);
         if (cache_load(opath, code)) return 0;
-        if (offline_compile(src, code, log) == 0) {
+        if (offline_compile(src, code, log, extra) == 0) {
             cache_store(opath, code);
             return 0;
+        }
+        if (!extra.empty()) {
+            log += "POLAR_SC_CLANG_FLAGS set: no cached object and no clang driver to build one\n";
+            return -EIO;
         }
     }
     const std::string cpath = cache_path(src);
