@@ -62,7 +62,9 @@ def test_tuning_validation_and_no_environment(pkg, monkeypatch):
     txt = open(os.path.join(util.ROOT, "sc_polar_decoder_hls_amd", "csrc", "polar_sc_host.cpp")).read()
     assert re.findall(r'getenv\("(\w+)"\)', txt) == ["POLAR_SC_VERBOSE"]   # error detail on stderr only
     txt = open(os.path.join(util.ROOT, "sc_polar_decoder_hls_amd", "csrc", "polar_sc_jit.cpp")).read()
-    assert re.findall(r'getenv\("(\w+)"\)', txt) == ["POLAR_SC_RTC_CACHE"]
+    # the cache directory, and extra clang flags for compiler A/Bs (part of the cache key, so the
+    # machine code -- and polar_sc_plan_launch_info's code_key -- says which flags built it)
+    assert sorted(re.findall(r'getenv\("(\w+)"\)', txt)) == ["POLAR_SC_CLANG_FLAGS", "POLAR_SC_RTC_CACHE"]
 
 
 def test_default_config_is_reference(pkg):
