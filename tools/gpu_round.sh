@@ -6,6 +6,9 @@
 #   prof    -- per config: kernel-trace stats, FETCH_SIZE and WRITE_SIZE (separate passes, the
 #              gfx950 PMC slot limits), two SQ passes; tools/prof_decode.py records the launch
 #              shape and code-object key each profile is of (bench.py reads traffic only for it)
+#   benchprof -- bench.py itself under rocprofv3 --kernel-trace --stats, one config per run
+#              (C2, C3, C5, C5 share; no secondary entries, so each trace holds one decode
+#              kernel): the trace average next to the HIP-event kernel_ms of the same command
 #   stamps  -- per-op s_memtime stamps of the pair kernels built by tools/pair_stamps.py
 # usage: bash tools/gpu_round.sh <tag> <step> [<step> ...]
 set -euo pipefail
@@ -45,6 +48,16 @@ for step in "$@"; do
       set -- $c
       mkdir -p "$OUT/$1"
       prof "$1" "$2" "$3" "$4"
+    done ;;
+  benchprof)
+    for c in "c2 --config c2" "c3 --config c3" "c5 --config c5" "c5b64 --config c5 --batch 64"; do
+      set -- $c
+      name=$1; shift
+      ( cd /tmp && export TMPDIR=/tmp &&
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/bench_$name" -o trace --output-format csv -- \
+          python3 "$ROOT/bench.py" --no-secondary --no-ebn0-sweep --no-cpu-baseline "$@" \
+          > "$OUT/bench_$name.json" 2> "$OUT/bench_$name.err" )
+      echo "bench $name traced"
     done ;;
   stamps)
     for b in "$ROOT"/build_tools/pair_stamps_*; do
