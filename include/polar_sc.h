@@ -267,7 +267,8 @@ int polar_sc_plan_get_schedule(const polar_sc_plan *plan, polar_sc_op *ops, uint
                                uint32_t *count);
 
 /* Per-mask kernel (plans with stats.storage == 2, N <= 1024): generate its HIP source and
- * compile it for gfx950 with hipRTC now (host only, no GPU needed); otherwise it is built
+ * compile it for gfx950 now (host only, no GPU needed: the ROCm clang driver, or hipRTC when
+ * the driver is absent or the process has a GPU open); otherwise it is built
  * on the first decode. -ENOTSUP for plans that use the hipcc-built schedule interpreter
  * (polar_sc_tuning.kernel = 1). */
 int polar_sc_plan_compile(const polar_sc_plan *plan);
@@ -276,7 +277,7 @@ int polar_sc_plan_compile(const polar_sc_plan *plan);
 int polar_sc_plan_kernel_source(const polar_sc_plan *plan, char *buf, size_t cap, size_t *len);
 
 /* Launch shape a polar_sc_decode of `batch` frames would use on a device with `cus` compute
- * units (0 = 256, MI355X), computed on the host (compiles the generated kernel with hipRTC if
+ * units (0 = 256, MI355X), computed on the host (compiles the generated kernel if
  * needed; no GPU). The waves of a block must fit the 512 registers per SIMD lane that they
  * share (VGPRs + AGPRs, from the code object's kernel descriptor); the decode lowers its
  * waves per frame group / pair until they do, and returns -ENOTSUP when not even one wave
