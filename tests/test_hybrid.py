@@ -110,6 +110,20 @@ def test_llr_bits_kernels_compile(pkg, q):
         dec.compile()
 
 
+def test_clang_flags_knob(pkg, monkeypatch):
+    """POLAR_SC_CLANG_FLAGS (compiler A/Bs) reaches the clang driver and keys the code-object
+    cache: a valid flag builds a code object of its own, an invalid one fails the compile
+    instead of falling back to hipRTC (which would ignore it)."""
+    mask = util.mask("FB_N128_K64")
+    base = pkg.Decoder(mask).launch_info(1)["code_key"]
+    monkeypatch.setenv("POLAR_SC_CLANG_FLAGS", "-mllvm --amdgpu-schedule-metric-bias=0")
+    dec = pkg.Decoder(mask)
+    assert dec.compile() and dec.launch_info(1)["code_key"] == base   # same code, own cache entry
+    monkeypatch.setenv("POLAR_SC_CLANG_FLAGS", "-fno-such-clang-flag")
+    with pytest.raises(pkg.PolarError):
+        pkg.Decoder(mask).compile()
+
+
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sub_words", [2, 4, 8, 16, 32, 64])
