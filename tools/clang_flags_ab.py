@@ -29,12 +29,12 @@ CONFIGS = {"c2": ("FB_N1024_K512", 65536), "c3": ("frozen_n_65536_k_32768", 4096
            "c5": ("frozen_n_262144_k_131072", 512), "c5_64": ("frozen_n_262144_k_131072", 64)}
 
 
-def prewarm(names):
+def prewarm(names, configs):
     import sc_polar_decoder_hls_amd as pkg
     import util
     for v in names:
         os.environ["POLAR_SC_CLANG_FLAGS"] = VARIANTS[v]
-        for c in ("c2", "c3", "c5"):
+        for c in sorted({"c5" if c == "c5_64" else c for c in configs}):
             dec = pkg.Decoder(util.mask(CONFIGS[c][0]))
             ok = dec.compile()
             print(v, c, ok, dec.launch_info(CONFIGS[c][1])["code_key"], flush=True)
@@ -80,7 +80,7 @@ def main():
     ap.add_argument("--configs", default="c2,c3,c5,c5_64")
     args = ap.parse_args()
     if args.prewarm:
-        return prewarm(args.variants.split(","))
+        return prewarm(args.variants.split(","), args.configs.split(","))
     if args.child:
         return child(args.steps, args.configs.split(","))
     for r in range(args.rounds):
