@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define POLAR_SC_ABI_VERSION 3
+#define POLAR_SC_ABI_VERSION 4
 #define POLAR_SC_PAR 16
 
 /*
@@ -105,6 +105,11 @@ typedef struct polar_sc_tuning {
                                  function per distinct subtree), 2 = inlined into the kernel
                                  at every call site (no call frame: no callee-saved register
                                  stores; longer hipRTC compile) */
+    int32_t layout;           /* pair plans: 0 = automatic, 1 = frame pairs (two frames per
+                                 wave in the 16-bit halves, four words per register), 2 = solo
+                                 (one frame per wave, the halves carry words 8 j + 4 h + r:
+                                 eight words per register, half the instructions per frame on
+                                 nodes of >= 16 words; PAR 16 only) */
 } polar_sc_tuning;
 
 /* Immutable decode plan: N, config, frozen mask, compiled decode schedule and its device

@@ -98,6 +98,33 @@ def gpu_plans():
     return out
 
 
+SOLO_SUB_WORDS = (64, 256, 512)
+
+
+def solo_sub_words(N):
+    """solo plans: subtrees of 64 .. 512 words, at most half the code"""
+    return [sw for sw in SOLO_SUB_WORDS if sw <= N // 32]
+
+
+def solo_plans():
+    """(name, mask, tuning) of the solo-layout GPU tests (tests/test_solo.py) and the bench."""
+    t = {"kernel": 3, "layout": 2}
+    out = [(n, mask(n), dict(t)) for n, _ in PARITY_MASKS]
+    for N in (2048, 8192, 32768):
+        for i, m in enumerate(struct_masks(N)):
+            out += [("struct%d_%d" % (N, i), m, dict(t, sub_words=sw)) for sw in solo_sub_words(N)]
+    out += [("frozen_n_2048_k_1024", mask("frozen_n_2048_k_1024"), dict(t, sub_words=64)),
+            ("frozen_n_8192_k_4096", mask("frozen_n_8192_k_4096"), dict(t, sub_words=256)),
+            ("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"), dict(t, sub_words=512)),
+            ("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"), dict(t, sub_words=64)),
+            ("wave_mask", wave_mask(), dict(t, sub_words=64)),
+            ("frozen_n_32768_k_29492", mask("frozen_n_32768_k_29492"), dict(t, tier_words=512, sub_words=128)),
+            ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), dict(t, sub_words=256)),
+            ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), dict(t, sub_words=512)),
+            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(t, sub_words=512))]
+    return out
+
+
 PAIR_PARS = (32, 64)   # PAR > 16 on the pair kernel (script_tests.sh:11,124 sweeps 64)
 
 
@@ -219,7 +246,7 @@ def prewarm_all(verbose=False):
     q8 = pkg.default_config()
     q8.llr_bits = 8
     _build.prewarm({n: mask(n) for n in RATE09_MASKS}, configs=[q8], verbose=verbose)
-    _build.prewarm_plans(gpu_plans() + cpu_test_plans(), verbose=verbose)
+    _build.prewarm_plans(gpu_plans() + solo_plans() + cpu_test_plans(), verbose=verbose)
     _build.prewarm_items(gpu_par64_plans(), verbose=verbose)
     # the pruning / ELAG / format sweeps: PRUNING_LEVEL 1 leaf decoders and EXTENDED 0 run the
     # generated kernels (one code object per mask and configuration); the interpreter formats

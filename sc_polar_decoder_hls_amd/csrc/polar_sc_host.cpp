@@ -474,11 +474,11 @@ bool tuning_valid(const polar_sc_tuning &t)
 {
     auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
     return (t.kernel >= 0 && t.kernel <= 3) && (t.waves_per_group == 0 || (pow2(t.waves_per_group) && t.waves_per_group <= 16)) &&
-           (t.sub_words == 0 || (pow2(t.sub_words) && t.sub_words >= 2 && t.sub_words <= 256)) &&
+           (t.sub_words == 0 || (pow2(t.sub_words) && t.sub_words >= 2 && t.sub_words <= 512)) &&
            t.tier_words >= -1 && (t.tier_words <= 0 || pow2(t.tier_words)) &&
            (t.lds_slots == 0 || t.lds_slots == 256 || t.lds_slots == 512 || t.lds_slots == 1024) &&
            (t.hybrid_waves == 0 || t.hybrid_waves == 4 || t.hybrid_waves == 8) && t.chain_max >= 0 &&
-           t.chain_max <= 4 && t.sub_inline >= 0 && t.sub_inline <= 2;
+           t.chain_max <= 4 && t.sub_inline >= 0 && t.sub_inline <= 2 && t.layout >= 0 && t.layout <= 2;
 }
 
 int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
@@ -553,7 +553,7 @@ int ensure_device(const polar_sc_plan *p, size_t batch, DevState **out, DevMode 
     if (p->gmem || p->pair) {
         size_t waves = (batch + 7) / 8;
         size_t need = p->gmem ? waves * (size_t)p->hbm_group_dwords * 4u : 0u;
-        if (p->pair) need = std::max(need, (batch + 1) / 2 * (size_t)p->pair_dwords * 4u);
+        if (p->pair) need = std::max(need, (p->solo ? batch : (batch + 1) / 2) * (size_t)p->pair_dwords * 4u);
         if (need > st.scratch_bytes) {
             if (st.scratch) {
                 if (hipDeviceSynchronize() != hipSuccess) return -EIO;
@@ -847,17 +847,29 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         delete p;
         return rc;
     }
+    // solo layout (one frame per wave, 8 words per register): PAR 16 only; a forced solo
+    // layout the plan cannot take is an error
+    const bool solo_ok = c.par == 16;
+    if ((t.layout != 0 && !want_pair) || (t.layout == 2 && !solo_ok)) {
+        delete p;
+        return -ENOTSUP;
+    }
+    const bool solo = want_pair && t.layout == 2;
     bool use_pair = false;
     if (want_pair) {
+        const int wpr = solo ? 8 : 4;
         int S = std::min<int>(polar_host::PAIR_SUB_WORDS, (int)p->G / 2);
         if (t.sub_words) {
-            // >= 32 words: the halves of every upper node are whole 8-row slot groups
-            if (t.sub_words < 32 || (uint32_t)t.sub_words > p->G / 2) {
+            // the halves of every upper node are whole 8-row slot groups: >= 32 words (pair),
+            // >= 64 (solo); at most 256 (pair) / 512 (solo) words of register code
+            if (t.sub_words < 8 * wpr || (uint32_t)t.sub_words > p->G / 2 ||
+                t.sub_words > (solo ? polar_host::SOLO_SUB_WORDS_MAX : polar_host::PAIR_SUB_WORDS)) {
                 delete p;
                 return -EINVAL;
             }
             S = t.sub_words;
         }
+        p->solo = solo ? 1 : 0;
         SubCtx sc;
         sc.words = (uint32_t)S;
         compile_node(*p, p->pair_ops, 0, 0, p->GP, true, &sc);
@@ -868,8 +880,8 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         s.sub_words = (uint32_t)S;
         s.n_sub_kinds = (uint32_t)p->subs.size();
         s.n_sub_calls = sc.calls;
-        p->pair_slot_rows = ((int)p->G - S) / 4;
-        p->pair_dwords = p->pair_slot_rows * 32 + (int)(p->G / 64) * 64;
+        p->pair_slot_rows = ((int)p->G - S) / p->wpr();
+        p->pair_dwords = p->pair_slot_rows * 32 + std::max<int>(1, (int)p->G / (16 * p->wpr())) * 64;
         if (t.tier_words > 0) {
             if (t.tier_words <= S) {
                 delete p;
@@ -890,6 +902,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
                 return -ENOTSUP;
             }
             p->pair = 0;
+            p->solo = 0;
             p->sub_words = 0;
             p->subs.clear();
             p->pair_ops.clear();
@@ -961,7 +974,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         s.storage = 1u;
         s.tier_steps = (uint32_t)p->pair_tier.steps.size();
         s.tier_words = (uint32_t)p->pair_tier.tw;
-        s.lds_bytes_per_wave = (uint32_t)p->sub_words / 4u * 128u;
+        s.lds_bytes_per_wave = (uint32_t)(p->sub_words / p->wpr()) * 128u;
         s.scratch_bytes_per_wave = (uint64_t)p->pair_dwords * 4u;
     }
     *out = p;
@@ -1208,6 +1221,8 @@ int polar_sc_plan_launch_info(const polar_sc_plan *p, size_t batch, uint32_t cus
     const int simds = 4 * (int)(cus ? cus : 256u);
     int regs = 0, regs_seg = 0;
     if (p->jit || p->hybrid || p->pair) {
+        // under the plan lock: compile / decode may fill p->jit_code from another thread
+        std::lock_guard<std::mutex> lk(p->mu);
         if (const int rc = polar_host::jit_compile(*p)) return rc;
         polar_host::code_regs(*p, regs, regs_seg);
         if (regs < 0 || regs_seg < 0) return -EIO;   // kernel missing from the code object

@@ -1106,7 +1106,7 @@ int launch_tier(const polar_sc_plan &p, const DevState &st, const int8_t *llr, u
 PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, int regs_seg)
 {
     PairShape sh;
-    sh.pairs = (batch + 1) / 2;
+    sh.pairs = p.solo ? batch : (batch + 1) / 2;   // blocks: frame pairs, or frames (solo)
     const long cus = simds > 0 ? simds / 4 : 256;
     int W = p.tune.waves_per_group;
     if (W == 0) {
@@ -1120,22 +1120,24 @@ PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, in
     sh.W = W;
     if (W == 0) return sh;
     const long per_cu = (sh.pairs + cus - 1) / cus;
-    // LDS: levels of nodes S .. L words (32 (2 L - S) bytes) + the SPC exchange (3 W rows of 256 B)
+    // LDS: levels of nodes S .. L words ((2 L - S) / wpr slot rows of 128 B) + the SPC exchange
+    // (3 W rows of 256 B)
     const long budget = CU_LDS_BYTES / (per_cu > 0 ? per_cu : 1) - 3l * W * 256l;
-    const int S = p.sub_words, G = (int)p.G;
+    const int S = p.sub_words, G = (int)p.G, wpr = p.wpr();
+    const long bpw = 128 / wpr;   // slot bytes per word
     int L = 0;
     for (int w = S; w <= G / 2; w *= 2) {
         if (tier && w >= p.pair_tier.tw) break;
-        if (32l * (2l * w - S) <= budget) L = w;
+        if (bpw * (2l * w - S) <= budget) L = w;
     }
     // polar_sc_tuning.lds_slots: the levels of nodes up to this many words in LDS whatever
     // the batch (fewer pairs then fit a CU: the A/B of keeping more levels on chip)
     if (const int want = p.tune.lds_slots) {
         L = 0;
         for (int w = S; w <= G / 2 && w <= want; w *= 2)
-            if (!(tier && w >= p.pair_tier.tw) && 32l * (2l * w - S) + 3l * W * 256l <= CU_LDS_BYTES) L = w;
+            if (!(tier && w >= p.pair_tier.tw) && bpw * (2l * w - S) + 3l * W * 256l <= CU_LDS_BYTES) L = w;
     }
-    const int lds_rows = L ? (2 * L - S) / 4 : 0;
+    const int lds_rows = L ? (2 * L - S) / wpr : 0;
     sh.lds_row0 = p.pair_slot_rows - lds_rows;
     sh.lds = (unsigned)(lds_rows * 128 + 3 * W * 256);
     return sh;
@@ -1161,8 +1163,8 @@ int jit_launch_pair(const polar_sc_plan &p, const DevState &st, const int8_t *ll
     for (const TierStep &t : p.pair_tier.steps) {
         hipError_t e;
         if (t.grid) {
-            int g = t.op.code == POLAR_OP_G ? 1 : 0, k = t.op.level, n4 = t.op.n / 4;
-            int ub = t.op.upos >= 0 ? t.op.upos / 4 : -1;
+            int g = t.op.code == POLAR_OP_G ? 1 : 0, k = t.op.level, n4 = t.op.n / p.wpr();
+            int ub = t.op.upos >= 0 ? t.op.upos / p.wpr() : -1;
             const long waves = pairs * (long)((n4 + cw - 1) / cw);
             void *args[] = {(void *)&llr, (void *)&scratch, (void *)&N, (void *)&b, (void *)&pd, (void *)&sr,
                             (void *)&g, (void *)&k, (void *)&n4, (void *)&ub, (void *)&cw};

@@ -27,11 +27,35 @@
 //     contiguous (16 B per lane, 1 KB per group of 8 rows: one dwordx4 / b128 access per lane);
 //     levels of nodes <= lds_words words sit in LDS, wider ones in HBM scratch. The upper F / G run on those four bytes at once (SWAR
 //     below) while two magnitudes fit 7 bits (Q <= 7).
+//
+// Solo layout (POLAR_SOLO 1, polar_sc_tuning.layout = 2): ONE frame per wave. The two 16-bit
+// halves carry the two interleaved halves of the frame's nodes instead of two frames: register
+// j of a node of w >= 8 words has word 8 j + 4 h + r in row r, half h. For nodes of >= 16 words
+// F / G / H / R1 pair word 8 j + 4 h + r with 8 (j + w / 16) + 4 h + r -- same row, same half --
+// so every loop below runs unchanged on "virtual frames" h of half the words (G = N / 32
+// virtual words per half); an op on a node of n words is n / 8 instructions instead of n / 4.
+// Only REP and SPC combine the halves (word order / tie order across h), and the channel rows
+// (real words 8 j + 4 h + r: 128-byte row stride, half h at + 64) and the output differ.
+// Nodes of 8 words and below are handled in the generated subtree code (polar_sc_pairgen.cpp).
 #pragma once
 
 #include "polar_sc_device.h"
 
+#ifndef POLAR_SOLO
+#define POLAR_SOLO 0
+#endif
+
 namespace polar {
+
+constexpr bool PAIR_SOLO = POLAR_SOLO != 0;
+// bytes between channel rows j and j + 1 of one (virtual) frame
+constexpr unsigned ROWB = PAIR_SOLO ? 128u : 64u;
+
+// rotate the 16-bit halves (solo: the other half of the frame's node, lane-local)
+__device__ __forceinline__ u32 hswap(u32 x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+// the low / high half in both halves
+__device__ __forceinline__ u32 bcast_lo(u32 x) { return __builtin_amdgcn_perm(x, x, 0x01000100u); }
+__device__ __forceinline__ u32 bcast_hi(u32 x) { return __builtin_amdgcn_perm(x, x, 0x03020302u); }
 
 typedef unsigned short u16;
 typedef __attribute__((address_space(3))) u16 lds_u16;
@@ -150,6 +174,31 @@ __device__ __forceinline__ u32 rep_sm_rows(u32 acc, u32 v, const Lanes &ln)
         acc = G_sm<REPSAT>(t.t2, acc, 0u);
         return G_sm<REPSAT>(t.t3, acc, 0u);
     }
+}
+
+// Solo layout: the REP chain of one register's words in order -- half 0 (words 8 j + r), then
+// half 1 (8 j + 4 + r); the accumulator is the low half (the high half is don't-care)
+__device__ __forceinline__ u32 rep_acc_solo(u32 acc, u32 t0, u32 t1, u32 t2, u32 t3)
+{
+    acc = rep_acc(rep_acc(rep_acc(rep_acc(acc, t0), t1), t2), t3);
+    return rep_acc(rep_acc(rep_acc(rep_acc(acc, t0 >> 16), t1 >> 16), t2 >> 16), t3 >> 16);
+}
+__device__ __forceinline__ u32 rep_sm_solo(u32 acc, u32 v, const Lanes &ln)
+{
+    const X4 t = rows4(row_add_tree(v, ln));
+    acc = G_sm<REPSAT>(t.t0, acc, 0u);
+    acc = G_sm<REPSAT>(t.t1, acc, 0u);
+    acc = G_sm<REPSAT>(t.t2, acc, 0u);
+    acc = G_sm<REPSAT>(t.t3, acc, 0u);
+    acc = G_sm<REPSAT>(t.t0 >> 16, acc, 0u);
+    acc = G_sm<REPSAT>(t.t1 >> 16, acc, 0u);
+    acc = G_sm<REPSAT>(t.t2 >> 16, acc, 0u);
+    return G_sm<REPSAT>(t.t3 >> 16, acc, 0u);
+}
+// true if the (low-half) accumulator of some lane is zero
+__device__ __forceinline__ bool rep_any_zero_lo(u32 acc)
+{
+    return __builtin_amdgcn_ballot_w64((acc & 0xFFFFu) == 0u) != 0ull;
 }
 
 // REP of a node of two words (row r holds word r & 1): the biased row sums t -> accumulator
@@ -323,8 +372,8 @@ struct PairCtx {
     // channel rows j, j + 1 (j even) as a slot dword (wrapper_in + qconv_format)
     __device__ __forceinline__ u32 chan2(int j) const
     {
-        const u32 lo = (u32)chl[64 * j] | ((u32)chl[64 * j + 64] << 8);
-        const u32 hi = (u32)chh[64 * j] | ((u32)chh[64 * j + 64] << 8);
+        const u32 lo = (u32)chl[ROWB * j] | ((u32)chl[ROWB * j + ROWB] << 8);
+        const u32 hi = (u32)chh[ROWB * j] | ((u32)chh[ROWB * j + ROWB] << 8);
         const u32 raw = lo | (hi << 16);
         if constexpr (PAIR_SWAR) return conv4(raw);
         else return ppack(conv_pair(raw & 0x00FF00FFu), conv_pair((raw >> 8) & 0x00FF00FFu));
@@ -372,7 +421,7 @@ __device__ __forceinline__ ChanQ chan_quad(const PairCtx &c)
     // chl = frame lo + 16 row + pos; chh - chl = (hi frame - lo frame) N (uniform)
     q.base = uniform_ptr(c.chl - (16u * (lane >> 4) + lane_pos(pl)));
     const u32 dhi = __builtin_amdgcn_readfirstlane((u32)(c.chh - c.chl));
-    q.off = 16u * (lane >> 4) + (pl & ~3u) + 64u * (k & 1u) + ((k & 2u) ? dhi : 0u);
+    q.off = 16u * (lane >> 4) + (pl & ~3u) + ROWB * (k & 1u) + ((k & 2u) ? dhi : 0u);
     q.sel.init(pl);
     q.al = ((u32)(unsigned long)q.base & 3u) == 0u;
     return q;
@@ -389,7 +438,7 @@ __device__ __forceinline__ u32x4 chan8a(const ChanQ &q, int j)
     u32 raw[4];
 #pragma unroll
     for (int t = 0; t < 4; t++)   // rows j + 2 t, + 1: words 4 (j + 2 t) + r (+ 4)
-        raw[t] = *(const g_u32 *)(q.base + (64u * (u32)(j + 2 * t) + q.off));
+        raw[t] = *(const g_u32 *)(q.base + (ROWB * (u32)(j + 2 * t) + q.off));
     u32x4 r;
 #pragma unroll
     for (int t = 0; t < 4; t++) r[t] = chan_conv(quad_transpose(raw[t], q));
@@ -695,19 +744,24 @@ __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int 
         for (int o = 0; o < 2; o++) {
             const u32 lam = F_sm(prow(a, o), prow(b, o)), sg = pk_sra(lam, 15);
             const X4 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
-            acc = rep_acc_rows(acc, t.t0, t.t1, t.t2, t.t3);
+            if constexpr (PAIR_SOLO) acc = rep_acc_solo(acc, t.t0, t.t1, t.t2, t.t3);
+            else acc = rep_acc_rows(acc, t.t0, t.t1, t.t2, t.t3);
         }
     }
-    if (rep_any_zero(acc)) {
+    if (PAIR_SOLO ? rep_any_zero_lo(acc) : rep_any_zero(acc)) {
         const Lanes ln = c.lanes();
         acc = 0;
         for (int j = 0; j < n4; j += 2) {
             u32 a, b;
             psrc2<ROOT, SL>(c, s0, n4, j, a, b);
 #pragma unroll
-            for (int o = 0; o < 2; o++) acc = rep_sm_rows(acc, F_sm(prow(a, o), prow(b, o)), ln);
+            for (int o = 0; o < 2; o++) {
+                if constexpr (PAIR_SOLO) acc = rep_sm_solo(acc, F_sm(prow(a, o), prow(b, o)), ln);
+                else acc = rep_sm_rows(acc, F_sm(prow(a, o), prow(b, o)), ln);
+            }
         }
     }
+    if constexpr (PAIR_SOLO) acc = bcast_lo(acc);   // one frame: both halves of the node
     const u32 full = pk_sra(acc, 15);   // two's complement or SM16: the decision is bit 15 / 31
     for (int l = 0; l < n4; l += 16) pbits_put(c, l0 + l, n4 - l < 16 ? n4 - l : 16, full);
 }
@@ -747,7 +801,13 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
             pbits_put(c, first, l0 + j + 1 - first, acc);
             acc = 0;
         }
-        if constexpr (SPC) {
+        if constexpr (SPC && PAIR_SOLO) {
+            // (word 8 j + 4 h + r, position) order: half 1 keys carry bit 6
+            par ^= h;
+            const u32 wk = ((u32)j << 7) | ksub;
+            klo = __builtin_elementwise_min(klo, ((lam & 0xFFu) << 24) | wk);
+            khi = __builtin_elementwise_min(khi, (((lam >> 16) & 0xFFu) << 24) | wk | 64u);
+        } else if constexpr (SPC) {
             par ^= h;
             const u32 wk = ((u32)j << 6) | ksub;   // (word, position) order
             klo = __builtin_elementwise_min(klo, ((lam & 0xFFu) << 24) | wk);
@@ -786,6 +846,15 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
                 klo = __builtin_elementwise_min(klo, (u32)x[(3 * w + 1) * 64]);
                 khi = __builtin_elementwise_min(khi, (u32)x[(3 * w + 2) * 64]);
             }
+        }
+        if constexpr (PAIR_SOLO) {
+            // one frame: the parity of both halves, the first minimum of both
+            const u32 k = __builtin_elementwise_min(klo, khi);
+            if (((par ^ (par << 16)) & 0x80000000u) && (k & 63u) == ksub) {
+                const int l = l0 + (int)((k >> 7) & 0x1FFFFu);
+                c.bst(l >> 4, c.bld(l >> 4) ^ (((k & 64u) ? 0x10000u : 1u) << (l & 15)));
+            }
+            return;
         }
         // the flipped word: 4 (key >> 6) + ((key >> 4) & 3), position bitrev4^-1(key & 15)
         const bool flo = (par & 0x8000u) && (klo & 63u) == ksub;
@@ -852,12 +921,20 @@ __device__ __noinline__ void pair_out(PairCtx c, g_u16 *o_lo, g_u16 *o_hi, bool 
     const int e0 = (nd * c.wi) / c.W, e1 = (nd * (c.wi + 1)) / c.W;
     for (int d = e0; d < e1; d++) {
         const u32 t = row_transpose16(to_position_order(c.bld(d), ln), ln);
-        const int w = 4 * (16 * d + (int)ln.pl) + row;
-        if (st_lo) o_lo[w] = (unsigned short)(t & 0xFFFFu);
-        if (st_hi) o_hi[w] = (unsigned short)(t >> 16);
+        if constexpr (PAIR_SOLO) {   // half h of local word l, row r: word 8 l + 4 h + r
+            const int w = 8 * (16 * d + (int)ln.pl) + row;
+            if (st_lo) {
+                o_lo[w] = (unsigned short)(t & 0xFFFFu);
+                o_lo[w + 4] = (unsigned short)(t >> 16);
+            }
+        } else {
+            const int w = 4 * (16 * d + (int)ln.pl) + row;
+            if (st_lo) o_lo[w] = (unsigned short)(t & 0xFFFFu);
+            if (st_hi) o_hi[w] = (unsigned short)(t >> 16);
+        }
     }
     if (c.lead())
-        for (int w = c.G + (int)ln.pl + 16 * row; w < out_stride; w += 64) {   // pad words
+        for (int w = (PAIR_SOLO ? 2 : 1) * c.G + (int)ln.pl + 16 * row; w < out_stride; w += 64) {   // pad words
             if (st_lo) o_lo[w] = 0;
             if (st_hi) o_hi[w] = 0;
         }
@@ -870,15 +947,15 @@ __device__ __forceinline__ bool pair_init(PairCtx &c, const signed char *llr, un
                                           lds_w32 *lbase)
 {
     const int lane = threadIdx.x & 63;
-    c.G = N >> 4;
+    c.G = PAIR_SOLO ? N >> 5 : N >> 4;   // (solo: virtual words per half)
     c.wi = wi;
     c.W = W;
     c.lds_row0 = lds_row0;
-    const long f_lo = 2 * pair, f_hi = 2 * pair + 1;
+    const long f_lo = PAIR_SOLO ? pair : 2 * pair, f_hi = 2 * pair + 1;
     const long fl = f_lo < batch ? f_lo : (long)batch - 1, fh = f_hi < batch ? f_hi : (long)batch - 1;
     const int off = 16 * (int)c.row() + (int)c.lanes().pos;
     c.chl = (const g_u8 *)llr + fl * (long)N + off;
-    c.chh = (const g_u8 *)llr + fh * (long)N + off;
+    c.chh = PAIR_SOLO ? c.chl + 64 : (const g_u8 *)llr + fh * (long)N + off;   // (solo: words 8 j + 4 + r)
     g_u32 *base = (g_u32 *)scratch + pair * (long)pair_dwords;
     c.hs = base + 4 * lane;
     c.hb = base + (slot_rows >> 1) * 64 + lane;   // slot_rows x 128 B = slot_rows / 2 dword rows
@@ -897,7 +974,7 @@ __device__ __forceinline__ void pair_tier_body(const signed char *llr, unsigned 
     const int chunks = (n4 + cw - 1) / cw;
     const long pair = wave / chunks;
     const int j = wave - (int)pair * chunks;
-    if (2 * pair >= batch) return;
+    if ((PAIR_SOLO ? pair : 2 * pair) >= batch) return;
     PairCtx c;
     pair_init(c, llr, scratch, N, batch, pair, pair_dwords, slot_rows, slot_rows, 0, 1, nullptr);
     const int j0 = j * cw, j1 = j0 + cw < n4 ? j0 + cw : n4;

@@ -28,13 +28,20 @@ struct PairGen {
     const std::vector<polar_sc_op> &ops;   // subtree schedule, levels / positions relative to its root
     std::ostringstream o;
     int LG;                                // the subtree root has 2^LG words
+    // solo layout (polar_sc_pair.h POLAR_SOLO): one frame per wave, a register of a node of
+    // >= 8 words holds words 8 j + 4 h + r (half h, row r); nodes of 4 words and below are
+    // replicated in both halves, so their ops are the pair code's
+    bool solo;
+    int wpr;                               // words per register of the lane-private nodes: 4 / 8
     std::map<int, std::string> small1;     // result masks of 1-word nodes, by word position
     std::map<int, std::string> small2;     // result masks of 2-word nodes (row r: word r & 1)
     int nvar = 0;
 
-    PairGen(const std::vector<polar_sc_op> &ops_, int lg) : ops(ops_), LG(lg) {}
+    PairGen(const std::vector<polar_sc_op> &ops_, int lg, bool solo_ = false)
+        : ops(ops_), LG(lg), solo(solo_), wpr(solo_ ? 8 : 4) {}
 
-    static int regs(int sd) { return sd >= 2 ? 1 << (sd - 2) : 1; }   // registers of a node of 2^sd words
+    // registers of a node of 2^sd words
+    int regs(int sd) const { return solo ? (sd >= 3 ? 1 << (sd - 3) : 1) : (sd >= 2 ? 1 << (sd - 2) : 1); }
     static int planes(int r) { return r >= 16 ? r / 16 : 1; }
     static std::string M(int sd, int i) { return "m" + std::to_string(sd) + "[" + std::to_string(i) + "]"; }
     // sign plane of register i of a node of 2^sd words, shifted so that register i is at bit 0
@@ -115,7 +122,7 @@ struct PairGen {
     // ---- ops on nodes of >= 4 output words: lane-private, four words per register ----------
     void big_op(const polar_sc_op &op, int pd, int cd, int n4)
     {
-        const int np = planes(n4), l0 = op.pos / 4, ub = op.upos >= 0 ? op.upos / 4 : -1;
+        const int np = planes(n4), l0 = op.pos / wpr, ub = op.upos >= 0 ? op.upos / wpr : -1;
         const bool root = pd == LG;   // the subtree root: SM16 words re-read from its stage slot
         if (root && (op.code == POLAR_OP_REP || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC)) root_split(2 * n4);
         if (root && op.code == POLAR_OP_F) {
@@ -173,17 +180,18 @@ struct PairGen {
             o << "  { // REP n " << op.n << "\n    u32 acc_ = 0u, FS_[" << np << "];\n";
             for (int k = 0; k < np; k++)
                 o << "    FS_[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << ";\n";
+            // (solo: the words of a register in order 8 i + r, then 8 i + 4 + r, into the low half)
             for (int i = 0; i < n4; i++) {
                 o << "    { const X4 t_ = rows4(row_sum_biased(F_split_biased<" << i % 16 << ">(" << M(pd, i) << ", "
                   << M(pd, n4 + i) << ", FS_[" << i / 16 << "])));\n"
-                  << "      acc_ = rep_acc_rows(acc_, t_.t0, t_.t1, t_.t2, t_.t3); }\n";
+                  << "      acc_ = " << (solo ? "rep_acc_solo" : "rep_acc_rows") << "(acc_, t_.t0, t_.t1, t_.t2, t_.t3); }\n";
                 chunk_fence(i, n4);
             }
-            o << "    if (rep_any_zero(acc_)) {\n      acc_ = 0u;\n";
+            o << "    if (" << (solo ? "rep_any_zero_lo" : "rep_any_zero") << "(acc_)) {\n      acc_ = 0u;\n";
             for (int i = 0; i < n4; i++)
-                o << "      acc_ = rep_sm_rows(acc_, F_split_sm<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i)
-                  << ", FS_[" << i / 16 << "]), ln);\n";
-            o << "    }\n    const u32 full_ = pk_sra(acc_, 15);\n";
+                o << "      acc_ = " << (solo ? "rep_sm_solo" : "rep_sm_rows") << "(acc_, F_split_sm<" << i % 16 << ">("
+                  << M(pd, i) << ", " << M(pd, n4 + i) << ", FS_[" << i / 16 << "]), ln);\n";
+            o << "    }\n    const u32 full_ = pk_sra(" << (solo ? "bcast_lo(acc_)" : "acc_") << ", 15);\n";
             for (int j = 0; j < n4; j += 16) put_mask(l0 + j, n4 < 16 ? n4 : 16, "full_");
             o << "  }\n";
             clobber_parent(pd, n4);
@@ -198,12 +206,14 @@ struct PairGen {
                 o << "    X_[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << " ^ " << U(ub, k) << ";\n";
             if (spc) o << "    u32 klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu, par_ = 0u;\n    const u32 rw_ = spc_sub(c.row, ln);\n";
             for (int i = 0; i < n4; i++) {
+                // key: (|lambda|, word, bitrev4(position)); solo: word 8 i + 4 h + r (bit 6 = h)
                 if (spc)
                     o << "    { const u32 l_ = G_split<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i) << ", X_["
                       << i / 16 << "], LT_[" << i / 16 << "]);\n"
-                      << "      klo_ = __builtin_elementwise_min(klo_, (l_ << 24) | rw_ | " << (i << 6) << "u);\n"
-                      << "      khi_ = __builtin_elementwise_min(khi_, ((l_ >> 16) << 24) | rw_ | " << (i << 6)
-                      << "u); }\n";
+                      << "      klo_ = __builtin_elementwise_min(klo_, (l_ << 24) | rw_ | " << (solo ? i << 7 : i << 6)
+                      << "u);\n"
+                      << "      khi_ = __builtin_elementwise_min(khi_, ((l_ >> 16) << 24) | rw_ | "
+                      << (solo ? (i << 7) | 64 : i << 6) << "u); }\n";
                 else
                     o << "    LT_[" << i / 16 << "] = plane_put<" << i % 16 << ">(LT_[" << i / 16 << "], pk_sub(" << M(pd, i)
                       << ", " << M(pd, n4 + i) << "));\n";
@@ -219,6 +229,25 @@ struct PairGen {
                 if (n4 < 16) {
                     const unsigned m = (1u << n4) - 1u;
                     o << "    par_ &= 0x" << std::hex << (m | (m << 16)) << std::dec << "u;\n";
+                }
+                if (solo) {
+                    // one frame: parity of both halves, the first minimum of both
+                    o << "    par_ = (__builtin_popcount(par_) & 1u) << 15;\n"
+                         "    par_ = row_xor(par_);\n"
+                         "    klo_ = row_min_u32(__builtin_elementwise_min(klo_, khi_));\n"
+                         "    { X2 p_ = swap16(par_); par_ = p_.a ^ p_.b; p_ = swap32(par_); par_ = p_.a ^ p_.b;\n"
+                         "      X2 a_ = swap16(klo_); klo_ = __builtin_elementwise_min(a_.a, a_.b);\n"
+                         "      a_ = swap32(klo_); klo_ = __builtin_elementwise_min(a_.a, a_.b); }\n"
+                         "    const u32 ilo_ = (klo_ >> 7) & 0x1FFFFu, hs_ = (klo_ >> 2) & 16u;\n"
+                         "    const bool flo_ = land(par_ & 0x8000u, (klo_ & 63u) == rw_);\n";
+                    if (n4 <= 16)
+                        o << "    bw[" << l0 / 16 << "] ^= sel(flo_, 1u << (" << l0 % 16 << " + ilo_ + hs_), 0u);\n";
+                    else
+                        for (int k = 0; k < n4 / 16; k++)
+                            o << "    bw[" << l0 / 16 + k << "] ^= sel(land(flo_, (ilo_ >> 4) == " << k
+                              << "u), 1u << ((ilo_ & 15u) + hs_), 0u);\n";
+                    o << "  }\n";
+                    break;
                 }
                 o << "    par_ = ((__builtin_popcount(par_ & 0xFFFFu) & 1u) << 15) | ((__builtin_popcount(par_ >> 16) & 1u) << 31);\n"
                      "    par_ = row_xor(par_);\n"
@@ -264,6 +293,86 @@ struct PairGen {
         }
         default:
             throw std::runtime_error("pairgen: unexpected op");
+        }
+    }
+
+    // ---- solo layout: ops with 4 output words (a parent of 8 words = one register, word
+    // 4 h + r in half h, row r) ------------------------------------------------------------
+    // the children of an 8-word node sit in the two halves of one register: F / REP use the
+    // half rotated into place (symmetric ops: both halves get the result); G / R1 / SPC are
+    // computed in the low half (a = word r, b = word r + 4) and broadcast. Decisions of a
+    // 4-word node go to local word pos / 8, half (pos / 4) & 1, all rows.
+    static std::string bitmask(int l, int hd)
+    {
+        std::ostringstream s;
+        s << "0x" << std::hex << (1u << (l % 16 + 16 * hd)) << std::dec << "u";
+        return s.str();
+    }
+    // the sign(a') ^ sign(b) plane bit 0 of a half op: sign planes of both halves + u of the left
+    // sibling (half 0 of local word ub)
+    std::string half_x(int pd, int ub)
+    {
+        std::ostringstream s;
+        s << "s" << pd << "[0] ^ hswap(s" << pd << "[0])";
+        if (ub >= 0) s << " ^ (bw[" << ub / 16 << "] >> " << ub % 16 << ")";
+        return s.str();
+    }
+    void half_op(const polar_sc_op &op, int pd, int cd)
+    {
+        const int l = op.pos / 8, hd = (op.pos / 4) & 1, ub = op.upos >= 0 ? op.upos / 8 : -1;
+        const std::string mp = M(pd, 0), sp = "s" + std::to_string(pd) + "[0]";
+        switch (op.code) {
+        case POLAR_OP_F:
+            o << "  { // F n 4 (halves)\n    " << M(cd, 0) << " = pk_min(" << mp << ", hswap(" << mp << "));\n    s" << cd
+              << "[0] = " << sp << " ^ hswap(" << sp << ");\n  }\n";
+            break;
+        case POLAR_OP_G:
+            o << "  { // G n 4 upos " << op.upos << " (halves)\n    u32 LT_ = 0u; const u32 X_ = " << half_x(pd, ub)
+              << ";\n    const u32 m_ = G_split<0>(" << mp << ", hswap(" << mp << "), X_, LT_);\n    " << M(cd, 0)
+              << " = bcast_lo(m_);\n    s" << cd << "[0] = bcast_lo(hswap(" << sp << ") ^ (X_ & ~LT_));\n  }\n";
+            break;
+        case POLAR_OP_REP:
+            o << "  { // REP n 4 (halves)\n    u32 acc_ = 0u; const u32 FS_ = " << sp << " ^ hswap(" << sp
+              << "), mb_ = hswap(" << mp << ");\n"
+              << "    { const X4 t_ = rows4(row_sum_biased(F_split_biased<0>(" << mp << ", mb_, FS_)));\n"
+              << "      acc_ = rep_acc_rows(acc_, t_.t0, t_.t1, t_.t2, t_.t3); }\n"
+              << "    if (rep_any_zero(acc_)) {\n      acc_ = rep_sm_rows(0u, F_split_sm<0>(" << mp << ", mb_, FS_), ln);\n    }\n"
+              << "    bw[" << l / 16 << "] = bsel(" << bitmask(l, hd) << ", pk_sra(acc_, 15), bw[" << l / 16 << "]);\n  }\n";
+            break;
+        case POLAR_OP_R1:
+            o << "  { // R1 n 4 upos " << op.upos << " (halves)\n    const u32 X_ = " << half_x(pd, ub)
+              << ";\n    const u32 LT_ = plane_put<0>(0u, pk_sub(" << mp << ", hswap(" << mp << ")));\n"
+              << "    const u32 h_ = hswap(" << sp << ") ^ (X_ & ~LT_);\n"
+              << "    bw[" << l / 16 << "] = bsel(" << bitmask(l, hd) << ", h_ << " << l % 16 + 16 * hd << ", bw[" << l / 16
+              << "]);\n  }\n";
+            break;
+        case POLAR_OP_SPC:
+            o << "  { // SPC n 4 upos " << op.upos << " (halves)\n    u32 LT_ = 0u; const u32 X_ = " << half_x(pd, ub)
+              << ";\n    const u32 l_ = G_split<0>(" << mp << ", hswap(" << mp << "), X_, LT_);\n"
+              << "    const u32 h_ = hswap(" << sp << ") ^ (X_ & ~LT_);\n"
+              << "    u32 par_ = row_xor((h_ & 1u) << 15);\n"
+              << "    const u32 rw_ = spc_sub(c.row, ln);\n"
+              << "    u32 klo_ = row_min_u32(((l_ & 0xFFu) << 24) | rw_);\n"
+              << "    { X2 p_ = swap16(par_); par_ = p_.a ^ p_.b; p_ = swap32(par_); par_ = p_.a ^ p_.b;\n"
+              << "      X2 a_ = swap16(klo_); klo_ = __builtin_elementwise_min(a_.a, a_.b);\n"
+              << "      a_ = swap32(klo_); klo_ = __builtin_elementwise_min(a_.a, a_.b); }\n"
+              << "    const bool flo_ = land(par_ & 0x8000u, (klo_ & 63u) == rw_);\n"
+              << "    bw[" << l / 16 << "] = bsel(" << bitmask(l, hd) << ", (h_ ^ sel(flo_, 1u, 0u)) << " << l % 16 + 16 * hd
+              << ", bw[" << l / 16 << "]);\n  }\n";
+            break;
+        case POLAR_OP_H:
+        case POLAR_OP_H0: {
+            // node of 8 words at pos: children in halves 0 / 1 of local word pos / 8
+            const bool h = op.code == POLAR_OP_H;
+            const int j = l / 16, b = l % 16;
+            o << "  { // " << (h ? "H" : "H0") << " n 4 (halves)\n";
+            if (h) o << "    bw[" << j << "] ^= (bw[" << j << "] >> 16) & " << (1u << b) << "u;\n";
+            else o << "    bw[" << j << "] = bsel(" << (1u << b) << "u, bw[" << j << "] >> 16, bw[" << j << "]);\n";
+            o << "  }\n";
+            break;
+        }
+        default:
+            throw std::runtime_error("pairgen: unexpected half op");
         }
     }
 
@@ -366,7 +475,12 @@ struct PairGen {
                 o << "  { // " << (h ? "H" : "H0") << " n 2\n    const u32 w_ = " << R;
                 if (h) o << " ^ (" << small2.at(op.pos) << " & row_lo2(c.row))";
                 o << ";\n";
-                put_mask(op.pos / 4, 1, "w_");
+                if (solo) {   // local word pos / 8, half (pos / 4) & 1
+                    const int l = op.pos / 8;
+                    o << "    bw[" << l / 16 << "] = bsel(" << bitmask(l, (op.pos / 4) & 1) << ", w_, bw[" << l / 16 << "]);\n";
+                } else {
+                    put_mask(op.pos / 4, 1, "w_");
+                }
                 o << "  }\n";
             }
             break;
@@ -383,10 +497,12 @@ struct PairGen {
         if (op.code == POLAR_OP_H || op.code == POLAR_OP_H0) {
             // H of a node of 2n words: small when the node is 2 or 4 words
             if (op.n <= 2) small_op(op, pd, cd);
-            else big_op(op, pd, cd, op.n / 4);
+            else if (op.n < wpr) half_op(op, pd, cd);
+            else big_op(op, pd, cd, op.n / wpr);
             return;
         }
-        if (op.n >= 4) big_op(op, pd, cd, op.n / 4);
+        if (op.n >= wpr) big_op(op, pd, cd, op.n / wpr);
+        else if (op.n == 4 && solo) half_op(op, pd, cd);
         else small_op(op, pd, cd);
     }
 
@@ -395,7 +511,7 @@ struct PairGen {
     // inl: inlined at its call sites (polar_sc_tuning.sub_inline = 2) instead of a call
     void sub_function(int id, bool inl)
     {
-        const int words = 1 << LG, R = regs(LG), nbw = words / 4 >= 16 ? words / 64 : 1;
+        const int words = 1 << LG, R = regs(LG), lw = words / wpr, nbw = lw >= 16 ? lw / 16 : 1;   // lw: local words
         // (plain arguments: a PairCtx passed by reference would live on the private stack)
         o << "__device__ " << (inl ? "__forceinline__" : "__noinline__") << " void polar_psub_" << id
           << "(const u32 *src_, g_u32 *hb_, int l0)\n{\n"
@@ -413,10 +529,10 @@ struct PairGen {
             if (op.code == POLAR_OP_END) break;
             this->op(op);
         }
-        if (words / 4 >= 16) {
+        if (lw >= 16) {
             for (int j = 0; j < nbw; j++) o << "  BST(" << j << ", bw[" << j << "]);\n";
         } else {
-            const unsigned m = (1u << (words / 4)) - 1u;
+            const unsigned m = (1u << lw) - 1u;
             o << "  BSTM(0x" << std::hex << (m | (m << 16)) << std::dec << "u, bw[0]);\n";
         }
         o << "}\n\n";
@@ -430,9 +546,10 @@ const char *const kPairCH = "#define CH(j) prow(src_[((j) >> 3) * 256 + (((j) >>
                             "    (((v) << (l0 & 15)) & ((m) << (l0 & 15))))\n";
 
 // upper-level record -> call of a polar_sc_pair.h loop function
-void upper_call(std::ostringstream &o, const polar_sc_op &op)
+// (wpr: words per slot row of one (virtual) frame -- 4 pair, 8 solo)
+void upper_call(std::ostringstream &o, const polar_sc_op &op, int wpr)
 {
-    const int n4 = op.n / 4, l0 = op.pos / 4, ub = op.upos >= 0 ? op.upos / 4 : -1;
+    const int n4 = op.n / wpr, l0 = op.pos / wpr, ub = op.upos >= 0 ? op.upos / wpr : -1;
     o << "    c.sync(); ";
     switch (op.code) {
     case POLAR_OP_F: o << "pop_fg_split<false>(c, " << op.level << ", " << n4 << ", -1);"; break;
@@ -470,7 +587,7 @@ int chain_len(const std::vector<polar_sc_op> &ops, size_t i, int cmax)
     }
     return d;
 }
-void chain_call(std::ostringstream &o, const std::vector<polar_sc_op> &ops, size_t i, int d)
+void chain_call(std::ostringstream &o, const std::vector<polar_sc_op> &ops, size_t i, int d, int wpr)
 {
     const polar_sc_op &o0 = ops[i];
     unsigned gm = 0;
@@ -478,7 +595,7 @@ void chain_call(std::ostringstream &o, const std::vector<polar_sc_op> &ops, size
         if (ops[i + k].code == POLAR_OP_G) gm |= 1u << k;
     const bool g0 = o0.code == POLAR_OP_G;
     o << "    c.sync(); pop_chain<" << d << ", " << (o0.level == 0 ? "true" : "false") << ", " << (g0 ? "true" : "false")
-      << ">(c, " << o0.level << ", " << o0.n / 4 << ", " << (g0 && o0.upos >= 0 ? o0.upos / 4 : -1) << ", " << gm
+      << ">(c, " << o0.level << ", " << o0.n / wpr << ", " << (g0 && o0.upos >= 0 ? o0.upos / wpr : -1) << ", " << gm
       << "u);   // chain";
     for (int k = 0; k < d; k++) {
         const polar_sc_op &q = ops[i + k];
@@ -489,16 +606,17 @@ void chain_call(std::ostringstream &o, const std::vector<polar_sc_op> &ops, size
 
 // one decode kernel: a block of W waves per frame pair; `seg` selects the schedule segment
 // (the cases between POLAR_OP_SEGEND records; 0 when the plan has no grid tier)
-void pair_kernel(std::ostringstream &o, const char *name, const std::vector<polar_sc_op> &ops, int cmax)
+void pair_kernel(std::ostringstream &o, const char *name, const std::vector<polar_sc_op> &ops, int cmax, bool solo)
 {
+    const int wpr = solo ? 8 : 4;
     o << "extern \"C\" __global__ void __launch_bounds__(" << 64 * PAIR_WAVES_MAX << ") " << name << "(\n"
       << "    const signed char *__restrict__ llr, unsigned short *__restrict__ out, unsigned int *__restrict__ scratch,\n"
       << "    int N, int batch, int out_stride, int pair_dwords, int slot_rows, int lds_row0, int seg)\n{\n"
       << "  extern __shared__ __attribute__((aligned(16))) unsigned int smem_[];\n"
       << "  PairCtx c;\n"
       << "  const int W = blockDim.x >> 6, wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-      << "  const long pair = blockIdx.x;\n"
-      << "  if (2 * pair >= batch) return;\n"
+      << "  const long pair = blockIdx.x;   // (solo: the frame)\n"
+      << "  if (" << (solo ? "pair" : "2 * pair") << " >= batch) return;\n"
       << "  pair_init(c, llr, scratch, N, batch, pair, pair_dwords, slot_rows, lds_row0, wi, W, (lds_w32 *)smem_);\n"
       << "  switch (seg) {\n  case 0:\n";
     int seg = 0;
@@ -511,17 +629,21 @@ void pair_kernel(std::ostringstream &o, const char *name, const std::vector<pola
         }
         const int d = chain_len(ops, i, cmax);
         if (d >= 2) {
-            chain_call(o, ops, i, d);
+            chain_call(o, ops, i, d, wpr);
             i += (size_t)d - 1;
             continue;
         }
-        upper_call(o, op);
+        upper_call(o, op, wpr);
     }
-    o << "    c.sync();\n"
-      << "    pair_out(c, (g_u16 *)out + (2 * pair) * (long)out_stride, (g_u16 *)out + (2 * pair + 1) * (long)out_stride,\n"
-      << "             2 * pair < batch,\n"
-      << "             2 * pair + 1 < batch, out_stride);\n"
-      << "    return;\n  default: return;\n  }\n}\n";
+    o << "    c.sync();\n";
+    if (solo)
+        o << "    pair_out(c, (g_u16 *)out + pair * (long)out_stride, (g_u16 *)out + pair * (long)out_stride, true, false,\n"
+          << "             out_stride);\n";
+    else
+        o << "    pair_out(c, (g_u16 *)out + (2 * pair) * (long)out_stride, (g_u16 *)out + (2 * pair + 1) * (long)out_stride,\n"
+          << "             2 * pair < batch,\n"
+          << "             2 * pair + 1 < batch, out_stride);\n";
+    o << "    return;\n  default: return;\n  }\n}\n";
 }
 
 }  // namespace
@@ -531,7 +653,10 @@ void pair_kernel(std::ostringstream &o, const char *name, const std::vector<pola
 std::string pair_source(const polar_sc_plan &p)
 {
     std::ostringstream o;
-    o << "#define POLAR_LANE_REMAP 1\n#define POLAR_Q " << p.cfg.llr_bits << "\n#define POLAR_LPAR "
+    const bool solo = p.solo != 0;
+    const int wpr = solo ? 8 : 4;
+    o << "#define POLAR_LANE_REMAP 1\n" << (solo ? "#define POLAR_SOLO 1\n" : "") << "#define POLAR_Q " << p.cfg.llr_bits
+      << "\n#define POLAR_LPAR "
       << (p.cfg.par == 64 ? 6 : p.cfg.par == 32 ? 5 : 4)
       << "\n" << (p.cfg.extended ? "" : "#define POLAR_EXT 0\n")   // EXTENDED = 0: saturating leaves
       << "#include \"polar_sc_pair.h\"\n"
@@ -539,22 +664,23 @@ std::string pair_source(const polar_sc_plan &p)
     int lg = 0;
     while ((1 << lg) < p.sub_words) lg++;
     for (size_t id = 0; id < p.subs.size(); id++) {
-        PairGen g(p.subs[id], lg);
+        PairGen g(p.subs[id], lg, solo);
         g.sub_function((int)id, p.tune.sub_inline == 2);
         o << g.o.str();
     }
     o << "}  // namespace polar\nusing namespace polar;\n";
     // the decode kernel over the whole schedule, and (grid-tier plans) the segment kernel
     const int cmax = p.tune.chain_max ? p.tune.chain_max : PAIR_CHAIN_MAX;
-    pair_kernel(o, "polar_sc_pair_kernel", p.pair_ops, cmax);
+    pair_kernel(o, "polar_sc_pair_kernel", p.pair_ops, cmax, solo);
     // test hook (polar_sc_debug_subtree): subtree decoder `id` on 64 lanes of root slot rows
     // in[64 j + lane] (u16 SM8 pairs, repacked into row-pair dwords in LDS), its partial-sum
     // dwords to out[64 d + lane]
+    const int rp = p.sub_words / wpr / 2;   // row-pair dwords of the root slot
     o << "extern \"C\" __global__ void __launch_bounds__(64) polar_sc_pair_subtest_kernel(\n"
       << "    const unsigned short *__restrict__ in, unsigned int *__restrict__ out, int id)\n{\n"
-      << "  __shared__ unsigned int rows_[" << p.sub_words / 8 << " * 64];\n"
+      << "  __shared__ unsigned int rows_[" << (rp < 4 ? 4 : rp) << " * 64];\n"
       << "  const int lane = threadIdx.x & 63;\n"
-      << "  for (int i = 0; i < " << p.sub_words / 8 << "; i++) {\n"
+      << "  for (int i = 0; i < " << rp << "; i++) {\n"
       << "    const unsigned int r0 = in[128 * i + lane], r1 = in[128 * i + 64 + lane];\n"
       << "    rows_[(i >> 2) * 256 + 4 * lane + (i & 3)] = (r0 & 0xFFu) | ((r1 & 0xFFu) << 8) | ((r0 >> 8) << 16) |\n"
       << "                                                ((r1 >> 8) << 24);\n"
@@ -565,7 +691,7 @@ std::string pair_source(const polar_sc_plan &p)
         o << "  case " << id << ": polar_psub_" << id << "(src, (g_u32 *)out + lane, 0); return;\n";
     o << "  default: return;\n  }\n}\n";
     if (!p.pair_tier.steps.empty()) {
-        pair_kernel(o, "polar_sc_pair_seg_kernel", p.pair_tier.seg_ops, cmax);
+        pair_kernel(o, "polar_sc_pair_seg_kernel", p.pair_tier.seg_ops, cmax, solo);
         o << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_pair_tier_kernel(\n"
           << "    const signed char *__restrict__ llr, unsigned int *__restrict__ scratch, int N, int batch, int pair_dwords,\n"
           << "    int slot_rows, int code_g, int k, int n4, int ub, int cw)\n{\n"

@@ -79,6 +79,7 @@ constexpr int HYBRID_MAX_WAVES = 8;
 // <= 256 VGPRs per wave), subtrees of at most PAIR_SUB_WORDS words in registers
 constexpr int PAIR_WAVES_MAX = 8;
 constexpr int PAIR_SUB_WORDS = 256;
+constexpr int SOLO_SUB_WORDS_MAX = 512;   // solo plans: half the registers per word
 // unified register file per SIMD lane (VGPRs + AGPRs) shared by the waves on the SIMD
 constexpr int SIMD_REGS = 512;
 // one CU's LDS (gfx950)
@@ -87,7 +88,7 @@ constexpr long CU_LDS_BYTES = 160l * 1024l;
 // launch shape of a pair plan for one batch (jit_launch_pair, polar_sc_plan_launch_info)
 struct PairShape {
     int W = 0;            // waves per frame pair (0: the kernel does not fit, -ENOTSUP)
-    long pairs = 0;       // blocks
+    long pairs = 0;       // blocks (frame pairs; solo plans: frames)
     int lds_row0 = 0;     // first stage-slot row held in LDS
     unsigned lds = 0;     // dynamic LDS bytes per block
 };
@@ -141,10 +142,14 @@ struct polar_sc_plan {
     // subtrees of sub_words words as generated register code (subs), the upper levels as
     // loops over stage-slot rows (pair_ops); optional grid tier (pair_tier.steps non-empty)
     int pair = 0;
+    // solo layout of a pair plan (polar_sc_pair.h POLAR_SOLO): one frame per block, a slot row /
+    // register = 8 words of the frame (pair: 4 words of two frames)
+    int solo = 0;
     std::vector<polar_sc_op> pair_ops;
     polar_host::PairTier pair_tier;
-    int pair_slot_rows = 0;          // stage-slot rows per pair (levels of nodes G/2 .. sub_words)
-    int pair_dwords = 0;             // HBM scratch per pair: slot rows (128 B) + bit dwords (256 B)
+    int pair_slot_rows = 0;          // stage-slot rows per pair / solo frame (levels of nodes G/2 .. sub_words)
+    int pair_dwords = 0;             // HBM scratch per pair / frame: slot rows (128 B) + bit dwords (256 B)
+    int wpr() const { return solo ? 8 : 4; }   // words of one (virtual) frame per slot row
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;
     mutable std::mutex host_mu;                             // polar_sc_decode_host staging

@@ -281,6 +281,42 @@ def swap32(x):
     return X2(x[LANE & ~32], x[LANE | 32])
 
 
+def hswap(x):
+    x = V(x).astype(np.int64)
+    return (((x >> 16) | (x << 16)) & 0xFFFFFFFF).astype(U32)
+
+
+def bcast_lo(x):
+    x = V(x).astype(np.int64) & 0xFFFF
+    return (x | (x << 16)).astype(U32)
+
+
+def bcast_hi(x):
+    x = V(x).astype(np.int64) >> 16
+    return (x | (x << 16)).astype(U32)
+
+
+def rep_acc_solo(acc, t0, t1, t2, t3):
+    for t in (t0, t1, t2, t3):
+        acc = rep_acc(acc, t)
+    for t in (t0, t1, t2, t3):
+        acc = rep_acc(acc, V(t) >> 16)
+    return acc
+
+
+def rep_sm_solo(acc, v, ln):
+    t = rows4(row_add_tree(v, ln))
+    for tt in (t.t0, t.t1, t.t2, t.t3):
+        acc = G_sm(REPSAT, tt, acc, 0)
+    for tt in (t.t0, t.t1, t.t2, t.t3):
+        acc = G_sm(REPSAT, V(tt) >> 16, acc, 0)
+    return acc
+
+
+def rep_any_zero_lo(acc):
+    return bool((lo(acc) == 0).any())
+
+
 def rows4(x):
     p = swap16(x)
     q0, q1 = swap32(p.a), swap32(p.b)
@@ -497,6 +533,11 @@ class Ctx:
 
 
 # ---- the whole decode ----------------------------------------------------------------
+def is_solo(src):
+    """the generated source is of the solo layout (polar_sc_pair.h POLAR_SOLO)"""
+    return "#define POLAR_SOLO 1" in src
+
+
 def decode(dec, llr):
     """Emulated decode of int8 frames [B, N] with pair plan `dec`: x^ [B, N] uint8."""
     src = dec.kernel_source()
@@ -509,6 +550,12 @@ def decode(dec, llr):
     B = llr.shape[0]
     out = np.zeros((B, N), np.uint8)
     ln, c = Lanes(), Ctx()
+    if is_solo(src):
+        # one frame per wave: the halves are the frame's words 8 j + 4 h + r ("virtual frames")
+        for f in range(B):
+            bits = _decode_pair(llr[f].astype(np.int64), None, G // 2, S, upper, subs, ln, c, solo=True)
+            out[f] = _bits_to_frames(bits, G, ln, solo=True)
+        return out
     for p in range(0, B, 2):
         f0, f1 = p, min(p + 1, B - 1)
         bits = _decode_pair(llr[f0].astype(np.int64), llr[f1].astype(np.int64), G, S, upper, subs, ln, c)
@@ -548,7 +595,8 @@ def _upper_ops(src):
     return ops
 
 
-def _decode_pair(c0, c1, G, S, upper, subs, ln, c):
+def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
+    """solo: c0 is the frame, G its virtual words per half (N / 32)"""
     pos = lane_pos(LANE & 15)
     row = LANE >> 4
     # slots: level k (node of G >> k words) -> list of G >> k >> 2 rows (u16 SM8 pairs)
@@ -557,6 +605,9 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c):
     bits = [V(0) for _ in range(max(nbd, 1))]
 
     def chan(j):
+        if solo:   # row j: words 8 j + 4 h + r
+            off = 16 * (8 * j + row) + pos
+            return conv_pair((c0[off] & 0xFF) | ((c0[off + 64] & 0xFF) << 16))
         off = 16 * (4 * j + row) + pos
         return conv_pair((c0[off] & 0xFF) | ((c1[off] & 0xFF) << 16))
 
@@ -594,14 +645,20 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c):
             for lam in lams:
                 sg = pk_sra(lam, 15)
                 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200)))
-                acc = rep_acc(rep_acc(rep_acc(rep_acc(acc, t.t0), t.t1), t.t2), t.t3)
-            if rep_any_zero(acc):
+                if solo:
+                    acc = rep_acc_solo(acc, t.t0, t.t1, t.t2, t.t3)
+                else:
+                    acc = rep_acc(rep_acc(rep_acc(rep_acc(acc, t.t0), t.t1), t.t2), t.t3)
+            if (rep_any_zero_lo if solo else rep_any_zero)(acc):
                 acc = V(0)
                 for lam in lams:
+                    if solo:
+                        acc = rep_sm_solo(acc, lam, ln)
+                        continue
                     t = rows4(row_add_tree(lam, ln))
                     for tt in (t.t0, t.t1, t.t2, t.t3):
                         acc = G_sm(REPSAT, tt, acc, 0)
-            full = pk_sra(acc, 15)
+            full = pk_sra(bcast_lo(acc) if solo else acc, 15)
             for l in range(0, n4, 16):
                 bput(l0 + l, min(16, n4 - l), full)
         elif kind in ("R1", "SPC"):
@@ -619,12 +676,28 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c):
                     first = max((l0 + j) & ~15, l0)
                     bput(first, l0 + j + 1 - first, acc)
                     acc = V(0)
-                if kind == "SPC":
+                if kind == "SPC" and solo:
+                    # key (|lambda|, word 8 j + 4 h + r, bitrev4(position))
+                    par = par ^ h
+                    wk = ((j << 7) | (row << 4)).astype(U32)
+                    klo = np.minimum(klo, ((lam & 0xFF) << 24) | wk)
+                    khi = np.minimum(khi, (((lam >> 16) & 0xFF) << 24) | wk | 64)
+                elif kind == "SPC":
                     par = par ^ h
                     wk = ((4 * j + row) << 4).astype(U32)
                     klo = np.minimum(klo, ((lam & 0xFF) << 24) | wk)
                     khi = np.minimum(khi, (((lam >> 16) & 0xFF) << 24) | wk)
-            if kind == "SPC":
+            if kind == "SPC" and solo:
+                parity = (int(np.bitwise_xor.reduce(V(par).astype(np.int64))) >> 15) & 1
+                parity ^= (int(np.bitwise_xor.reduce(V(par).astype(np.int64))) >> 31) & 1
+                k = np.minimum(klo | ln.br, khi | ln.br).min()
+                if parity:
+                    l = l0 + int((k >> 7) & 0x1FFFF)
+                    hb = 16 if (k & 64) else 0
+                    for L in range(64):
+                        if (int(k) & 63) == ((int(row[L]) << 4) | int(ln.br[L])):
+                            bits[l >> 4][L] ^= U32(1 << ((l & 15) + hb))
+            elif kind == "SPC":
                 par = row_xor(par)
                 klo = row_min_u32(klo | ln.br)
                 khi = row_min_u32(khi | ln.br)
@@ -675,10 +748,20 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c):
     return bits
 
 
-def _bits_to_frames(bits, G, ln):
-    """partial sums (local words per lane) -> x^ of both frames"""
+def _bits_to_frames(bits, G, ln, solo=False):
+    """partial sums (local words per lane) -> x^ of both frames (solo: of the one frame)"""
     pos = lane_pos(LANE & 15)
     row = LANE >> 4
+    if solo:
+        x = np.zeros(G * 16, np.uint8)
+        for d, v in enumerate(bits):
+            v = v.astype(np.int64)
+            for j in range(16):
+                for h in range(2):
+                    w = 8 * (16 * d + j) + 4 * h + row
+                    ok = w < G
+                    x[(16 * w + pos)[ok]] = ((v >> (j + 16 * h)) & 1)[ok]
+        return x
     x = np.zeros((2, G * 16), np.uint8)
     for d, v in enumerate(bits):
         v = v.astype(np.int64)
@@ -697,7 +780,8 @@ def run_sub(dec, sid, rows, subs=None):
     if subs is None:
         subs = Sub(dec.kernel_source(), dec.stats["n_sub_kinds"])
     S = dec.stats["sub_words"]
-    bits = [V(0) for _ in range(max(1, S // 64))]
+    wpr = 8 if is_solo(dec.kernel_source()) else 4
+    bits = [V(0) for _ in range(max(1, S // (16 * wpr)))]
 
     def CH(j):
         return slot_unpack(V(rows[j]))

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol(pkg):
     missing = [f for f in decl if not hasattr(lib, f)]
     assert not missing, missing
     assert set(decl) == set(pkg.EXPORTS)
-    assert lib.polar_sc_abi_version() == 3
+    assert lib.polar_sc_abi_version() == 4
 
 
 def test_no_oracle_in_product():
@@ -40,12 +40,22 @@ def test_tuning_validation_and_no_environment(pkg, monkeypatch):
     """polar_sc_tuning: out-of-range fields -> -EINVAL; the plan (and its generated kernel
     source) depends on the mask, config and tuning only, never on the environment."""
     m = util.mask("FB_N1024_K512")
-    for bad in ({"kernel": 4}, {"waves_per_group": 3}, {"waves_per_group": 32}, {"sub_words": 512},
+    for bad in ({"kernel": 4}, {"waves_per_group": 3}, {"waves_per_group": 32}, {"sub_words": 1024},
                 {"tier_words": -2}, {"tier_words": 1000}, {"lds_slots": 300}, {"hybrid_waves": 16},
-                {"chain_max": 5}, {"chain_max": -1}, {"sub_inline": 3}, {"sub_inline": -1}):
+                {"chain_max": 5}, {"chain_max": -1}, {"sub_inline": 3}, {"sub_inline": -1}, {"layout": 3},
+                {"layout": -1}):
         with pytest.raises(pkg.PolarError) as e:
             pkg.Decoder(m, tuning=bad)
         assert e.value.rc == -22, bad
+    # a layout only pair plans have (N >= 2048), and solo only at PAR 16: -ENOTSUP
+    with pytest.raises(pkg.PolarError) as e:
+        pkg.Decoder(m, tuning={"layout": 2})
+    assert e.value.rc == -95
+    c64 = pkg.default_config()
+    c64.par = 64
+    with pytest.raises(pkg.PolarError) as e:
+        pkg.Decoder(util.mask("frozen_n_16384_k_8192"), config=c64, tuning={"layout": 2})
+    assert e.value.rc == -95
     with pytest.raises(KeyError):
         pkg.make_tuning({"wpg": 1})
     src = pkg.Decoder(m).kernel_source()
