@@ -300,7 +300,19 @@ typedef struct polar_sc_launch_info {
                                    and kernel descriptors of the plan's compiled code
                                    object (equal code -> equal key whatever the source
                                    text), 0 = none */
+    uint32_t layout;            /* pair plans: 1 = frame pairs, 2 = solo (one frame per
+                                   wave); an automatic-layout plan decodes batches of at
+                                   most 2 frames per SIMD solo; 0 = not a pair plan */
+    uint32_t sub_words;         /* hybrid / pair plans: subtree size of the decoding plan */
+    uint32_t compiler;          /* which compiler built the generated kernel:
+                                   POLAR_SC_COMPILER_CLANG (the ROCm clang driver the library
+                                   was built with: the default when no GPU is open in the
+                                   process, or a code object it cached) or
+                                   POLAR_SC_COMPILER_HIPRTC (hipRTC: no clang driver, or a GPU
+                                   already open and no cached clang object); 0 = none */
 } polar_sc_launch_info;
+
+enum { POLAR_SC_COMPILER_CLANG = 1, POLAR_SC_COMPILER_HIPRTC = 2 };
 
 int polar_sc_plan_launch_info(const polar_sc_plan *plan, size_t batch, uint32_t cus, polar_sc_launch_info *info);
 

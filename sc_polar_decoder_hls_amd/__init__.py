@@ -98,7 +98,8 @@ class polar_sc_plan_stats(ctypes.Structure):
 class polar_sc_launch_info(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_uint32), ("regs", ctypes.c_uint32), ("regs_seg", ctypes.c_uint32),
                 ("waves_per_block", ctypes.c_uint32), ("blocks", ctypes.c_uint64), ("lds_bytes", ctypes.c_uint32),
-                ("lds_row0", ctypes.c_uint32), ("code_key", ctypes.c_uint64)]
+                ("lds_row0", ctypes.c_uint32), ("code_key", ctypes.c_uint64), ("layout", ctypes.c_uint32),
+                ("sub_words", ctypes.c_uint32), ("compiler", ctypes.c_uint32)]
 
 
 # exported symbols of include/polar_sc.h (tests check that the library exports all of them)

@@ -82,19 +82,23 @@ def struct_sub_words(N):
 
 def gpu_plans():
     """(name, mask, tuning) of every pair plan the GPU tests decode with."""
-    out = [(n, mask(n), {"kernel": 3}) for n, _ in PARITY_MASKS]
+    p = {"kernel": 3, "layout": 1}   # (tests/test_pair.py pair(): the frame-pair layout)
+    out = [(n, mask(n), dict(p)) for n, _ in PARITY_MASKS]
     for N in (2048, 8192, 32768):
         for i, m in enumerate(struct_masks(N)):
-            out += [("struct%d_%d" % (N, i), m, {"kernel": 3, "sub_words": sw}) for sw in struct_sub_words(N)]
-    out += [("frozen_n_2048_k_1024", mask("frozen_n_2048_k_1024"), {"kernel": 3, "sub_words": sw})
-            for sw in (32, 64)]
-    out += [("frozen_n_8192_k_4096", mask("frozen_n_8192_k_4096"), {"kernel": 3, "sub_words": 256}),
-            ("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"), {"kernel": 3, "sub_words": 64}),
-            ("wave_mask", wave_mask(), {"kernel": 3, "sub_words": 64}),
-            ("frozen_n_32768_k_29492", mask("frozen_n_32768_k_29492"),
-             {"kernel": 3, "tier_words": 512, "sub_words": 128}),
-            ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), {"kernel": 3}),
-            ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), {"kernel": 3, "tier_words": 1024})]
+            out += [("struct%d_%d" % (N, i), m, dict(p, sub_words=sw)) for sw in struct_sub_words(N)]
+    out += [("frozen_n_2048_k_1024", mask("frozen_n_2048_k_1024"), dict(p, sub_words=sw)) for sw in (32, 64)]
+    out += [("frozen_n_8192_k_4096", mask("frozen_n_8192_k_4096"), dict(p, sub_words=256)),
+            ("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"), dict(p, sub_words=64)),
+            ("wave_mask", wave_mask(), dict(p, sub_words=64)),
+            ("frozen_n_32768_k_29492", mask("frozen_n_32768_k_29492"), dict(p, tier_words=512, sub_words=128)),
+            ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), dict(p)),
+            ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), dict(p, tier_words=1024)),
+            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, lds_slots=256)),
+            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, lds_slots=1024))]
+    for wpg in (1, 2, 4, 8):
+        out += [("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"), dict(p, waves_per_group=wpg, sub_words=64)),
+                ("wave_mask", wave_mask(), dict(p, waves_per_group=wpg, sub_words=64))]
     return out
 
 
@@ -122,6 +126,9 @@ def solo_plans():
             ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), dict(t, sub_words=256)),
             ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), dict(t, sub_words=512)),
             ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(t, sub_words=512))]
+    for wpg in (1, 2, 4, 8):
+        out += [("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"), dict(t, waves_per_group=wpg, sub_words=64)),
+                ("wave_mask", wave_mask(), dict(t, waves_per_group=wpg, sub_words=64))]
     return out
 
 
@@ -143,7 +150,8 @@ def gpu_par64_plans():
 def cpu_test_plans():
     """(name, mask, tuning) of the plans the CPU register-budget test compiles (the round-3
     dispatch abort's configuration: chain_max = 4 on the structured N = 32768 mask)."""
-    return [("struct32768_0", struct_masks(32768)[0], {"kernel": 3, "sub_words": sw, "chain_max": 4}) for sw in (64, 256)]
+    return [("struct32768_0", struct_masks(32768)[0], {"kernel": 3, "layout": 1, "sub_words": sw, "chain_max": 4})
+            for sw in (64, 256)]
 
 
 # ---- datapath formats (tests/test_gpu_formats.py): (PAR, SIGMAG, EXTENDED, LLR_BITS) ---------

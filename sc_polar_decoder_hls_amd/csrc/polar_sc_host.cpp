@@ -9,6 +9,7 @@
 #include "polar_sc_plan.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -584,12 +585,35 @@ int waves_per_group(const polar_sc_plan *p, size_t batch, int simds)
     return w;
 }
 
+// SIMDs of the current device (4 per CU), cached per device ordinal
+int current_simds()
+{
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 1024;
+    if (dev < 64 && cache[dev].load()) return cache[dev].load();
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (dev < 64) cache[dev].store(4 * cus);
+    return 4 * cus;
+}
+
+// the plan that decodes a batch of `batch` frames on a device of `simds` SIMDs: the solo
+// alternate of an automatic-layout pair plan while the batch is at most SOLO_FRAMES_PER_SIMD
+// frames per SIMD (one frame per wave then still fits one dispatch round), else the plan
+const polar_sc_plan *layout_for(const polar_sc_plan *p, size_t batch, int simds)
+{
+    if (p->alt && batch <= (size_t)polar_host::SOLO_FRAMES_PER_SIMD * (size_t)simds) return p->alt;
+    return p;
+}
+
 int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size_t batch,
                   int out_stride, void *stream)
 {
     if (!p || (batch > 0 && (!llr || !out))) return -EINVAL;
     if (batch == 0) return 0;
     if (batch > (size_t)0x7FFFFFF8) return -EINVAL;
+    if (p->alt) p = layout_for(p, batch, current_simds());
     DevState *st = nullptr;
     // HBM-scratch plans launch under the plan lock: a concurrent decode of a larger batch on
     // another thread reallocates the scratch only after this launch has been queued (and
@@ -977,6 +1001,17 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         s.lds_bytes_per_wave = (uint32_t)(p->sub_words / p->wpr()) * 128u;
         s.scratch_bytes_per_wave = (uint64_t)p->pair_dwords * 4u;
     }
+    // automatic layout: a PAR 16 pair plan also holds its solo plan (subtrees of up to 512
+    // words), which small batches decode with (layout_for); none when the tuning cannot carry
+    // over (a subtree size below 64 words)
+    if (p->pair && !p->solo && t.layout == 0 && c.par == 16) {
+        polar_sc_tuning ts = t;
+        ts.layout = 2;
+        ts.kernel = 3;
+        if (!ts.sub_words) ts.sub_words = (int32_t)std::min<uint32_t>(polar_host::SOLO_SUB_WORDS_MAX, p->G / 2);
+        polar_sc_plan *a = nullptr;
+        if (polar_sc_plan_create_tuned(&a, N, info_mask, &c, &ts) == 0) p->alt = a;
+    }
     *out = p;
     return 0;
 }
@@ -984,6 +1019,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
 int polar_sc_plan_destroy(polar_sc_plan *p)
 {
     if (!p) return -EINVAL;
+    if (p->alt) polar_sc_plan_destroy(p->alt);
     for (auto &kv : p->host_bufs) {
         if (kv.second.llr) (void)hipFree(kv.second.llr);
         if (kv.second.out) (void)hipFree(kv.second.out);
@@ -1010,6 +1046,11 @@ int polar_sc_plan_prepare(const polar_sc_plan *p, size_t max_batch)
 {
     if (!p) return -EINVAL;
     DevState *st = nullptr;
+    if (p->alt) {   // the solo alternate takes the batches up to its threshold
+        const size_t cap = (size_t)polar_host::SOLO_FRAMES_PER_SIMD * (size_t)current_simds();
+        if (int rc = ensure_device(p->alt, std::min(max_batch ? max_batch : 1, cap), &st)) return rc;
+        if (max_batch && max_batch <= cap) return 0;
+    }
     return ensure_device(p, max_batch ? max_batch : 1, &st);
 }
 
@@ -1190,6 +1231,8 @@ int polar_sc_plan_compile(const polar_sc_plan *p)
 {
     if (!p) return -EINVAL;
     if (!p->jit && !p->hybrid && !p->pair) return -ENOTSUP;
+    if (p->alt)
+        if (int rc = polar_sc_plan_compile(p->alt)) return rc;
     std::lock_guard<std::mutex> lk(p->mu);
     return polar_host::jit_compile(*p);
 }
@@ -1219,6 +1262,9 @@ int polar_sc_plan_launch_info(const polar_sc_plan *p, size_t batch, uint32_t cus
     polar_sc_launch_info r{};
     r.kernel = p->stats.kernel;
     const int simds = 4 * (int)(cus ? cus : 256u);
+    p = layout_for(p, batch, simds);   // (automatic layout: the plan that decodes this batch)
+    r.layout = p->pair ? (p->solo ? 2u : 1u) : 0u;
+    r.sub_words = (uint32_t)p->sub_words;
     int regs = 0, regs_seg = 0;
     if (p->jit || p->hybrid || p->pair) {
         // under the plan lock: compile / decode may fill p->jit_code from another thread
@@ -1227,6 +1273,7 @@ int polar_sc_plan_launch_info(const polar_sc_plan *p, size_t batch, uint32_t cus
         polar_host::code_regs(*p, regs, regs_seg);
         if (regs < 0 || regs_seg < 0) return -EIO;   // kernel missing from the code object
         r.code_key = polar_host::code_key(*p);
+        r.compiler = p->jit_compiler;
     }
     r.regs = (uint32_t)regs;
     r.regs_seg = (uint32_t)regs_seg;

@@ -19,6 +19,7 @@
 #include <dlfcn.h>
 #include <elf.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <spawn.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
@@ -641,7 +642,8 @@ std::string cache_dir()
 }
 
 // the cache key: the source, the embedded headers it includes, the options, the hipRTC version
-uint64_t source_key(const std::string &src)
+// (rtc = false: objects of the offline clang driver, whose identity is part of `src` instead)
+uint64_t source_key(const std::string &src, bool rtc = true)
 {
     uint64_t h = 1469598103934665603ull;
     h = fnv1a(h, src.data(), src.size());
@@ -650,6 +652,7 @@ uint64_t source_key(const std::string &src)
     if (src.find("\"polar_sc_interp.h\"") != std::string::npos) h = fnv1a(h, kPolarInterpSrc, sizeof kPolarInterpSrc);
     if (src.find("\"polar_sc_pair.h\"") != std::string::npos) h = fnv1a(h, kPolarPairSrc, sizeof kPolarPairSrc);
     for (const char *o : kRtcOpts) h = fnv1a(h, o, std::strlen(o) + 1);
+    if (!rtc) return h;
     int ver_major = 0, ver_minor = 0;
     hiprtcVersion(&ver_major, &ver_minor);
     h = fnv1a(h, (const char *)&ver_major, sizeof ver_major);
@@ -691,12 +694,12 @@ uint64_t code_key(const polar_sc_plan &p)
 }
 
 namespace {
-std::string cache_path(const std::string &src)
+std::string cache_path(const std::string &src, bool rtc = true)
 {
     const std::string dir = cache_dir();
     if (dir.empty()) return "";
     char name[40];
-    std::snprintf(name, sizeof name, "/%016llx.co", (unsigned long long)source_key(src));
+    std::snprintf(name, sizeof name, "/%016llx.co", (unsigned long long)source_key(src, rtc));
     return dir + name;
 }
 
@@ -790,6 +793,24 @@ std::vector<std::string> extra_clang_flags()
     return out;
 }
 
+// identity of the clang driver for the cache key of its objects: path, size and mtime of the
+// binary (the hipRTC version says nothing about the compiler that built them)
+std::string clang_identity(const std::string &clang)
+{
+    struct stat st {};
+    if (clang.empty() || stat(clang.c_str(), &st) != 0) return "no clang";
+    return clang + " " + std::to_string((long long)st.st_size) + " " + std::to_string((long long)st.st_mtime);
+}
+
+// seconds a child compile may take before it is killed and hipRTC builds the kernel instead
+// (POLAR_SC_CLANG_TIMEOUT; the inlined C5 subtree variant, the longest, takes ~250 s)
+int clang_timeout_s()
+{
+    const char *e = getenv("POLAR_SC_CLANG_TIMEOUT");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 900;
+}
+
 int offline_compile(const std::string &src, std::vector<char> &code, std::string &log,
                     const std::vector<std::string> &extra)
 {
@@ -818,7 +839,20 @@ int offline_compile(const std::string &src, std::vector<char> &code, std::string
         pid_t pid;
         if (posix_spawn(&pid, clang.c_str(), &fa, nullptr, (char *const *)argv.data(), environ) == 0) {
             int status = 0;
-            if (waitpid(pid, &status, 0) == pid && WIFEXITED(status) && WEXITSTATUS(status) == 0) {
+            pid_t w = 0;
+            // bounded wait: a hung compiler must not hang the decode (it is killed, and the
+            // caller falls back to hipRTC)
+            for (long waited_ms = 0; (w = waitpid(pid, &status, WNOHANG)) == 0; waited_ms += 20) {
+                if (waited_ms >= 1000l * clang_timeout_s()) {
+                    kill(pid, SIGKILL);
+                    w = waitpid(pid, &status, 0);
+                    log += "clang driver killed after " + std::to_string(clang_timeout_s()) + " s\n";
+                    status = -1;
+                    break;
+                }
+                usleep(20000);
+            }
+            if (w == pid && status != -1 && WIFEXITED(status) && WEXITSTATUS(status) == 0) {
                 std::ifstream f(out, std::ios::binary);
                 std::vector<char> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
                 if (buf.size() >= 4 && std::memcmp(buf.data(), "\x7f" "ELF", 4) == 0) {
@@ -839,16 +873,19 @@ int offline_compile(const std::string &src, std::vector<char> &code, std::string
 
 // whole: a generated kernel source (compiled by the clang driver when available, under its own
 // cache key); otherwise, and for the interpreter sources, hipRTC
-int rtc_compile(const std::string &src, std::vector<char> &code, std::string &log, bool whole = false)
+// *compiler (optional): which compiler built the returned object, POLAR_SC_COMPILER_*
+int rtc_compile(const std::string &src, std::vector<char> &code, std::string &log, bool whole = false,
+                uint32_t *compiler = nullptr)
 {
+    if (compiler) *compiler = POLAR_SC_COMPILER_HIPRTC;
     if (whole) {
         const std::vector<std::string> extra = extra_clang_flags();
-        std::string key = src + "\n// offline clang driver\n";
+        std::string key = src + "\n// offline clang driver: " + clang_identity(rocm_clang()) + "\n";
         for (const std::string &w : extra) key += "// " + w + "\n";
-        const std::string opath = cache_path(key);
-        if (cache_load(opath, code)) return 0;
-        if (offline_compile(src, code, log, extra) == 0) {
-            cache_store(opath, code);
+        const std::string opath = cache_path(key, false);
+        if (cache_load(opath, code) || offline_compile(src, code, log, extra) == 0) {
+            if (compiler) *compiler = POLAR_SC_COMPILER_CLANG;
+            if (!opath.empty()) cache_store(opath, code);
             return 0;
         }
         if (!extra.empty()) {
@@ -906,7 +943,7 @@ int jit_compile(const polar_sc_plan &p)
         p.jit_log = e.what();
         return -ENOTSUP;
     }
-    return rtc_compile(src, p.jit_code, p.jit_log, true);
+    return rtc_compile(src, p.jit_code, p.jit_log, true, &p.jit_compiler);
 }
 
 // Per-mask plans whose LLR_BITS is not the hipcc-built 6: the per-op monitor runs the schedule
@@ -968,6 +1005,8 @@ void code_regs(const polar_sc_plan &p, int &regs, int &regs_seg)
 {
     const char *main = p.pair ? "polar_sc_pair_kernel" : (p.hybrid ? "polar_sc_hybrid_kernel" : "polar_sc_mask_kernel");
     regs = kernel_regs(p.jit_code, main);
+    // hybrid plans launch their traced variant with the same shape
+    if (p.hybrid && regs > 0) regs = std::max(regs, kernel_regs(p.jit_code, "polar_sc_hybrid_trace_kernel"));
     regs_seg = p.pair && !p.pair_tier.steps.empty() ? kernel_regs(p.jit_code, "polar_sc_pair_seg_kernel") : 0;
 }
 

@@ -570,9 +570,14 @@ void upper_call(std::ostringstream &o, const polar_sc_op &op, int wpr)
 // F / G records that fuse into one pop_chain call (polar_sc_pair.h): record i + 1 is F, or G
 // with zero partial sums (the H0 route), on the node record i wrote -- one level down, half the
 // words. At most PAIR_CHAIN_MAX records (2^(D-1) row groups of each operand per column): a
-// noinline chain of 4 records takes ~250 VGPRs, and hipRTC then spills it into AGPRs past the
-// 256 registers a 512-thread launch allows (the dispatch is rejected); 3 records stay at ~160
-// for the whole kernel (tools/check_rtc_registers.py, tests/test_pair.py).
+// noinline chain of 4 records takes the kernel to the full 256 registers of an 8-wave block
+// (torch's hipRTC: 128 VGPRs + 128 AGPRs and 760 B of scratch; the ROCm clang driver: 256
+// VGPRs, 548 B), 3 records stay well below. The round-3 dispatch abort of a chain-4 plan
+// (HSA_STATUS_ERROR_INVALID_ISA) does not recur with either object of the committed source:
+// both dispatch at 8 waves, also with the scratch padded to the aborted dispatch's 812 B
+// (tools/rtc_isa_check.py, tools/isa_dispatch_probe.cpp, profiles/r05_ab/isa_r3_probe.log);
+// what an 8-wave block needs is ceil(8 / 4) x the descriptor's unified register count <= 512,
+// which the launch guard enforces (polar_sc_jit.cpp kernel_regs / fit_waves).
 constexpr int PAIR_CHAIN_MAX = 3;
 int chain_len(const std::vector<polar_sc_op> &ops, size_t i, int cmax)
 {

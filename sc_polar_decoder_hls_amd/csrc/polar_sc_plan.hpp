@@ -80,6 +80,10 @@ constexpr int HYBRID_MAX_WAVES = 8;
 constexpr int PAIR_WAVES_MAX = 8;
 constexpr int PAIR_SUB_WORDS = 256;
 constexpr int SOLO_SUB_WORDS_MAX = 512;   // solo plans: half the registers per word
+// automatic layout: solo while the batch is at most this many frames per SIMD (the solo
+// kernels take ~248 registers, so two waves per SIMD keep one dispatch round; beyond that the
+// pair layout's two frames per wave win -- tools/layout_ab.py, profiles/r05_ab/)
+constexpr int SOLO_FRAMES_PER_SIMD = 2;
 // unified register file per SIMD lane (VGPRs + AGPRs) shared by the waves on the SIMD
 constexpr int SIMD_REGS = 512;
 // one CU's LDS (gfx950)
@@ -145,6 +149,10 @@ struct polar_sc_plan {
     // solo layout of a pair plan (polar_sc_pair.h POLAR_SOLO): one frame per block, a slot row /
     // register = 8 words of the frame (pair: 4 words of two frames)
     int solo = 0;
+    // automatic layout (polar_sc_tuning.layout = 0) of a PAR 16 pair plan: the solo plan of the
+    // same mask, used by decodes whose batch leaves SIMDs idle in the pair layout
+    // (polar_sc_host.cpp layout_for); owned, destroyed with this plan
+    polar_sc_plan *alt = nullptr;
     std::vector<polar_sc_op> pair_ops;
     polar_host::PairTier pair_tier;
     int pair_slot_rows = 0;          // stage-slot rows per pair / solo frame (levels of nodes G/2 .. sub_words)
@@ -155,6 +163,7 @@ struct polar_sc_plan {
     mutable std::mutex host_mu;                             // polar_sc_decode_host staging
     mutable std::map<int, polar_host::HostBufs> host_bufs;
     mutable std::vector<char> jit_code;   // compiled code object (lazily built)
+    mutable uint32_t jit_compiler = 0;    // POLAR_SC_COMPILER_* of jit_code
     mutable std::vector<char> interp_code;   // per-mask plans, llr_bits != 6: traced interpreter
     mutable std::vector<char> code16;        // interpreter on the int16 channel (polar_sc_decode_i16)
     mutable std::string jit_log;

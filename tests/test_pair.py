@@ -15,7 +15,9 @@ from test_gpu_parity import _assert_same
 
 
 def pair(pkg, mask, **tuning):
-    return pkg.Decoder(mask, tuning=dict(tuning, kernel=3))
+    """a pair plan in the frame-pair layout (the automatic layout would decode small batches
+    with its solo alternate, tests/test_solo.py)"""
+    return pkg.Decoder(mask, tuning=dict(dict(layout=1), **tuning, kernel=3))
 
 
 # the plan lists live in the package's build tooling (build() compiles them ahead)
@@ -284,3 +286,32 @@ def test_pair_par64_structured(pkg, cuda, oracle_mod, N, par):
         for sw in (64, 256):
             dec = pkg.Decoder(mask, config=par64_config(pkg, par=par), tuning={"kernel": 3, "sub_words": sw})
             _assert_same(run(pkg, cuda, dec, llr), ref, "PAR %d N=%d rep %d S=%d" % (par, N, rep, sw))
+
+
+def test_launch_info_and_compile_from_two_threads(pkg):
+    """polar_sc_plan_launch_info compiles under the plan lock: launch_info and
+    compile on the same uncompiled plan from two threads agree, and the plan is compiled once
+    (every launch_info reports the same machine code)."""
+    import threading
+    dec = pair(pkg, util.mask("frozen_n_2048_k_1024"), sub_words=32)
+    infos, errs = [], []
+
+    def info():
+        try:
+            infos.append(dec.launch_info(64))
+        except Exception as e:   # pragma: no cover - reported below
+            errs.append(e)
+
+    def comp():
+        try:
+            dec.compile()
+        except Exception as e:   # pragma: no cover
+            errs.append(e)
+
+    ts = [threading.Thread(target=f) for f in (info, comp, info, comp)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    assert len({i["code_key"] for i in infos}) == 1 and infos[0]["regs"] > 0, infos

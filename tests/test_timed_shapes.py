@@ -15,9 +15,11 @@ import pytest
 import util
 from test_gpu_parity import _assert_same
 
-# (mask, frames per GPU, waves per frame pair of the launch)
-SHAPES = [("frozen_n_65536_k_32768", 4096, 1), ("frozen_n_262144_k_131072", 512, 8),
-          ("frozen_n_262144_k_131072", 64, 8)]
+# (mask, frames per GPU, layout, waves per block of the launch): C3 decodes in the frame-pair
+# layout (one block per pair), C5 in the solo layout (one block per frame, subtrees of 512
+# words) -- the automatic layout's choice for those batches on a 256-CU MI355X
+SHAPES = [("frozen_n_65536_k_32768", 4096, 1, 1), ("frozen_n_262144_k_131072", 512, 2, 4),
+          ("frozen_n_262144_k_131072", 64, 2, 8)]
 
 
 def noiseless_batch(torch, mask, batch, seed):
@@ -46,15 +48,18 @@ def awgn_rows(batch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,batch,W", SHAPES)
-def test_timed_shape_full_batch(pkg, cuda, oracle_mod, name, batch, W):
+@pytest.mark.parametrize("name,batch,layout,W", SHAPES)
+def test_timed_shape_full_batch(pkg, cuda, oracle_mod, name, batch, layout, W):
     torch = cuda
     mask = util.mask(name)
     N = mask.size
     dec = pkg.Decoder(mask)
     info = dec.launch_info(batch)
-    # the shape bench.py times: one block per pair, W waves per pair
-    assert (info["kernel"], info["waves_per_block"], info["blocks"]) == (3, W, batch // 2), info
+    # the shape bench.py times: one block per pair (solo: per frame), W waves
+    blocks = batch // 2 if layout == 1 else batch
+    assert (info["kernel"], info["layout"], info["waves_per_block"], info["blocks"]) == (3, layout, W, blocks), info
+    if layout == 2:
+        assert info["sub_words"] == 512, info
     if W == 1:
         # C3: only the subtree-root level in LDS, F-descent chains in the generated kernel
         S = dec.stats["sub_words"]

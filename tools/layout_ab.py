@@ -17,7 +17,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 CONFIGS = {"c3": ("frozen_n_65536_k_32768", 4096), "c5": ("frozen_n_262144_k_131072", 512),
-           "c5_64": ("frozen_n_262144_k_131072", 64), "n16384_4096": ("frozen_n_16384_k_8192", 4096),
+           "c5_64": ("frozen_n_262144_k_131072", 64), "c3_2048": ("frozen_n_65536_k_32768", 2048),
+           "c3_1024": ("frozen_n_65536_k_32768", 1024), "n16384_4096": ("frozen_n_16384_k_8192", 4096),
            "n16384_256": ("frozen_n_16384_k_8192", 256), "n65536_256": ("frozen_n_65536_k_32768", 256)}
 DEFAULT_VARIANTS = "layout=1;layout=2;layout=2,sub_words=512"
 

@@ -32,7 +32,7 @@ DRIVER = r'''
 #include <vector>
 int main()
 {
-    const int N = P_N, batch = P_BATCH, pairs = (batch + 1) / 2, W = P_W;
+    const int N = P_N, batch = P_BATCH, pairs = P_BLOCKS, W = P_W;   // (solo plans: one block per frame)
     std::vector<signed char> h((size_t)batch * N);
     srand(1);
     for (auto &b : h) { int v = 4 + (rand() % 9) - 4 + ((rand() % 7) == 0 ? -8 : 0); b = (signed char)((rand() & 1) ? v : -v); }
@@ -111,7 +111,9 @@ def build(mask_name, batch, tuning, variant=""):
     # launch shape of the library's own decision (polar_sc_plan_launch_info)
     info = dec.launch_info(batch)
     W, lds_row0, lds = info["waves_per_block"], info["lds_row0"], info["lds_bytes"]
-    slot_rows = (G - S) // 4
+    solo = "#define POLAR_SOLO 1" in src
+    slot_rows = (G - S) // (8 if solo else 4)
+    blocks = batch if solo else (batch + 1) // 2
     pair_dwords = st["scratch_bytes_per_wave"] // 4
     # stamp segment 0: after pair_init, after every op
     head = "int lds_row0, int seg)\n{\n"
@@ -146,12 +148,12 @@ def build(mask_name, batch, tuning, variant=""):
     src = src[:i] + "\n".join(lines)
     nst = n + 1
     defs = ("#define NST %d\n#define P_N %d\n#define P_BATCH %d\n#define P_W %d\n#define P_PAIR_DWORDS %d\n"
-            "#define P_SLOT_ROWS %d\n#define P_LDS_ROW0 %d\n#define P_LDS %d\n"
-            % (nst, N, batch, W, pair_dwords, slot_rows, lds_row0, lds))
+            "#define P_SLOT_ROWS %d\n#define P_LDS_ROW0 %d\n#define P_LDS %d\n#define P_BLOCKS %d\n"
+            % (nst, N, batch, W, pair_dwords, slot_rows, lds_row0, lds, blocks))
     tab = ("static const char *LABEL[] = {%s};\nstatic const char *CLASS[] = {%s};\n"
            % (", ".join('"%s"' % s for s in labels), ", ".join('"%s"' % s for s in classes)))
     os.makedirs(OUT, exist_ok=True)
-    tag = "pair_stamps_%s_b%d%s" % (mask_name, batch, "_" + variant if variant else "")
+    tag = "pair_stamps_%s_b%d%s%s" % (mask_name, batch, "_solo" if solo else "", "_" + variant if variant else "")
     path = os.path.join(OUT, tag + ".hip")
     with open(path, "w") as f:
         f.write("#include <hip/hip_runtime.h>\n" + defs + src + tab + DRIVER)
