@@ -31,12 +31,32 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # PMC summaries (tools/profile_gpu.sh + tools/pmc_summary.py) of the current kernels: the HBM
 # bytes they report (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, separate passes) fill
 # roofline.traffic when the benchmarked (mask, frames per GPU) is the profiled one.
-TRAFFIC_PROFILES = {
-    ("FB_N1024_K512", 65536): os.path.join(ROOT, "profiles", "r04_v8_c2_pmc.json"),
-    ("frozen_n_65536_k_32768", 4096): os.path.join(ROOT, "profiles", "r04_v8_c3_pmc.json"),
-    ("frozen_n_262144_k_131072", 512): os.path.join(ROOT, "profiles", "r04_v8_c5_pmc.json"),
-    ("frozen_n_262144_k_131072", 64): os.path.join(ROOT, "profiles", "r04_v8_c5b64_pmc.json"),
-}
+PROFILE_DIR = os.path.join(ROOT, "profiles")
+
+
+def find_traffic_profile(mask_name, per_gpu, key):
+    """The committed PMC summary (profiles/<round>_<tag>_pmc.json, tools/pmc_summary.py) of this
+    workload and machine code: same mask and batch in its launch_info and the same code_key
+    (the hash of the kernels' instructions and descriptors, polar_sc_plan_launch_info); the
+    newest round's when several match. (None, None) if there is none; (None, path) if profiles
+    of the workload exist only for other machine code."""
+    import glob
+    other = None
+    for path in sorted(glob.glob(os.path.join(PROFILE_DIR, "r*_pmc.json")), reverse=True):
+        try:
+            with open(path) as f:
+                prof = json.load(f)
+        except (OSError, ValueError):
+            continue
+        info = prof.get("launch_info") or {}
+        if info.get("mask") != mask_name or info.get("batch") != per_gpu:
+            continue
+        if prof.get("code_key") == key:
+            return prof, path
+        other = other or path
+    return None, other
+
+
 # Rotated input: the timed loop cycles through distinct resident batches of at least this
 # many bytes in total, so the LLR reads come from HBM and not from the 256 MB Infinity Cache
 # (MI355X_MICROARCH.md) that would hold one C2 batch (67 MB).
@@ -63,10 +83,16 @@ CONFIGS = {
 
 
 # kernel that carries the decode for each plan storage class (polar_sc_plan_stats.storage)
-def kernel_name(stats):
-    """The kernel that carries the decode of a plan (polar_sc_plan_stats.kernel / .storage)."""
+def kernel_name(stats, info=None):
+    """The kernel that carries the decode of a plan (polar_sc_plan_stats.kernel / .storage;
+    info: polar_sc_plan_launch_info of the timed batch -- the layout an automatic pair plan
+    takes for it)."""
     if stats["kernel"] == 1:
         return "polar_sc_mask_kernel (per-mask generated kernel)"
+    if stats["kernel"] == 3 and info and info.get("layout") == 2:
+        return ("polar_sc_pair_kernel, solo layout (generated: one frame per wave, eight words per register, "
+                "%d-LLR subtree decoders, upper levels over stage-slot rows; %d waves per frame)"
+                % (16 * info["sub_words"], info["waves_per_block"]))
     if stats["kernel"] == 3:
         k = ("polar_sc_pair_kernel (generated: one frame pair per wave, %d generated %d-LLR subtree decoders, "
              "upper levels over stage-slot rows)" % (stats["n_sub_kinds"], 16 * stats["sub_words"]))
@@ -272,19 +298,16 @@ def roofline_entry(name, N, per_gpu, kern_ms, dec, fmt=None):
     the kernels' instructions and descriptors, polar_sc_plan_launch_info -- equals this plan's)."""
     bytes_per_launch = 1.125 * N * per_gpu
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src, prof, note = None, None, None, None
+    traffic, traffic_src, note = None, None, None
     key = dec.launch_info(per_gpu)["code_key"]
-    prof_path = TRAFFIC_PROFILES.get((name, per_gpu)) if not fmt else None
-    if prof_path and os.path.exists(prof_path):
-        with open(prof_path) as f:
-            prof = json.load(f)
-        if prof.get("code_key") != key:
-            note = "profile %s is of code object %s, this run timed %s: traffic not reported" % (
-                os.path.relpath(prof_path, ROOT), prof.get("code_key"), key)
-            prof = None
-        elif "hbm_read_bytes_corrected" in prof and "hbm_write_bytes" in prof:
-            traffic = prof["hbm_read_bytes_corrected"] + prof["hbm_write_bytes"]
-            traffic_src = os.path.relpath(prof_path, ROOT)
+    prof, prof_path = find_traffic_profile(name, per_gpu, key)
+    if prof is None:
+        note = ("profile %s is of other machine code than this run's %s: traffic not reported"
+                % (os.path.relpath(prof_path, ROOT), key) if prof_path else
+                "no committed PMC profile of this workload's code object %s" % key)
+    elif "hbm_read_bytes_corrected" in prof and "hbm_write_bytes" in prof:
+        traffic = prof["hbm_read_bytes_corrected"] + prof["hbm_write_bytes"]
+        traffic_src = os.path.relpath(prof_path, ROOT)
     ent = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
            "traffic_source": traffic_src, "kernel_ms": kern_ms, "code_key": key,
@@ -329,7 +352,7 @@ def secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mask_name, 
     ent = {"workload": note, "mask": mask_name, "N": N, "K": K, "datapath": dict(fmt), "frames_per_gpu": per_gpu,
            "frames_all_ranks": frames_all, "steps": steps, "warmup": warm, "rotated_batches": nb,
            "ms_per_step": elapsed / steps * 1e3, "info_bits_per_s": frames_all * steps / elapsed * K,
-           "frames_per_sec": frames_all * steps / elapsed, "kernel": kernel_name(dec.stats)}
+           "frames_per_sec": frames_all * steps / elapsed, "kernel": kernel_name(dec.stats, dec.launch_info(per_gpu))}
     ent["roofline"], _ = roofline_entry(mask_name, N, per_gpu, kern_ms, dec, fmt)
     if rank == 0 and args.check > 0:
         from oracle import oracle
@@ -570,7 +593,7 @@ def main():
 
     if rank == 0:
         roof, prof = roofline_entry(name, N, per_gpu, kern_ms, dec)
-        prof_path = TRAFFIC_PROFILES.get((name, per_gpu))
+        prof_path = os.path.join(ROOT, roof["traffic_source"]) if roof.get("traffic_source") else None
         valu = None
         if prof is not None:
             if "valu_insts_per_wave" in prof:
@@ -608,7 +631,7 @@ def main():
             "config": {"workload": desc, "N": N, "K": K, "frames_per_gpu": per_gpu,
                        "mask": name, "parallelism": "frames sharded, dp%d" % world,
                        "rotated_batches": nb, "rotated_bytes": nb * per_gpu * N},
-            "roofline": dict(roof, kernel=kernel_name(dec.stats)),
+            "roofline": dict(roof, kernel=kernel_name(dec.stats, dec.launch_info(per_gpu))),
             "valu_roofline": valu,
             "settle_ms": args.settle_ms,
             "secondary": secondary,

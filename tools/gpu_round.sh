@@ -19,9 +19,9 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
 echo "head $(cat "$ROOT/.head" 2>/dev/null || echo unknown)" > "$OUT/head.txt"
-prof() {   # name mask batch reps
-  local name=$1 mask=$2 batch=$3 reps=$4
-  local DRV="$ROOT/tools/prof_decode.py --mask $mask --batch $batch --reps $reps"
+prof() {   # name mask batch reps [polar_sc_config fields]
+  local name=$1 mask=$2 batch=$3 reps=$4 cfg=${5:-}
+  local DRV="$ROOT/tools/prof_decode.py --mask $mask --batch $batch --reps $reps${cfg:+ --config $cfg}"
   ( cd /tmp && export TMPDIR=/tmp &&
     timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/$name/trace" -o trace --output-format csv -- python3 $DRV > "$OUT/$name/trace.log" 2>&1 &&
     timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/$name/fetch" -o fetch --output-format csv -- python3 $DRV > "$OUT/$name/fetch.log" 2>&1 &&
@@ -44,10 +44,11 @@ for step in "$@"; do
     echo "bench steps20 ok" ;;
   prof)
     for c in "c2 FB_N1024_K512 65536 10" "c3 frozen_n_65536_k_32768 4096 4" "c5 frozen_n_262144_k_131072 512 3" \
-             "c5b64 frozen_n_262144_k_131072 64 3"; do
+             "c5b64 frozen_n_262144_k_131072 64 3" "par16 frozen_n_16384_k_8192 4096 5" \
+             "par64 frozen_n_16384_k_8192 4096 5 par=64" "q8 frozen_n_16384_k_14746 4096 5 llr_bits=8"; do
       set -- $c
       mkdir -p "$OUT/$1"
-      prof "$1" "$2" "$3" "$4"
+      prof "$@"
     done ;;
   benchprof)
     for c in "c2 --config c2" "c3 --config c3" "c5 --config c5" "c5b64 --config c5 --batch 64"; do

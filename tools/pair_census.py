@@ -45,6 +45,48 @@ def classify(label):
     return label.split()[0]
 
 
+def mark_mask_kernel(src):
+    """the per-mask kernel (N <= 1024): markers before every op block of polar_sc_mask_kernel"""
+    out, n, inside = [], 0, False
+    for line in src.split("\n"):
+        if "polar_sc_mask_kernel(" in line:
+            inside = True
+        m = re.match(r"^  \{ // (\S+)(?: level \d+)? n (\d+)", line) or re.match(r"^  \{ // ([FG]\+leaf)", line)
+        if inside and m:
+            if "leaf" in m.group(1):
+                label = "leaf"
+            else:
+                kind, nn = m.group(1), int(m.group(2))
+                label = "%s n%s" % ("H" if kind == "H0" else kind, nn if nn < 8 else "8+")
+            out.append('  asm volatile(";@@ %s"); __builtin_amdgcn_sched_barrier(0);' % label)
+            n += 1
+        out.append(line)
+    return "\n".join(out), n
+
+
+def mask_census(asm):
+    valu, allc = collections.Counter(), collections.Counter()
+    cur, cls = False, "prologue"
+    for line in asm.split("\n"):
+        if re.match(r"^polar_sc_mask_kernel:", line):
+            cur = True
+            continue
+        if not cur:
+            continue
+        if re.match(r"^\.Lfunc_end", line):
+            break
+        m = re.match(r"^\s*;@@ (.*)$", line)
+        if m:
+            cls = m.group(1).strip()
+            continue
+        m = re.match(r"^\s+([sv]_\w+|ds_\w+|global_\w+|buffer_\w+|scratch_\w+|flat_\w+)\b", line)
+        if m:
+            allc[cls] += 1
+            if m.group(1).startswith("v_"):
+                valu[cls] += 1
+    return valu, allc
+
+
 def mark(src):
     out, n = [], 0
     in_sub = False
@@ -134,6 +176,16 @@ def main():
     tun = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in args.tuning.split(",") if kv)
     dec = pkg.Decoder(util.mask(args.mask), tuning=tun or None)
     src = open(args.source).read() if args.source else dec.kernel_source()
+    if "polar_sc_mask_kernel(" in src:   # per-mask kernel: one straight-line function
+        marked, nmark = mark_mask_kernel(src)
+        with tempfile.TemporaryDirectory() as tmp:
+            tot_v, tot_a = mask_census(compile_asm(marked, tmp))
+        nv = sum(tot_v.values())
+        print("%s: per-mask kernel, %d op markers; VALU per wave %d, all instructions %d"
+              % (args.mask, nmark, nv, sum(tot_a.values())))
+        for c, v in sorted(tot_v.items(), key=lambda kv: -kv[1]):
+            print("%-14s %10d %5.1f%% %10d" % (c, v, 100.0 * v / max(nv, 1), tot_a[c]))
+        return
     calls = collections.Counter(int(m) for m in re.findall(r"polar_psub_(\d+)\(c\.slot_ptr", src.split("polar_sc_pair_subtest_kernel")[0]))
     marked, nmark = mark(src)
     with tempfile.TemporaryDirectory() as tmp:
