@@ -299,7 +299,8 @@ def roofline_entry(name, N, per_gpu, kern_ms, dec, fmt=None):
     bytes_per_launch = 1.125 * N * per_gpu
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src, note = None, None, None
-    key = dec.launch_info(per_gpu)["code_key"]
+    info = dec.launch_info(per_gpu)
+    key = info["code_key"]
     prof, prof_path = find_traffic_profile(name, per_gpu, key)
     if prof is None:
         note = ("profile %s is of other machine code than this run's %s: traffic not reported"
@@ -311,6 +312,9 @@ def roofline_entry(name, N, per_gpu, kern_ms, dec, fmt=None):
     ent = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
            "traffic_source": traffic_src, "kernel_ms": kern_ms, "code_key": key,
+           # which compiler built the timed kernel: the ROCm clang driver (prewarmed code
+           # objects) or hipRTC (a cache miss on this machine)
+           "compiler": {1: "ROCm clang driver", 2: "hipRTC"}.get(info.get("compiler"), None),
            "algorithmic_bytes_per_launch": bytes_per_launch}
     if note:
         ent["traffic_note"] = note

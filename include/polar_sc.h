@@ -110,6 +110,11 @@ typedef struct polar_sc_tuning {
                                  (one frame per wave, the halves carry words 8 j + 4 h + r:
                                  eight words per register, half the instructions per frame on
                                  nodes of >= 16 words; PAR 16 only) */
+    int32_t sub_root;         /* pair plans: where a generated subtree decoder reads its root.
+                                 0 = automatic (as 2 when the plan has upper levels above the
+                                 subtrees' parents), 1 = from a stage slot written by the
+                                 upper-level F / G, 2 = as F / G of its parent's slot rows
+                                 (the subtree-root level then needs no slot) */
 } polar_sc_tuning;
 
 /* Immutable decode plan: N, config, frozen mask, compiled decode schedule and its device

@@ -56,7 +56,7 @@ class polar_sc_tuning(ctypes.Structure):
     """Kernel selection / launch shape of a plan (include/polar_sc.h); all 0 = automatic."""
     _fields_ = [(n, ctypes.c_int32) for n in (
         "kernel", "waves_per_group", "sub_words", "tier_words", "lds_slots", "hybrid_waves", "chain_max",
-        "sub_inline", "layout")]
+        "sub_inline", "layout", "sub_root")]
 
 
 def make_tuning(tuning):

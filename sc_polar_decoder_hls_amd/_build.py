@@ -72,8 +72,15 @@ def build(force=False, verbose=False):
     # (polar_sc_jit.cpp offline_compile)
     hc = shutil.which(hipcc()) or hipcc()
     clang = os.path.join(os.path.dirname(os.path.dirname(os.path.realpath(hc))), "lib", "llvm", "bin", "clang++")
+    # the driver's version text, fixed at library build time: part of the cache key of the
+    # objects it builds (identical on every machine the library and its cache travel to)
+    try:
+        ver = subprocess.run([clang, "--version"], capture_output=True, text=True, timeout=60).stdout.split("\n")[0]
+    except (OSError, subprocess.SubprocessError):
+        ver = "unknown"
+    ver = "".join(ch for ch in ver if ch.isalnum() or ch in " .-_()/+:")
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           '-DPOLAR_ROCM_CLANG="%s"' % clang,
+           '-DPOLAR_ROCM_CLANG="%s"' % clang, '-DPOLAR_ROCM_CLANG_VERSION="%s"' % ver,
            "-I" + os.path.join(ROOT, "include"), "-I" + GEN_DIR] + SOURCES + ["-o", tmp, "-lhiprtc"]
     if verbose:
         print(" ".join(cmd))

@@ -95,7 +95,9 @@ def gpu_plans():
             ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), dict(p)),
             ("frozen_n_262144_k_131072", mask("frozen_n_262144_k_131072"), dict(p, tier_words=1024)),
             ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, lds_slots=256)),
-            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, lds_slots=1024))]
+            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, lds_slots=1024)),
+            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, sub_root=1)),
+            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), {"kernel": 3, "layout": 2, "sub_root": 1})]
     for wpg in (1, 2, 4, 8):
         out += [("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"), dict(p, waves_per_group=wpg, sub_words=64)),
                 ("wave_mask", wave_mask(), dict(p, waves_per_group=wpg, sub_words=64))]
@@ -150,8 +152,10 @@ def gpu_par64_plans():
 def cpu_test_plans():
     """(name, mask, tuning) of the plans the CPU register-budget test compiles (the round-3
     dispatch abort's configuration: chain_max = 4 on the structured N = 32768 mask)."""
-    return [("struct32768_0", struct_masks(32768)[0], {"kernel": 3, "layout": 1, "sub_words": sw, "chain_max": 4})
-            for sw in (64, 256)]
+    return [("struct32768_0", struct_masks(32768)[0], {"kernel": 3, "layout": 1, "sub_words": sw, "chain_max": 4,
+                                                       "sub_root": 1}) for sw in (64, 256)] + \
+        [("struct16384_0", struct_masks(16384)[0], {"kernel": 3, "layout": 1, "sub_words": 64, "chain_max": 4,
+                                                    "sub_root": 1})]
 
 
 # ---- datapath formats (tests/test_gpu_formats.py): (PAR, SIGMAG, EXTENDED, LLR_BITS) ---------

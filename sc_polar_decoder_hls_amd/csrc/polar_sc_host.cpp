@@ -479,7 +479,8 @@ bool tuning_valid(const polar_sc_tuning &t)
            t.tier_words >= -1 && (t.tier_words <= 0 || pow2(t.tier_words)) &&
            (t.lds_slots == 0 || t.lds_slots == 256 || t.lds_slots == 512 || t.lds_slots == 1024) &&
            (t.hybrid_waves == 0 || t.hybrid_waves == 4 || t.hybrid_waves == 8) && t.chain_max >= 0 &&
-           t.chain_max <= 4 && t.sub_inline >= 0 && t.sub_inline <= 2 && t.layout >= 0 && t.layout <= 2;
+           t.chain_max <= 4 && t.sub_inline >= 0 && t.sub_inline <= 2 && t.layout >= 0 && t.layout <= 2 &&
+           t.sub_root >= 0 && t.sub_root <= 2;
 }
 
 int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
@@ -898,13 +899,41 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         sc.words = (uint32_t)S;
         compile_node(*p, p->pair_ops, 0, 0, p->GP, true, &sc);
         emit(p->pair_ops, POLAR_OP_END, 0, 0, 0, -1, 0);
+        // Subtree roots without a slot level: the F / G record that writes a subtree's root
+        // (always the record right before its SUB, compile_node) is folded into the SUB, whose
+        // generated decoder then reads the root as F / G of the parent's slot rows
+        // (polar_sc_pairgen.cpp CHF / CHG). The subtree-root level (S words) then needs no
+        // slot: one level less in the slot rows, and the LDS it held takes the next level up
+        // (C3: the 512-word level on chip, 6 N instead of 8 N of HBM traffic per frame). Not
+        // for subtrees that are children of the root (G = 2 S: their parent is the channel).
+        const bool fuse = t.sub_root != 1 && (int)p->G / 2 > S;
+        if (fuse) {
+            std::vector<polar_sc_op> fused;
+            const std::vector<polar_sc_op> &ops = p->pair_ops;
+            for (size_t i = 0; i < ops.size(); i++) {
+                const polar_sc_op &o = ops[i];
+                if (i + 1 < ops.size() && (o.code == POLAR_OP_F || o.code == POLAR_OP_G) && o.n == S &&
+                    ops[i + 1].code == polar_host::POLAR_OP_SUB && ops[i + 1].level == o.level + 1 &&
+                    ops[i + 1].pos == o.pos) {
+                    polar_sc_op sub = ops[i + 1];
+                    sub.reserved[1] = o.code == POLAR_OP_F ? 1 : 2;   // the folded producer
+                    sub.upos = o.code == POLAR_OP_G ? o.upos : -1;
+                    fused.push_back(sub);
+                    i++;
+                } else {
+                    fused.push_back(o);
+                }
+            }
+            p->pair_ops.swap(fused);
+        }
+        p->pair_fused = fuse ? 1 : 0;
         p->pair = 1;
         p->sub_words = S;
         p->subs = std::move(sc.lists);
         s.sub_words = (uint32_t)S;
         s.n_sub_kinds = (uint32_t)p->subs.size();
         s.n_sub_calls = sc.calls;
-        p->pair_slot_rows = ((int)p->G - S) / p->wpr();
+        p->pair_slot_rows = ((int)p->G - (p->pair_fused ? 2 * S : S)) / p->wpr();
         p->pair_dwords = p->pair_slot_rows * 32 + std::max<int>(1, (int)p->G / (16 * p->wpr())) * 64;
         if (t.tier_words > 0) {
             if (t.tier_words <= S) {
@@ -927,6 +956,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
             }
             p->pair = 0;
             p->solo = 0;
+            p->pair_fused = 0;
             p->sub_words = 0;
             p->subs.clear();
             p->pair_ops.clear();
@@ -998,7 +1028,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         s.storage = 1u;
         s.tier_steps = (uint32_t)p->pair_tier.steps.size();
         s.tier_words = (uint32_t)p->pair_tier.tw;
-        s.lds_bytes_per_wave = (uint32_t)(p->sub_words / p->wpr()) * 128u;
+        s.lds_bytes_per_wave = (uint32_t)((p->pair_fused ? 2 : 1) * p->sub_words / p->wpr()) * 128u;
         s.scratch_bytes_per_wave = (uint64_t)p->pair_dwords * 4u;
     }
     // automatic layout: a PAR 16 pair plan also holds its solo plan (subtrees of up to 512

@@ -793,13 +793,18 @@ std::vector<std::string> extra_clang_flags()
     return out;
 }
 
-// identity of the clang driver for the cache key of its objects: path, size and mtime of the
-// binary (the hipRTC version says nothing about the compiler that built them)
-std::string clang_identity(const std::string &clang)
+// identity of the clang driver for the cache key of its objects (the hipRTC
+// version says nothing about the compiler that built them): the driver's path and version text
+// as the library build found them (_build.py). Not the binary's size or mtime: the cache travels
+// with the library to GPU boxes of the same image, whose files need not carry the same mtimes
+// -- a key that differed there made every decode fall back to hipRTC code (round 5, r05_v1).
+std::string clang_identity()
 {
-    struct stat st {};
-    if (clang.empty() || stat(clang.c_str(), &st) != 0) return "no clang";
-    return clang + " " + std::to_string((long long)st.st_size) + " " + std::to_string((long long)st.st_mtime);
+#if defined(POLAR_ROCM_CLANG) && defined(POLAR_ROCM_CLANG_VERSION)
+    return std::string(POLAR_ROCM_CLANG) + " " + POLAR_ROCM_CLANG_VERSION;
+#else
+    return "no clang";
+#endif
 }
 
 // seconds a child compile may take before it is killed and hipRTC builds the kernel instead
@@ -880,7 +885,7 @@ int rtc_compile(const std::string &src, std::vector<char> &code, std::string &lo
     if (compiler) *compiler = POLAR_SC_COMPILER_HIPRTC;
     if (whole) {
         const std::vector<std::string> extra = extra_clang_flags();
-        std::string key = src + "\n// offline clang driver: " + clang_identity(rocm_clang()) + "\n";
+        std::string key = src + "\n// offline clang driver: " + clang_identity() + "\n";
         for (const std::string &w : extra) key += "// " + w + "\n";
         const std::string opath = cache_path(key, false);
         if (cache_load(opath, code) || offline_compile(src, code, log, extra) == 0) {
@@ -1162,7 +1167,9 @@ PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, in
     // LDS: levels of nodes S .. L words ((2 L - S) / wpr slot rows of 128 B) + the SPC exchange
     // (3 W rows of 256 B)
     const long budget = CU_LDS_BYTES / (per_cu > 0 ? per_cu : 1) - 3l * W * 256l;
-    const int S = p.sub_words, G = (int)p.G, wpr = p.wpr();
+    // (S: the smallest slot level -- the subtree roots, or their parents when the roots are
+    // read as F / G of them, pair_fused)
+    const int S = p.pair_fused ? 2 * p.sub_words : p.sub_words, G = (int)p.G, wpr = p.wpr();
     const long bpw = 128 / wpr;   // slot bytes per word
     int L = 0;
     for (int w = S; w <= G / 2; w *= 2) {

@@ -15,6 +15,7 @@
 #include "polar_sc_plan.hpp"
 
 #include <map>
+#include <set>
 #include <stdexcept>
 #include <sstream>
 #include <string>
@@ -509,12 +510,23 @@ struct PairGen {
     // subtree decoder `id`: root words from the slot dwords at src_ (rows j, j + 1: CH), partial sums to
     // the pair's bit dwords from local word l0
     // inl: inlined at its call sites (polar_sc_tuning.sub_inline = 2) instead of a call
-    void sub_function(int id, bool inl)
+    // kind: where the root words come from (CH(j), defined before the function): 0 = the
+    // root's stage slot at src_; 1 / 2 = F / G of the parent's slot rows at src_ (G: the partial
+    // sums of the left sibling from local word ub_, -1 = zero)
+    void sub_function(int id, bool inl, int kind = 0)
     {
         const int words = 1 << LG, R = regs(LG), lw = words / wpr, nbw = lw >= 16 ? lw / 16 : 1;   // lw: local words
+        const int nq = words / wpr;   // rows of the root node (the parent has 2 nq)
+        o << "#undef CH\n";
+        if (kind == 0) o << "#define CH(j) prow(SLOT(j), ((j) & 1) != 0)\n";
+        else if (kind == 1) o << "#define CH(j) prow(fg4<false>(SLOT(j), SLOT((j) + " << nq << "), 0u), ((j) & 1) != 0)\n";
+        else
+            o << "#define CH(j) prow(fg4<true>(SLOT(j), SLOT((j) + " << nq << "), ub_ >= 0 ? ubits4(hb_[((ub_ + ((j) & ~1)) >> 4) * 64], "
+              << "ub_ + ((j) & ~1)) : 0u), ((j) & 1) != 0)\n";
         // (plain arguments: a PairCtx passed by reference would live on the private stack)
         o << "__device__ " << (inl ? "__forceinline__" : "__noinline__") << " void polar_psub_" << id
-          << "(const u32 *src_, g_u32 *hb_, int l0)\n{\n"
+          << (kind == 1 ? "_F" : kind == 2 ? "_G" : "") << "(const u32 *src_, g_u32 *hb_, int l0"
+          << (kind == 2 ? ", int ub_" : "") << ")\n{\n"
           << "  const u32 lane_ = threadIdx.x & 63u;\n  Lanes ln; ln.init(lane_ & 15u);\n"
           << "  struct { u32 row; } c; c.row = lane_ >> 4;\n  u32 bw[" << nbw << "] = {};\n";
         bool split_root = false;   // REP / R1 / SPC children of the root read split root words
@@ -540,7 +552,9 @@ struct PairGen {
 };
 // a root word of a subtree decoder: row j of its stage slot (row-pair dwords, SM8) -> SM16
 // partial-sum dword d of the subtree to the pair's bits (masked: subtrees of < 64 words)
-const char *const kPairCH = "#define CH(j) prow(src_[((j) >> 3) * 256 + (((j) >> 1) & 3)], ((j) & 1) != 0)\n"
+// SLOT(j): the slot dword of rows j & ~1, (j & ~1) + 1 (row pairs, 8-row groups); CH(j): a root
+// row of a subtree decoder (defined per decoder variant, PairGen::sub_function)
+const char *const kPairCH = "#define SLOT(j) src_[((j) >> 3) * 256 + (((j) >> 1) & 3)]\n"
                             "#define BST(d, v) (hb_[((l0 >> 4) + (d)) * 64] = (v))\n"
                             "#define BSTM(m, v) (hb_[(l0 >> 4) * 64] = (hb_[(l0 >> 4) * 64] & ~((m) << (l0 & 15))) | \\\n"
                             "    (((v) << (l0 & 15)) & ((m) << (l0 & 15))))\n";
@@ -560,7 +574,12 @@ void upper_call(std::ostringstream &o, const polar_sc_op &op, int wpr)
     case POLAR_OP_H: o << "pop_h<false>(c, " << l0 << ", " << n4 << ");"; break;
     case POLAR_OP_H0: o << "pop_h<true>(c, " << l0 << ", " << n4 << ");"; break;
     case POLAR_OP_SUB:
-        o << "if (c.lead()) polar_psub_" << op.fb << "(c.slot_ptr(c.lvl_row(" << op.level << ")), c.hb, " << l0 << ");";
+        if (op.reserved[1] == 0)
+            o << "if (c.lead()) polar_psub_" << op.fb << "(c.slot_ptr(c.lvl_row(" << op.level << ")), c.hb, " << l0 << ");";
+        else   // the root as F / G of the parent's slot rows (pair_fused)
+            o << "if (c.lead()) polar_psub_" << op.fb << (op.reserved[1] == 1 ? "_F" : "_G") << "(c.slot_ptr(c.lvl_row("
+              << op.level - 1 << ")), c.hb, " << l0 << (op.reserved[1] == 2 ? ", " + std::to_string(ub) : std::string())
+              << ");";
         break;
     default: throw std::runtime_error("pairgen: unexpected upper op");
     }
@@ -668,9 +687,16 @@ std::string pair_source(const polar_sc_plan &p)
       << "namespace polar {\n" << kPairCH;
     int lg = 0;
     while ((1 << lg) < p.sub_words) lg++;
-    for (size_t id = 0; id < p.subs.size(); id++) {
-        PairGen g(p.subs[id], lg, solo);
-        g.sub_function((int)id, p.tune.sub_inline == 2);
+    // the decoder variants the kernels call (SUB records: reserved[1] = root kind), and the
+    // subtest kernel's (kind 1 of a fused plan: its root rows fed through F with +QMAG)
+    std::set<std::pair<int, int>> need;
+    for (const std::vector<polar_sc_op> *ops : {&p.pair_ops, &p.pair_tier.seg_ops})
+        for (const polar_sc_op &op : *ops)
+            if (op.code == POLAR_OP_SUB) need.insert({(int)op.fb, op.reserved[1]});
+    for (size_t id = 0; id < p.subs.size(); id++) need.insert({(int)id, p.pair_fused ? 1 : 0});
+    for (const auto &v : need) {
+        PairGen g(p.subs[v.first], lg, solo);
+        g.sub_function(v.first, p.tune.sub_inline == 2, v.second);
         o << g.o.str();
     }
     o << "}  // namespace polar\nusing namespace polar;\n";
@@ -680,12 +706,17 @@ std::string pair_source(const polar_sc_plan &p)
     // test hook (polar_sc_debug_subtree): subtree decoder `id` on 64 lanes of root slot rows
     // in[64 j + lane] (u16 SM8 pairs, repacked into row-pair dwords in LDS), its partial-sum
     // dwords to out[64 d + lane]
+    // (fused plans: the decoder reads its root as F of parent rows = [the root rows; +QMAG],
+    // which gives back the root rows exactly, -0 included)
     const int rp = p.sub_words / wpr / 2;   // row-pair dwords of the root slot
+    const int tot = p.pair_fused ? 2 * rp : rp;
     o << "extern \"C\" __global__ void __launch_bounds__(64) polar_sc_pair_subtest_kernel(\n"
       << "    const unsigned short *__restrict__ in, unsigned int *__restrict__ out, int id)\n{\n"
-      << "  __shared__ unsigned int rows_[" << (rp < 4 ? 4 : rp) << " * 64];\n"
-      << "  const int lane = threadIdx.x & 63;\n"
-      << "  for (int i = 0; i < " << rp << "; i++) {\n"
+      << "  __shared__ unsigned int rows_[" << (tot < 4 ? 4 : tot) << " * 64];\n"
+      << "  const int lane = threadIdx.x & 63;\n";
+    if (p.pair_fused)
+        o << "  for (int i = " << rp << "; i < " << tot << "; i++) rows_[(i >> 2) * 256 + 4 * lane + (i & 3)] = QMAG * 0x01010101u;\n";
+    o << "  for (int i = 0; i < " << rp << "; i++) {\n"
       << "    const unsigned int r0 = in[128 * i + lane], r1 = in[128 * i + 64 + lane];\n"
       << "    rows_[(i >> 2) * 256 + 4 * lane + (i & 3)] = (r0 & 0xFFu) | ((r1 & 0xFFu) << 8) | ((r0 >> 8) << 16) |\n"
       << "                                                ((r1 >> 8) << 24);\n"
@@ -693,7 +724,7 @@ std::string pair_source(const polar_sc_plan &p)
       << "  const unsigned int *src = rows_ + 4 * lane;\n"
       << "  switch (id) {\n";
     for (size_t id = 0; id < p.subs.size(); id++)
-        o << "  case " << id << ": polar_psub_" << id << "(src, (g_u32 *)out + lane, 0); return;\n";
+        o << "  case " << id << ": polar_psub_" << id << (p.pair_fused ? "_F" : "") << "(src, (g_u32 *)out + lane, 0); return;\n";
     o << "  default: return;\n  }\n}\n";
     if (!p.pair_tier.steps.empty()) {
         pair_kernel(o, "polar_sc_pair_seg_kernel", p.pair_tier.seg_ops, cmax, solo);

@@ -155,7 +155,10 @@ struct polar_sc_plan {
     polar_sc_plan *alt = nullptr;
     std::vector<polar_sc_op> pair_ops;
     polar_host::PairTier pair_tier;
-    int pair_slot_rows = 0;          // stage-slot rows per pair / solo frame (levels of nodes G/2 .. sub_words)
+    // subtree roots read as F / G of their parent's slot rows (SUB records carry the folded
+    // producer in reserved[1]: 1 = F, 2 = G with upos); the subtree-root level has no slot
+    int pair_fused = 0;
+    int pair_slot_rows = 0;          // stage-slot rows per pair / solo frame (levels of nodes G/2 .. sub_words, or 2 sub_words when fused)
     int pair_dwords = 0;             // HBM scratch per pair / frame: slot rows (128 B) + bit dwords (256 B)
     int wpr() const { return solo ? 8 : 4; }   // words of one (virtual) frame per slot row
     mutable std::mutex mu;

@@ -467,7 +467,14 @@ def _assign(lhs, op, rhs):
 def transpile_sub(src, sid):
     """Python source of subtree decoder `sid` of a generated pair source: a function
     sub_<sid>(CH, BST, BSTM, ln, c)."""
-    start = src.index("void polar_psub_%d(" % sid)
+    # (fused plans have only the variants that read the root as F / G of the parent, _F / _G;
+    # their bodies are the same code on CH(j), which the emulation supplies)
+    for name in ("void polar_psub_%d(" % sid, "void polar_psub_%d_F(" % sid, "void polar_psub_%d_G(" % sid):
+        if name in src:
+            start = src.index(name)
+            break
+    else:
+        raise ValueError("pair_emu: no decoder %d in the source" % sid)
     body_start = src.index("{", start) + 1
     depth, i = 1, body_start
     while depth:
@@ -571,12 +578,12 @@ def _upper_ops(src):
     k0 = src.index("polar_sc_pair_kernel(")
     body = src[k0:src.index("pair_out(", k0)]
     ops = []
-    for m in re.finditer(r"(pop_fg_split<(\w+)>|pop_rep|pop_r1spc<(\w+)>|pop_h<(\w+)>|polar_psub_(\d+)|"
+    for m in re.finditer(r"(pop_fg_split<(\w+)>|pop_rep|pop_r1spc<(\w+)>|pop_h<(\w+)>|polar_psub_(\d+)(?:_([FG]))?|"
                          r"pop_chain<(\d+), (\w+), (\w+)>)\(([^;]*)\);", body):
-        args = [a.strip() for a in _split_top(m.group(9))]
+        args = [a.strip() for a in _split_top(m.group(10))]
         if m.group(1).startswith("pop_chain"):
             # a fused descent: record 0 (F, or G with partial sums at ub), then F / zero-u G
-            d, isg0 = int(m.group(6)), m.group(8) == "true"
+            d, isg0 = int(m.group(7)), m.group(9) == "true"
             k, n4, ub, gm = int(args[1]), int(args[2]), int(args[3]), int(args[4].rstrip("u"))
             ops.append(("G" if isg0 else "F", k, n4, ub))
             for i in range(1, d):
@@ -591,7 +598,15 @@ def _upper_ops(src):
             ops.append(("H0" if m.group(4) == "true" else "H", int(args[1]), int(args[2])))
         else:
             lvl = int(re.search(r"lvl_row\((\d+)\)", args[0]).group(1))
-            ops.append(("SUB", int(m.group(5)), lvl, int(args[2])))
+            if m.group(6):
+                # the subtree root as F / G of its parent's slot rows (pair_fused): that
+                # record, restated, then the decoder on the root level
+                isg = m.group(6) == "G"
+                nq = None   # (the decoder's root rows: half the parent's, filled in _decode_pair)
+                ops.append(("FG_ROOT", isg, lvl, int(args[3]) if isg else -1))
+                ops.append(("SUB", int(m.group(5)), lvl + 1, int(args[2])))
+            else:
+                ops.append(("SUB", int(m.group(5)), lvl, int(args[2])))
     return ops
 
 
@@ -627,6 +642,12 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
 
     for op in upper:
         kind = op[0]
+        if kind == "FG_ROOT":
+            # the parent level's slot holds 2 nq rows; the root level gets F / G of its halves
+            _, isg, k, ub = op
+            nq = len(slots[k]) // 2
+            op = ("G" if isg else "F", k, nq, ub)
+            kind = op[0]
         if kind in ("F", "G"):
             _, k, n4, ub = op
             outk = []

@@ -43,7 +43,7 @@ def test_tuning_validation_and_no_environment(pkg, monkeypatch):
     for bad in ({"kernel": 4}, {"waves_per_group": 3}, {"waves_per_group": 32}, {"sub_words": 1024},
                 {"tier_words": -2}, {"tier_words": 1000}, {"lds_slots": 300}, {"hybrid_waves": 16},
                 {"chain_max": 5}, {"chain_max": -1}, {"sub_inline": 3}, {"sub_inline": -1}, {"layout": 3},
-                {"layout": -1}):
+                {"layout": -1}, {"sub_root": 3}, {"sub_root": -1}):
         with pytest.raises(pkg.PolarError) as e:
             pkg.Decoder(m, tuning=bad)
         assert e.value.rc == -22, bad
@@ -72,9 +72,11 @@ def test_tuning_validation_and_no_environment(pkg, monkeypatch):
     txt = open(os.path.join(util.ROOT, "sc_polar_decoder_hls_amd", "csrc", "polar_sc_host.cpp")).read()
     assert re.findall(r'getenv\("(\w+)"\)', txt) == ["POLAR_SC_VERBOSE"]   # error detail on stderr only
     txt = open(os.path.join(util.ROOT, "sc_polar_decoder_hls_amd", "csrc", "polar_sc_jit.cpp")).read()
-    # the cache directory, and extra clang flags for compiler A/Bs (part of the cache key, so the
-    # machine code -- and polar_sc_plan_launch_info's code_key -- says which flags built it)
-    assert sorted(re.findall(r'getenv\("(\w+)"\)', txt)) == ["POLAR_SC_CLANG_FLAGS", "POLAR_SC_RTC_CACHE"]
+    # the cache directory, extra clang flags for compiler A/Bs (part of the cache key, so the
+    # machine code -- and polar_sc_plan_launch_info's code_key -- says which flags built it), and
+    # the time a child compile may take before hipRTC builds the kernel instead
+    assert sorted(re.findall(r'getenv\("(\w+)"\)', txt)) == ["POLAR_SC_CLANG_FLAGS", "POLAR_SC_CLANG_TIMEOUT",
+                                                              "POLAR_SC_RTC_CACHE"]
 
 
 def test_default_config_is_reference(pkg):

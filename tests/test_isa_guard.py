@@ -35,7 +35,8 @@ def _fits(regs, W):
 def test_guard_matches_register_condition_both_compilers(pkg):
     ric = _ric()
     from sc_polar_decoder_hls_amd._plansets import struct_masks
-    dec = pkg.Decoder(struct_masks(16384)[0], tuning={"kernel": 3, "layout": 1, "sub_words": 64, "chain_max": 4})
+    dec = pkg.Decoder(struct_masks(16384)[0], tuning={"kernel": 3, "layout": 1, "sub_words": 64, "chain_max": 4,
+                                                      "sub_root": 1})   # (round 3: roots in a slot level)
     src = dec.kernel_source()
     assert "pop_chain<4" in src
     objs = {"clang": ric.clang_compile(src), "torch_hiprtc": ric.hiprtc_compile(ric.torch_hiprtc(), src)[0]}

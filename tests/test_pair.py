@@ -35,8 +35,13 @@ def test_pair_plan_stats(pkg):
     s = pair(pkg, util.mask("frozen_n_65536_k_32768")).stats
     assert (s["kernel"], s["sub_words"], s["storage"]) == (3, 256, 1)
     assert s["n_sub_calls"] >= s["n_sub_kinds"] > 0 and s["tier_steps"] == 0
-    # per pair: (G - S) / 4 slot rows of 128 B + G / 64 bit rows of 256 B
-    assert s["scratch_bytes_per_wave"] == (4096 - 256) // 4 * 128 + 4096 // 64 * 256
+    # per pair: (G - 2 S) / 4 slot rows of 128 B (subtree roots read as F / G of their parents)
+    # + G / 64 bit rows of 256 B; with the roots in a slot level of their own, (G - S) / 4
+    assert s["scratch_bytes_per_wave"] == (4096 - 512) // 4 * 128 + 4096 // 64 * 256
+    s1 = pair(pkg, util.mask("frozen_n_65536_k_32768"), sub_root=1).stats
+    assert s1["scratch_bytes_per_wave"] == (4096 - 256) // 4 * 128 + 4096 // 64 * 256
+    assert "_F(c.slot_ptr" in pair(pkg, util.mask("frozen_n_65536_k_32768")).kernel_source()
+    assert "_F(c.slot_ptr" not in pair(pkg, util.mask("frozen_n_65536_k_32768"), sub_root=1).kernel_source()
     s = pair(pkg, util.mask("frozen_n_2048_k_1024")).stats
     assert s["sub_words"] == 64
     s = pair(pkg, util.mask("frozen_n_262144_k_131072"), tier_words=1024).stats
@@ -169,6 +174,19 @@ def test_pair_grid_tier(pkg, cuda, oracle_mod, batch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", [1, 2])
+def test_subtree_root_slot_vs_fused(pkg, cuda, oracle_mod, layout):
+    """Subtree roots from a slot level of their own (sub_root 1) and as F / G of the parent's
+    slot rows (the default): equal on every frame of a C3-sized sample, equal to the oracle."""
+    mask = util.mask("frozen_n_65536_k_32768")
+    llr, _ = util.synth_frames(mask, 6, ebn0_db=1.0, seed=31)
+    a = run(pkg, cuda, pair(pkg, mask, layout=layout), llr)
+    b = run(pkg, cuda, pair(pkg, mask, layout=layout, sub_root=1), llr)
+    _assert_same(a, b, "fused vs slot roots, layout %d" % layout)
+    _assert_same(a, oracle_mod.decode_fsm(mask, llr), "fused roots vs oracle, layout %d" % layout)
+
+
+@pytest.mark.gpu
 def test_pair_c5_sample(pkg, cuda, oracle_mod):
     mask = util.mask("frozen_n_262144_k_131072")
     llr, _ = util.synth_frames(mask, 3, ebn0_db=1.0, seed=5)
@@ -206,8 +224,9 @@ def test_pair_register_budget(pkg):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import check_rtc_registers as cr
     cache = os.path.join(os.path.dirname(pkg._build.LIB), "rtc_cache")
-    plans = [(util.mask("frozen_n_262144_k_131072"), {}), (struct_masks(32768)[0], {"sub_words": 64, "chain_max": 4}),
-             (struct_masks(32768)[0], {"sub_words": 256, "chain_max": 4})]
+    plans = [(util.mask("frozen_n_262144_k_131072"), {}),
+             (struct_masks(32768)[0], {"sub_words": 64, "chain_max": 4, "sub_root": 1}),
+             (struct_masks(32768)[0], {"sub_words": 256, "chain_max": 4, "sub_root": 1})]
     for m, tun in plans:
         dec = pair(pkg, m, **tun)
         for batch in (9, 64, 4096, 40001):
@@ -223,7 +242,7 @@ def test_pair_register_budget(pkg):
         assert not cr.over_budget(vgpr, 0, wg)[0]
     # an automatic 8-wave launch (small batch) of the chain_max = 4 kernel: 2 waves of 256
     # registers per SIMD
-    info = pair(pkg, struct_masks(32768)[0], sub_words=64, chain_max=4).launch_info(9)
+    info = pair(pkg, struct_masks(32768)[0], sub_words=64, chain_max=4, sub_root=1).launch_info(9)
     assert (info["regs"], info["waves_per_block"]) == (256, 8), info
 
 

@@ -34,9 +34,10 @@ def test_solo_plan_stats(pkg):
     d = solo(pkg, m)
     s = d.stats
     assert (s["kernel"], s["sub_words"], s["storage"]) == (3, 256, 1)
-    # per frame: (G - S) / 8 slot rows of 128 B + G / 128 bit rows of 256 B
-    assert s["scratch_bytes_per_wave"] == (4096 - 256) // 8 * 128 + 4096 // 128 * 256
-    assert s["lds_bytes_per_wave"] == 256 // 8 * 128
+    # per frame: (G - 2 S) / 8 slot rows of 128 B (the subtree roots are read as F / G of their
+    # parents: no slot level of their own) + G / 128 bit rows of 256 B
+    assert s["scratch_bytes_per_wave"] == (4096 - 512) // 8 * 128 + 4096 // 128 * 256
+    assert s["lds_bytes_per_wave"] == 512 // 8 * 128
     assert "#define POLAR_SOLO 1" in d.kernel_source()
     assert "POLAR_SOLO" not in pkg.Decoder(m).kernel_source()
     info = d.launch_info(64)

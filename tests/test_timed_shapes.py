@@ -60,10 +60,14 @@ def test_timed_shape_full_batch(pkg, cuda, oracle_mod, name, batch, layout, W):
     assert (info["kernel"], info["layout"], info["waves_per_block"], info["blocks"]) == (3, layout, W, blocks), info
     if layout == 2:
         assert info["sub_words"] == 512, info
+    # the code object build() prewarmed (the ROCm clang driver's), not a hipRTC rebuild on this
+    # machine (a cache-key mismatch once made every timed kernel hipRTC code)
+    assert info["compiler"] == 1, info
     if W == 1:
-        # C3: only the subtree-root level in LDS, F-descent chains in the generated kernel
+        # C3: the subtrees' parent level in LDS (the roots are read as F / G of it), F-descent
+        # chains in the generated kernel
         S = dec.stats["sub_words"]
-        assert info["lds_bytes"] == S // 4 * 128 + 3 * 256, info
+        assert info["lds_bytes"] == 2 * S // 4 * 128 + 3 * 256, info
         assert "pop_chain<3" in dec.kernel_source()
     llr, x = noiseless_batch(torch, mask, batch, seed=batch)
     rows = awgn_rows(batch)

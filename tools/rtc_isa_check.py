@@ -187,7 +187,7 @@ def main():
     else:
         import sc_polar_decoder_hls_amd as pkg
         from sc_polar_decoder_hls_amd._plansets import struct_masks
-        dec = pkg.Decoder(struct_masks(32768)[0], tuning={"kernel": 3, "layout": 1, "sub_words": args.sub_words,
+        dec = pkg.Decoder(struct_masks(32768)[0], tuning={"kernel": 3, "layout": 1, "sub_words": args.sub_words, "sub_root": 1,
                                                           "chain_max": args.chain_max})
         src = dec.kernel_source()
         res = {"plan": {"mask": "struct32768_0", "sub_words": args.sub_words, "chain_max": args.chain_max}}
