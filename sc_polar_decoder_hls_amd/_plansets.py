@@ -97,7 +97,9 @@ def gpu_plans():
             ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, lds_slots=256)),
             ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, lds_slots=1024)),
             ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, sub_root=1)),
-            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), {"kernel": 3, "layout": 2, "sub_root": 1})]
+            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), dict(p, sub_root=2)),
+            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), {"kernel": 3, "layout": 2, "sub_root": 1}),
+            ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), {"kernel": 3, "layout": 2, "sub_root": 2})]
     for wpg in (1, 2, 4, 8):
         out += [("frozen_n_16384_k_8192", mask("frozen_n_16384_k_8192"), dict(p, waves_per_group=wpg, sub_words=64)),
                 ("wave_mask", wave_mask(), dict(p, waves_per_group=wpg, sub_words=64))]

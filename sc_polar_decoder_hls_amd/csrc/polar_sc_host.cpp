@@ -906,7 +906,11 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         // slot: one level less in the slot rows, and the LDS it held takes the next level up
         // (C3: the 512-word level on chip, 6 N instead of 8 N of HBM traffic per frame). Not
         // for subtrees that are children of the root (G = 2 S: their parent is the channel).
-        const bool fuse = t.sub_root != 1 && (int)p->G / 2 > S;
+        // Automatic: pair layout only. The folded F / G runs on the lead wave alone, where the
+        // upper-level record split it over the W waves of a block: same box
+        // (profiles/r05_ab/sub_root_ab3_*.jsonl), C3 (W = 1) 0.844 / 0.824 vs 0.844 / 0.848 ms,
+        // but the solo C5 (W = 4 / 8) 1.414 vs 1.280 ms and its 64-frame share 1.082 vs 1.034.
+        const bool fuse = (t.sub_root == 2 || (t.sub_root == 0 && !solo)) && (int)p->G / 2 > S;
         if (fuse) {
             std::vector<polar_sc_op> fused;
             const std::vector<polar_sc_op> &ops = p->pair_ops;

@@ -180,7 +180,7 @@ def test_subtree_root_slot_vs_fused(pkg, cuda, oracle_mod, layout):
     slot rows (the default): equal on every frame of a C3-sized sample, equal to the oracle."""
     mask = util.mask("frozen_n_65536_k_32768")
     llr, _ = util.synth_frames(mask, 6, ebn0_db=1.0, seed=31)
-    a = run(pkg, cuda, pair(pkg, mask, layout=layout), llr)
+    a = run(pkg, cuda, pair(pkg, mask, layout=layout, sub_root=2), llr)
     b = run(pkg, cuda, pair(pkg, mask, layout=layout, sub_root=1), llr)
     _assert_same(a, b, "fused vs slot roots, layout %d" % layout)
     _assert_same(a, oracle_mod.decode_fsm(mask, llr), "fused roots vs oracle, layout %d" % layout)

@@ -34,10 +34,12 @@ def test_solo_plan_stats(pkg):
     d = solo(pkg, m)
     s = d.stats
     assert (s["kernel"], s["sub_words"], s["storage"]) == (3, 256, 1)
-    # per frame: (G - 2 S) / 8 slot rows of 128 B (the subtree roots are read as F / G of their
-    # parents: no slot level of their own) + G / 128 bit rows of 256 B
-    assert s["scratch_bytes_per_wave"] == (4096 - 512) // 8 * 128 + 4096 // 128 * 256
-    assert s["lds_bytes_per_wave"] == 512 // 8 * 128
+    # per frame: (G - S) / 8 slot rows of 128 B + G / 128 bit rows of 256 B (solo plans keep the
+    # subtree roots in a slot level of their own; sub_root 2 reads them as F / G of the parents)
+    assert s["scratch_bytes_per_wave"] == (4096 - 256) // 8 * 128 + 4096 // 128 * 256
+    assert s["lds_bytes_per_wave"] == 256 // 8 * 128
+    s2 = solo(pkg, m, sub_root=2).stats
+    assert s2["scratch_bytes_per_wave"] == (4096 - 512) // 8 * 128 + 4096 // 128 * 256
     assert "#define POLAR_SOLO 1" in d.kernel_source()
     assert "POLAR_SOLO" not in pkg.Decoder(m).kernel_source()
     info = d.launch_info(64)
@@ -63,6 +65,9 @@ def test_solo_generated_code_emulated(pkg, oracle_mod, N):
         ref = oracle_mod.decode_fsm(mask, llr)
         for sw in solo_sub_words(N):
             _assert_same(pair_emu.decode(solo(pkg, mask, sub_words=sw), llr), ref, "emulated N=%d mask %d S=%d" % (N, i, sw))
+            if sw < N // 32:   # roots as F / G of their parents
+                _assert_same(pair_emu.decode(solo(pkg, mask, sub_words=sw, sub_root=2), llr), ref,
+                             "emulated N=%d mask %d S=%d fused roots" % (N, i, sw))
 
 
 @pytest.mark.gpu

@@ -140,9 +140,9 @@ def census(asm):
     funcs = {}
     cur, cls = None, None
     for line in asm.split("\n"):
-        m = re.match(r"^(_Z\w*polar_psub_(\d+)\w*):", line)
+        m = re.match(r"^(_Z\w*polar_psub_(\d+(?:_[FG])?)\w*):", line)   # (_F / _G: fused-root variants)
         if m:
-            cur = int(m.group(2))
+            cur = m.group(2)
             funcs[cur] = (collections.Counter(), collections.Counter())
             cls = "prologue"
             continue
@@ -186,7 +186,7 @@ def main():
         for c, v in sorted(tot_v.items(), key=lambda kv: -kv[1]):
             print("%-14s %10d %5.1f%% %10d" % (c, v, 100.0 * v / max(nv, 1), tot_a[c]))
         return
-    calls = collections.Counter(int(m) for m in re.findall(r"polar_psub_(\d+)\(c\.slot_ptr", src.split("polar_sc_pair_subtest_kernel")[0]))
+    calls = collections.Counter(re.findall(r"polar_psub_(\d+(?:_[FG])?)\(c\.slot_ptr", src.split("polar_sc_pair_subtest_kernel")[0]))
     marked, nmark = mark(src)
     with tempfile.TemporaryDirectory() as tmp:
         asm = compile_asm(marked, tmp)

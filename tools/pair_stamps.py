@@ -112,7 +112,9 @@ def build(mask_name, batch, tuning, variant=""):
     info = dec.launch_info(batch)
     W, lds_row0, lds = info["waves_per_block"], info["lds_row0"], info["lds_bytes"]
     solo = "#define POLAR_SOLO 1" in src
-    slot_rows = (G - S) // (8 if solo else 4)
+    wpr = 8 if solo else 4
+    fused = st["lds_bytes_per_wave"] == 2 * S // wpr * 128   # subtree roots read as F / G of the parents
+    slot_rows = (G - (2 * S if fused else S)) // wpr
     blocks = batch if solo else (batch + 1) // 2
     pair_dwords = st["scratch_bytes_per_wave"] // 4
     # stamp segment 0: after pair_init, after every op
