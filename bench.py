@@ -288,7 +288,21 @@ SECONDARY = (
     ("q8_n16384_k14746", "frozen_n_16384_k_14746", SWEEP_FRAMES, {"llr_bits": 8},
      "QUANT 8 (LLR_BITS 8) on the rate-0.9 code N=16384 K=14746 of script_tests.sh:7-9, %d frames per GPU"
      % SWEEP_FRAMES),
+    # parser_comp.sh:12 sweeps LLR_BITS up to 9: the int16 channel (the C-sim LLRs x 8)
+    ("q9_n16384", "frozen_n_16384_k_8192", SWEEP_FRAMES, {"llr_bits": 9},
+     "LLR_BITS 9 (parser_comp.sh:12; int16 channel, C-sim LLRs x 8) on N=16384 K=8192, %d frames per GPU"
+     % SWEEP_FRAMES),
 )
+
+
+def widen_q9(torch, llr, fmt):
+    """LLR_BITS 9 frames: the C-sim int8 LLRs (6-bit range) as int16 scaled into the 9-bit range"""
+    return llr.to(torch.int16) * 8 if fmt and fmt.get("llr_bits", 6) > 8 else llr
+
+
+def channel_bytes(fmt):
+    """input bytes per LLR: int8, or int16 for 9-bit LLRs (polar_sc_decode_i16)"""
+    return 2 if fmt and fmt.get("llr_bits", 6) > 8 else 1
 
 
 def roofline_entry(name, N, per_gpu, kern_ms, dec, fmt=None):
@@ -296,7 +310,7 @@ def roofline_entry(name, N, per_gpu, kern_ms, dec, fmt=None):
     the event-timed kernel time; traffic from the committed PMC summary of the same workload,
     used only when that profile is of the machine code timed here (its code_key -- the hash of
     the kernels' instructions and descriptors, polar_sc_plan_launch_info -- equals this plan's)."""
-    bytes_per_launch = 1.125 * N * per_gpu
+    bytes_per_launch = (channel_bytes(fmt) + 0.125) * N * per_gpu   # (1.125 N per frame; int16 channel 2.125 N)
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src, note = None, None, None
     info = dec.launch_info(per_gpu)
@@ -348,6 +362,7 @@ def secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mask_name, 
     dec.prepare(per_gpu)
     nb = max(1, min(8, -(-ROTATE_BYTES // (per_gpu * N))))
     batches = make_batches(pkg, torch, args, mask, per_gpu, frame0, sum(counts), dev, args.ebn0, nb)
+    batches = [(widen_q9(torch, b[0], fmt),) + tuple(b[1:]) for b in batches]
     outs = [torch.empty((per_gpu, dec.words), dtype=torch.int64, device=dev) for _ in range(nb)]
     steps = max(3, min(args.steps, 20))
     warm = 3

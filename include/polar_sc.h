@@ -111,8 +111,8 @@ typedef struct polar_sc_tuning {
                                  eight words per register, half the instructions per frame on
                                  nodes of >= 16 words; PAR 16 only) */
     int32_t sub_root;         /* pair plans: where a generated subtree decoder reads its root.
-                                 0 = automatic (2 in the frame-pair layout when the plan has
-                                 levels above the subtrees' parents, 1 in the solo layout),
+                                 0 = automatic (2 in the frame-pair layout when the frame
+                                 has at least 16 subtrees, 1 otherwise),
                                  1 = from a stage slot written by the
                                  upper-level F / G, 2 = as F / G of its parent's slot rows
                                  (the subtree-root level then needs no slot) */

@@ -453,14 +453,16 @@ class Decoder:
 
     def debug_subtree(self, sid, rows):
         """Test hook of pair plans: generated subtree decoder `sid` on root slot rows (uint16
-        [S/4, 64], SM8 pairs); returns its partial-sum dwords uint32 [max(1, S/64), 64]."""
+        [S/4, 64], SM8 pairs; solo layout: [S/8, 64]); returns its partial-sum dwords uint32
+        [max(1, S/64), 64] (solo: [max(1, S/128), 64])."""
         torch = _torch()
         S = self.stats["sub_words"]
+        nbits = max(1, S // (128 if "#define POLAR_SOLO 1" in self.kernel_source() else 64))
         inp = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.uint16).view(np.int16)).cuda()
         out = torch.zeros((max(1, S // 64), 64), dtype=torch.int32, device="cuda")
         _check("polar_sc_debug_subtree", lib().polar_sc_debug_subtree(self._plan, int(sid), ctypes.c_void_p(inp.data_ptr()),
                                                                        ctypes.c_void_p(out.data_ptr())))
-        return out.cpu().numpy().view(np.uint32)
+        return out.cpu().numpy().view(np.uint32)[:nbits]
 
     def decode_host(self, llr):
         """Host arrays in/out (synchronous): int8 [B, N] -> uint64 [B, ceil(N/64)]."""

@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 
+extern "C" int polar_sc_launch_widen(const int8_t *in_dev, int16_t *out_dev, size_t n, void *stream);
 extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out, const void *ops,
                                       uint32_t *scratch, int N, long batch, int out_stride,
                                       int waves_per_group, int groups_per_block, int group_dwords,
@@ -623,6 +624,21 @@ int decode_common(const polar_sc_plan *p, const int8_t *llr, uint16_t *out, size
     int rc = ensure_device(p, batch, &st, DEV_DECODE, (p->gmem || p->pair) ? &held : nullptr);
     if (rc) return rc;
     if (p->jit) return polar_host::jit_launch(*p, *st, llr, out, (long)batch, out_stride, stream);
+    if (p->slot16()) {   // the kernel reads the int16 channel: widen the int8 frames first
+        const size_t n = batch * (size_t)p->N, need = 2 * n;
+        if (st->wide_bytes < need) {
+            if (st->wide) {
+                if (hipDeviceSynchronize() != hipSuccess) return -EIO;
+                (void)hipFree(st->wide);
+                st->wide = nullptr;
+                st->wide_bytes = 0;
+            }
+            if (hipMalloc(&st->wide, need) != hipSuccess) return -ENOMEM;
+            st->wide_bytes = need;
+        }
+        if (polar_sc_launch_widen(llr, (int16_t *)st->wide, n, stream)) return -EIO;
+        return polar_host::jit_launch_pair(*p, *st, (const int8_t *)st->wide, out, (long)batch, out_stride, stream);
+    }
     if (p->pair) return polar_host::jit_launch_pair(*p, *st, llr, out, (long)batch, out_stride, stream);
     const int wpg = waves_per_group(p, batch, st->simds);
     if (p->hybrid) return polar_host::jit_launch_hybrid(*p, *st, llr, out, (long)batch, out_stride, wpg, stream);
@@ -847,7 +863,9 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // pair plans also take PAR 32 / 64 (the PAR word = one register of two / four device words;
     // the host expands its leaf into F / G / 16-LLR leaf records, par_expand: G_extended when
     // EXTENDED, the saturating G and POLAR_EXT 0 leaves when not)
-    const bool pair_fmt = dflt || ((c.par == 32 || c.par == 64) && c.sigmag == 1 && c.llr_bits <= 8);
+    // and 9-bit LLRs at PAR 16 (16-bit stage slots, the int16 channel: polar_sc_pair.h SLOT16)
+    const bool pair_fmt = dflt || ((c.par == 32 || c.par == 64) && c.sigmag == 1 && c.llr_bits <= 8) ||
+                          (c.par == 16 && c.sigmag == 1 && c.llr_bits == 9);
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR
     // level's F / G / H then run inside the straight-line code instead of as interpreter ops
@@ -874,7 +892,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     }
     // solo layout (one frame per wave, 8 words per register): PAR 16 only; a forced solo
     // layout the plan cannot take is an error
-    const bool solo_ok = c.par == 16;
+    const bool solo_ok = c.par == 16 && c.llr_bits <= 8;
     if ((t.layout != 0 && !want_pair) || (t.layout == 2 && !solo_ok)) {
         delete p;
         return -ENOTSUP;
@@ -906,11 +924,15 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         // slot: one level less in the slot rows, and the LDS it held takes the next level up
         // (C3: the 512-word level on chip, 6 N instead of 8 N of HBM traffic per frame). Not
         // for subtrees that are children of the root (G = 2 S: their parent is the channel).
-        // Automatic: pair layout only. The folded F / G runs on the lead wave alone, where the
-        // upper-level record split it over the W waves of a block: same box
-        // (profiles/r05_ab/sub_root_ab3_*.jsonl), C3 (W = 1) 0.844 / 0.824 vs 0.844 / 0.848 ms,
-        // but the solo C5 (W = 4 / 8) 1.414 vs 1.280 ms and its 64-frame share 1.082 vs 1.034.
-        const bool fuse = (t.sub_root == 2 || (t.sub_root == 0 && !solo)) && (int)p->G / 2 > S;
+        // Automatic: the pair layout with G >= 16 S only. The folded F / G runs on the lead
+        // wave alone, where the upper-level record split it over the W waves of a block, and
+        // each root row is computed twice (for the subtree's F and its G): it pays only where
+        // the level it takes off HBM is a deep one of a long code. Same box
+        // (profiles/r05_ab/sub_root_ab3_*.jsonl, n16384_sub_root_ab.jsonl): C3 (G = 16 S, W = 1)
+        // 0.844 / 0.824 ms vs 0.844 / 0.848 and 1.97 vs 2.7 GB per decode; N = 16384 (G = 4 S)
+        // 0.216 / 0.206 / 0.204 vs 0.201 / 0.194 / 0.194 ms (QUANT 8: 0.188 vs 0.168); the solo
+        // C5 (W = 4 / 8) 1.414 vs 1.280 ms, its 64-frame share 1.082 vs 1.034.
+        const bool fuse = (t.sub_root == 2 || (t.sub_root == 0 && !solo && (int)p->G >= 16 * S)) && (int)p->G / 2 > S;
         if (fuse) {
             std::vector<polar_sc_op> fused;
             const std::vector<polar_sc_op> &ops = p->pair_ops;
@@ -938,7 +960,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         s.n_sub_kinds = (uint32_t)p->subs.size();
         s.n_sub_calls = sc.calls;
         p->pair_slot_rows = ((int)p->G - (p->pair_fused ? 2 * S : S)) / p->wpr();
-        p->pair_dwords = p->pair_slot_rows * 32 + std::max<int>(1, (int)p->G / (16 * p->wpr())) * 64;
+        p->pair_dwords = p->pair_slot_rows * (p->slot_row_bytes() / 4) + std::max<int>(1, (int)p->G / (16 * p->wpr())) * 64;
         if (t.tier_words > 0) {
             if (t.tier_words <= S) {
                 delete p;
@@ -1032,13 +1054,13 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         s.storage = 1u;
         s.tier_steps = (uint32_t)p->pair_tier.steps.size();
         s.tier_words = (uint32_t)p->pair_tier.tw;
-        s.lds_bytes_per_wave = (uint32_t)((p->pair_fused ? 2 : 1) * p->sub_words / p->wpr()) * 128u;
+        s.lds_bytes_per_wave = (uint32_t)((p->pair_fused ? 2 : 1) * p->sub_words / p->wpr()) * (uint32_t)p->slot_row_bytes();
         s.scratch_bytes_per_wave = (uint64_t)p->pair_dwords * 4u;
     }
     // automatic layout: a PAR 16 pair plan also holds its solo plan (subtrees of up to 512
     // words), which small batches decode with (layout_for); none when the tuning cannot carry
     // over (a subtree size below 64 words)
-    if (p->pair && !p->solo && t.layout == 0 && c.par == 16) {
+    if (p->pair && !p->solo && t.layout == 0 && c.par == 16 && c.llr_bits <= 8) {
         polar_sc_tuning ts = t;
         ts.layout = 2;
         ts.kernel = 3;
@@ -1070,6 +1092,7 @@ int polar_sc_plan_destroy(polar_sc_plan *p)
         if (kv.second.module16) (void)hipModuleUnload(kv.second.module16);
         if (kv.second.ops16) (void)hipFree(kv.second.ops16);
         if (kv.second.scratch) (void)hipFree(kv.second.scratch);
+        if (kv.second.wide) (void)hipFree(kv.second.wide);
     }
     if (have_dev && !p->dev.empty()) (void)hipSetDevice(cur);
     delete p;
@@ -1114,6 +1137,12 @@ int polar_sc_decode_i16(const polar_sc_plan *p, const int16_t *llr_dev, uint64_t
     if (batch > (size_t)0x7FFFFFF8) return -EINVAL;
     DevState *st = nullptr;
     std::unique_lock<std::mutex> held;
+    if (p->slot16()) {   // pair plans of 9-bit LLRs read the int16 channel themselves
+        const int rc = ensure_device(p, batch, &st, DEV_DECODE, &held);
+        if (rc) return rc;
+        return polar_host::jit_launch_pair(*p, *st, (const int8_t *)llr_dev, (uint16_t *)hard_bits_dev, (long)batch,
+                                           (int)(4 * ((p->G + 3) / 4)), stream);
+    }
     int rc = ensure_device(p, batch, &st, DEV_I16, &held);
     if (rc) return rc;
     rc = polar_host::jit_load16(*p, *st);

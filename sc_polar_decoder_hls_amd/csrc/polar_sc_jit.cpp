@@ -1170,7 +1170,7 @@ PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, in
     // (S: the smallest slot level -- the subtree roots, or their parents when the roots are
     // read as F / G of them, pair_fused)
     const int S = p.pair_fused ? 2 * p.sub_words : p.sub_words, G = (int)p.G, wpr = p.wpr();
-    const long bpw = 128 / wpr;   // slot bytes per word
+    const long bpw = p.slot_row_bytes() / wpr;   // slot bytes per word
     int L = 0;
     for (int w = S; w <= G / 2; w *= 2) {
         if (tier && w >= p.pair_tier.tw) break;
@@ -1185,7 +1185,7 @@ PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, in
     }
     const int lds_rows = L ? (2 * L - S) / wpr : 0;
     sh.lds_row0 = p.pair_slot_rows - lds_rows;
-    sh.lds = (unsigned)(lds_rows * 128 + 3 * W * 256);
+    sh.lds = (unsigned)(lds_rows * p.slot_row_bytes() + 3 * W * 256);
     return sh;
 }
 

@@ -92,6 +92,30 @@ extern "C" int polar_sc_launch_decode(int gmem, const int8_t *llr, uint16_t *out
     return e == hipSuccess ? 0 : -(int)e - 1000;
 }
 
+namespace polar {
+// int8 channel -> int16 (sign extension), for plans whose generated kernel reads the int16
+// channel (pair plans of 9-bit LLRs, 16-bit stage slots) decoded through the int8 entry point
+__global__ void __launch_bounds__(256) polar_widen_kernel(const int8_t *__restrict__ in, int16_t *__restrict__ out,
+                                                          size_t n)
+{
+    // (byte loads: the int8 frames need not be 4-byte aligned)
+    const size_t i = ((size_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+    for (size_t k = i; k < i + 4u && k < n; k++) out[k] = in[k];
+}
+
+}  // namespace polar
+
+extern "C" int polar_sc_launch_widen(const int8_t *in_dev, int16_t *out_dev, size_t n, void *stream)
+{
+    if (n == 0) return 0;
+    const size_t blocks = (n + 1023u) / 1024u;
+    hipLaunchKernelGGL(polar::polar_widen_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in_dev,
+                       out_dev, n);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -(int)e - 1000;
+}
+
+
 extern "C" int polar_sc_launch_selftest(uint32_t *out_dev)
 {
     hipLaunchKernelGGL(polar::polar_sc_lane_selftest_kernel, dim3(1), dim3(64), 0, 0, out_dev);

@@ -63,7 +63,9 @@ typedef __attribute__((address_space(3))) u32 lds_w32;
 typedef __attribute__((address_space(1))) u32 g_u32;
 typedef __attribute__((address_space(1))) unsigned char g_u8;
 typedef __attribute__((address_space(1))) unsigned short g_u16;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
@@ -227,12 +229,12 @@ constexpr int PAIR_MAX_WAVES = 8;   // launch bound 512 threads: <= 256 VGPRs pe
 // slot dwords (row pairs, SM8 bytes lo_even, lo_odd, hi_even, hi_odd)
 // ---------------------------------------------------------------------------------------
 // row (odd ? 2 i + 1 : 2 i) of a slot dword as the SM16 pair of the register code
-__device__ __forceinline__ u32 prow(u32 d, bool odd)
+__device__ __forceinline__ u32 prow8(u32 d, bool odd)
 {
     return __builtin_amdgcn_perm(d, d, odd ? 0x03030101u : 0x02020000u) & ((0x8000u | QMAG) * 0x00010001u);
 }
 // two SM16 pairs (rows 2 i, 2 i + 1) -> slot dword
-__device__ __forceinline__ u32 ppack(u32 v0, u32 v1)
+__device__ __forceinline__ u32 ppack8(u32 v0, u32 v1)
 {
     const u32 t0 = (v0 & (QMAG * 0x00010001u)) | ((v0 >> 8) & 0x00800080u);   // SM8 in bytes 0, 2
     const u32 t1 = (v1 & (QMAG * 0x00010001u)) | ((v1 >> 8) & 0x00800080u);
@@ -302,18 +304,63 @@ __device__ __forceinline__ u32 conv4(u32 raw)
 }
 // F / G of a slot dword pair (either arithmetic)
 template <bool ISG>
-__device__ __forceinline__ u32 fg4(u32 a, u32 b, u32 u)
+__device__ __forceinline__ u32 fg4_8(u32 a, u32 b, u32 u)
 {
     if constexpr (PAIR_SWAR) {
         if constexpr (ISG) return G4(a, b, u);
         else return F4(a, b);
     } else if constexpr (ISG) {
-        return ppack(G_sm<GSAT>(prow(a, false), prow(b, false), (u << 8) & SGN),
-                     G_sm<GSAT>(prow(a, true), prow(b, true), u & SGN));
+        return ppack8(G_sm<GSAT>(prow8(a, false), prow8(b, false), (u << 8) & SGN),
+                      G_sm<GSAT>(prow8(a, true), prow8(b, true), u & SGN));
     } else {
-        return ppack(F_sm(prow(a, false), prow(b, false)), F_sm(prow(a, true), prow(b, true)));
+        return ppack8(F_sm(prow8(a, false), prow8(b, false)), F_sm(prow8(a, true), prow8(b, true)));
     }
 }
+
+// ---------------------------------------------------------------------------------------
+// slot formats. SM8 (LLR_BITS <= 8): a row pair (slot rows 2 i, 2 i + 1) is one dword of SM8
+// bytes, an 8-row group 16 B per lane. SLOT16 (LLR_BITS 9, where the F magnitudes of the
+// channel reach 255 and do not fit an SM8 byte): every slot row is the register format itself,
+// one SM16 pair; a row pair is two dwords, an 8-row group 32 B per lane. The loops below see a
+// row pair as su_t and an 8-row group as sg_t; u flags of a row pair keep the SM8 positions
+// (bits 7 / 23 row 2 i, 15 / 31 row 2 i + 1, ubits4).
+// ---------------------------------------------------------------------------------------
+constexpr bool PAIR_S16 = SLOT16;
+constexpr int GD = PAIR_S16 ? 8 : 4;   // dwords per lane of an 8-row group
+#if POLAR_Q > 8
+typedef u32x2 su_t;
+typedef u32x8 sg_t;
+typedef short chan_el;                 // int16 channel (polar_sc_decode_i16)
+__device__ __forceinline__ u32 prow(su_t d, bool odd) { return odd ? d.y : d.x; }
+__device__ __forceinline__ su_t ppack(u32 v0, u32 v1) { return su_t{v0, v1}; }
+__device__ __forceinline__ su_t sget(const sg_t &g, int t) { return su_t{g[2 * t], g[2 * t + 1]}; }
+__device__ __forceinline__ void sset(sg_t &g, int t, su_t v)
+{
+    g[2 * t] = v.x;
+    g[2 * t + 1] = v.y;
+}
+template <bool ISG>
+__device__ __forceinline__ su_t fg4(su_t a, su_t b, u32 u)
+{
+    if constexpr (ISG) return su_t{G_sm<GSAT>(a.x, b.x, (u << 8) & SGN), G_sm<GSAT>(a.y, b.y, u & SGN)};
+    else return su_t{F_sm(a.x, b.x), F_sm(a.y, b.y)};
+}
+#else
+typedef u32 su_t;
+typedef u32x4 sg_t;
+typedef unsigned char chan_el;
+__device__ __forceinline__ u32 prow(su_t d, bool odd) { return prow8(d, odd); }
+__device__ __forceinline__ su_t ppack(u32 v0, u32 v1) { return ppack8(v0, v1); }
+__device__ __forceinline__ su_t sget(const sg_t &g, int t) { return g[t]; }
+__device__ __forceinline__ void sset(sg_t &g, int t, su_t v) { g[t] = v; }
+template <bool ISG>
+__device__ __forceinline__ su_t fg4(su_t a, su_t b, u32 u) { return fg4_8<ISG>(a, b, u); }
+#endif
+typedef __attribute__((address_space(1))) su_t g_su;
+typedef __attribute__((address_space(3))) su_t lds_su;
+typedef __attribute__((address_space(1))) sg_t g_sg;
+typedef __attribute__((address_space(3))) sg_t lds_sg;
+typedef __attribute__((address_space(1))) chan_el g_chan;
 
 // ---------------------------------------------------------------------------------------
 // per-pair context
@@ -322,7 +369,7 @@ __device__ __forceinline__ u32 fg4(u32 a, u32 b, u32 u)
 // reference would put it on the private stack). Global pointers carry address space 1 so that
 // the loads and stores through them are global_*, not flat_*.
 struct PairCtx {
-    const g_u8 *chl, *chh;            // channel bytes at this lane's position, frames lo / hi
+    const g_chan *chl, *chh;          // channel LLRs at this lane's position, frames lo / hi
     g_u32 *hs;                        // HBM stage slots of the pair (lane offset 4 lane included)
     g_u32 *hb;                        // HBM partial-sum dwords of the pair (lane offset included)
     lds_w32 *ls;                      // LDS stage slots [lds_row0, ..) (lane offset 4 lane included)
@@ -343,45 +390,56 @@ struct PairCtx {
     __device__ __forceinline__ int lvl_row(int k) const { return (G - (G >> (k - 1))) >> 2; }
     __device__ __forceinline__ bool in_lds(int r) const { return r >= lds_row0; }
     // dword offset of slot row pair r / 2 (r even) from the lane's base
-    static __device__ __forceinline__ int sofs(int r) { return (r >> 3) * 256 + ((r >> 1) & 3); }
-    // slot dword of rows r, r + 1 (r even)
+    static __device__ __forceinline__ int sofs(int r) { return (r >> 3) * 64 * GD + ((r >> 1) & 3) * (GD / 4); }
+    // slot rows r, r + 1 (r even)
     template <bool L>
-    __device__ __forceinline__ u32 ld2(int r) const
+    __device__ __forceinline__ su_t ld2(int r) const
     {
-        if constexpr (L) return ls[sofs(r - lds_row0)];
-        else return hs[sofs(r)];
+        if constexpr (L) return *(const lds_su *)(ls + sofs(r - lds_row0));
+        else return *(const g_su *)(hs + sofs(r));
     }
-    // slot dwords of rows r .. r + 7 (r a multiple of 8)
+    // slot rows r .. r + 7 (r a multiple of 8)
     template <bool L>
-    __device__ __forceinline__ u32x4 ld8(int r) const
+    __device__ __forceinline__ sg_t ld8(int r) const
     {
-        if constexpr (L) return *(const lds_u32x4 *)(ls + ((r - lds_row0) >> 3) * 256);
-        else return *(const g_u32x4 *)(hs + (r >> 3) * 256);
+        if constexpr (L) return *(const lds_sg *)(ls + ((r - lds_row0) >> 3) * 64 * GD);
+        else return *(const g_sg *)(hs + (r >> 3) * 64 * GD);
     }
     template <bool L>
-    __device__ __forceinline__ void st8(int r, u32x4 v) const
+    __device__ __forceinline__ void st8(int r, sg_t v) const
     {
-        if constexpr (L) *(lds_u32x4 *)(ls + ((r - lds_row0) >> 3) * 256) = v;
-        else *(g_u32x4 *)(hs + (r >> 3) * 256) = v;
+        if constexpr (L) *(lds_sg *)(ls + ((r - lds_row0) >> 3) * 64 * GD) = v;
+        else *(g_sg *)(hs + (r >> 3) * 64 * GD) = v;
     }
     // the slot from row r on (r a multiple of 8) through a generic pointer (subtree roots)
     __device__ __forceinline__ const u32 *slot_ptr(int r) const
     {
-        return in_lds(r) ? (const u32 *)(ls + ((r - lds_row0) >> 3) * 256) : (const u32 *)(hs + (r >> 3) * 256);
+        return in_lds(r) ? (const u32 *)(ls + ((r - lds_row0) >> 3) * 64 * GD) : (const u32 *)(hs + (r >> 3) * 64 * GD);
     }
-    // channel rows j, j + 1 (j even) as a slot dword (wrapper_in + qconv_format)
-    __device__ __forceinline__ u32 chan2(int j) const
+    // channel rows j, j + 1 (j even) as a slot row pair (wrapper_in + qconv_format)
+    __device__ __forceinline__ su_t chan2(int j) const
     {
+#if POLAR_Q > 8
+        const u32 r0 = (u32)(unsigned short)chl[ROWB * j] | ((u32)(unsigned short)chh[ROWB * j] << 16);
+        const u32 r1 = (u32)(unsigned short)chl[ROWB * j + ROWB] | ((u32)(unsigned short)chh[ROWB * j + ROWB] << 16);
+        return ppack(conv_pair(r0), conv_pair(r1));
+#else
         const u32 lo = (u32)chl[ROWB * j] | ((u32)chl[ROWB * j + ROWB] << 8);
         const u32 hi = (u32)chh[ROWB * j] | ((u32)chh[ROWB * j + ROWB] << 8);
         const u32 raw = lo | (hi << 16);
         if constexpr (PAIR_SWAR) return conv4(raw);
         else return ppack(conv_pair(raw & 0x00FF00FFu), conv_pair((raw >> 8) & 0x00FF00FFu));
+#endif
     }
-    // channel rows j .. j + 7 (j a multiple of 8) as four slot dwords, byte loads (chan2)
-    __device__ __forceinline__ u32x4 chan8b(int j) const
+    // channel rows j .. j + 7 (j a multiple of 8) as an 8-row group, element loads (chan2)
+    __device__ __forceinline__ sg_t chan8b(int j) const
     {
-        return u32x4{chan2(j), chan2(j + 2), chan2(j + 4), chan2(j + 6)};
+        sg_t g;
+        sset(g, 0, chan2(j));
+        sset(g, 1, chan2(j + 2));
+        sset(g, 2, chan2(j + 4));
+        sset(g, 3, chan2(j + 6));
+        return g;
     }
     __device__ __forceinline__ u32 bld(int d) const { return hb[d * 64]; }
     __device__ __forceinline__ void bst(int d, u32 v) const { hb[d * 64] = v; }
@@ -419,8 +477,8 @@ __device__ __forceinline__ ChanQ chan_quad(const PairCtx &c)
     const u32 lane = threadIdx.x & 63u, pl = lane & 15u, k = pl & 3u;
     ChanQ q;
     // chl = frame lo + 16 row + pos; chh - chl = (hi frame - lo frame) N (uniform)
-    q.base = uniform_ptr(c.chl - (16u * (lane >> 4) + lane_pos(pl)));
-    const u32 dhi = __builtin_amdgcn_readfirstlane((u32)(c.chh - c.chl));
+    q.base = uniform_ptr((const g_u8 *)c.chl - (16u * (lane >> 4) + lane_pos(pl)));
+    const u32 dhi = __builtin_amdgcn_readfirstlane((u32)((const g_u8 *)c.chh - (const g_u8 *)c.chl));
     q.off = 16u * (lane >> 4) + (pl & ~3u) + ROWB * (k & 1u) + ((k & 2u) ? dhi : 0u);
     q.sel.init(pl);
     q.al = ((u32)(unsigned long)q.base & 3u) == 0u;
@@ -430,7 +488,7 @@ __device__ __forceinline__ u32 quad_transpose(u32 x, const ChanQ &q) { return qu
 __device__ __forceinline__ u32 chan_conv(u32 raw)
 {
     if constexpr (PAIR_SWAR) return conv4(raw);
-    else return ppack(conv_pair(raw & 0x00FF00FFu), conv_pair((raw >> 8) & 0x00FF00FFu));
+    else return ppack8(conv_pair(raw & 0x00FF00FFu), conv_pair((raw >> 8) & 0x00FF00FFu));
 }
 // channel rows j .. j + 7 (j a multiple of 8) as four slot dwords, aligned frames
 __device__ __forceinline__ u32x4 chan8a(const ChanQ &q, int j)
@@ -444,10 +502,15 @@ __device__ __forceinline__ u32x4 chan8a(const ChanQ &q, int j)
     for (int t = 0; t < 4; t++) r[t] = chan_conv(quad_transpose(raw[t], q));
     return r;
 }
-__device__ __forceinline__ u32x4 chan8(const PairCtx &c, const ChanQ &q, int j)
+__device__ __forceinline__ sg_t chan8(const PairCtx &c, const ChanQ &q, int j)
 {
+#if POLAR_Q > 8
+    (void)q;   // int16 channel: element loads
+    return c.chan8b(j);
+#else
     if (!q.al) return c.chan8b(j);
     return chan8a(q, j);
+#endif
 }
 
 // bits of local words [l0, l0 + cnt) (cnt <= 16, inside one dword) := acc (bit j = word l0 + j
@@ -479,16 +542,16 @@ __device__ __forceinline__ void pfg_rows(const PairCtx &c, int s0, int d0, int n
     // (ping-pong: the loads of the next batch are issued before the arithmetic of this one).
     // HBM: 2 x 4 dwordx4 loads (+ 3 partial-sum dwords) per batch; the channel 8 x 4 byte
     // loads; LDS 2 x 2 b128.
-    constexpr int NG = ROOT ? 2 : (SL ? 2 : 4);
+    constexpr int NG = (ROOT ? 2 : (SL ? 2 : 4)) / (PAIR_S16 ? 2 : 1);   // (16-bit slots: the same registers)
     ChanQ cq;
-    if constexpr (ROOT) cq = chan_quad(c);
+    if constexpr (ROOT && !PAIR_S16) cq = chan_quad(c);
     constexpr int RB = 8 * NG;   // rows per batch
-    auto src = [&](int j) -> u32x4 {
+    auto src = [&](int j) -> sg_t {
         if constexpr (ROOT) return chan8(c, cq, j);
         else return c.template ld8<SL>(s0 + j);
     };
     struct Batch {
-        u32x4 a[NG], b[NG];
+        sg_t a[NG], b[NG];
         u32 u0, u1, u2;   // (scalars: a selected array element would go to scratch)
     };
     auto load = [&](Batch &x, int j) {
@@ -513,15 +576,15 @@ __device__ __forceinline__ void pfg_rows(const PairCtx &c, int s0, int d0, int n
         }
 #pragma unroll
         for (int g = 0; g < NG; g++) {
-            u32x4 r;
+            sg_t r;
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 if constexpr (ISG) {
                     const int k = 8 * g + 2 * t;   // row in the batch
                     const u32 u = ub >= 0 ? ubits4s(uq[k >> 4], k & 15) : 0u;
-                    r[t] = fg4<true>(x.a[g][t], x.b[g][t], u);
+                    sset(r, t, fg4<true>(sget(x.a[g], t), sget(x.b[g], t), u));
                 } else {
-                    r[t] = fg4<false>(x.a[g][t], x.b[g][t], 0u);
+                    sset(r, t, fg4<false>(sget(x.a[g], t), sget(x.b[g], t), 0u));
                 }
             }
             c.template st8<DL>(d0 + j + 8 * g, r);
@@ -546,13 +609,13 @@ __device__ __forceinline__ void pfg_rows(const PairCtx &c, int s0, int d0, int n
     }
     for (; j < j1; j += 8) {   // remaining groups
         Batch x;
-        const u32x4 a = src(j), b = src(n4 + j);
-        u32x4 r;
+        const sg_t a = src(j), b = src(n4 + j);
+        sg_t r;
         const u32 ud = ub >= 0 ? c.bld((ub + j) >> 4) : 0u;
 #pragma unroll
         for (int t = 0; t < 4; t++) {
-            if constexpr (ISG) r[t] = fg4<true>(a[t], b[t], ub >= 0 ? ubits4(ud, ub + j + 2 * t) : 0u);
-            else r[t] = fg4<false>(a[t], b[t], 0u);
+            if constexpr (ISG) sset(r, t, fg4<true>(sget(a, t), sget(b, t), ub >= 0 ? ubits4(ud, ub + j + 2 * t) : 0u));
+            else sset(r, t, fg4<false>(sget(a, t), sget(b, t), 0u));
         }
         (void)x;
         c.template st8<DL>(d0 + j, r);
@@ -606,26 +669,26 @@ __device__ __noinline__ void pchain(PairCtx c, int k, int n4, int ub, u32 gm)
     const int s0 = ROOT ? 0 : c.lvl_row(k);
     const bool sl = !ROOT && c.in_lds(s0);
     ChanQ cq;
-    if constexpr (ROOT) cq = chan_quad(c);
+    if constexpr (ROOT && !PAIR_S16) cq = chan_quad(c);
     // HBM slots and partial sums through a wave-uniform base + one 32-bit lane offset
     const u32 lane = threadIdx.x & 63u;
-    const g_u8 *const hsb = (const g_u8 *)uniform_ptr(c.hs - 4u * lane);
+    const g_u8 *const hsb = (const g_u8 *)uniform_ptr(c.hs - (u32)GD * lane);
     const g_u8 *const hbb = (const g_u8 *)uniform_ptr(c.hb - lane);
-    auto ldh = [&](int r) -> u32x4 { return *(const g_u32x4 *)(hsb + ((u32)(r >> 3) * 1024u + 16u * lane)); };
-    auto sth = [&](int r, u32x4 v) { *(g_u32x4 *)(hsb + ((u32)(r >> 3) * 1024u + 16u * lane)) = v; };
-    auto st = [&](int r, u32x4 v) {
+    auto ldh = [&](int r) -> sg_t { return *(const g_sg *)(hsb + ((u32)(r >> 3) * (256u * GD) + (4u * GD) * lane)); };
+    auto sth = [&](int r, sg_t v) { *(g_sg *)(hsb + ((u32)(r >> 3) * (256u * GD) + (4u * GD) * lane)) = v; };
+    auto st = [&](int r, sg_t v) {
         if (c.in_lds(r)) c.template st8<true>(r, v);
         else sth(r, v);
     };
     struct Col {
-        u32x4 a[M], b[M];
+        sg_t a[M], b[M];
         u32 u[M];
     };
     auto load = [&](Col &x, int g) {
 #pragma unroll
         for (int m = 0; m < M; m++) {
             const int j = 8 * g + m * nl;
-            if constexpr (ROOT && AL) {
+            if constexpr (ROOT && AL && !PAIR_S16) {
                 x.a[m] = chan8a(cq, j);
                 x.b[m] = chan8a(cq, n4 + j);
             } else if constexpr (ROOT) {
@@ -649,8 +712,8 @@ __device__ __noinline__ void pchain(PairCtx c, int k, int n4, int ub, u32 gm)
             const int j = j0 + m * nl;
 #pragma unroll
             for (int t = 0; t < 4; t++) {
-                if constexpr (ISG0) x.a[m][t] = fg4<true>(x.a[m][t], x.b[m][t], ub >= 0 ? ubits4(x.u[m], ub + j + 2 * t) : 0u);
-                else x.a[m][t] = fg4<false>(x.a[m][t], x.b[m][t], 0u);
+                if constexpr (ISG0) sset(x.a[m], t, fg4<true>(sget(x.a[m], t), sget(x.b[m], t), ub >= 0 ? ubits4(x.u[m], ub + j + 2 * t) : 0u));
+                else sset(x.a[m], t, fg4<false>(sget(x.a[m], t), sget(x.b[m], t), 0u));
             }
             st(d1 + j, x.a[m]);
         }
@@ -662,14 +725,14 @@ __device__ __noinline__ void pchain(PairCtx c, int k, int n4, int ub, u32 gm)
 #pragma unroll
                 for (int m = 0; m < h; m++) {
 #pragma unroll
-                    for (int t = 0; t < 4; t++) x.a[m][t] = fg4<true>(x.a[m][t], x.a[m + h][t], 0u);
+                    for (int t = 0; t < 4; t++) sset(x.a[m], t, fg4<true>(sget(x.a[m], t), sget(x.a[m + h], t), 0u));
                     st(di + j0 + m * nl, x.a[m]);
                 }
             } else {
 #pragma unroll
                 for (int m = 0; m < h; m++) {
 #pragma unroll
-                    for (int t = 0; t < 4; t++) x.a[m][t] = fg4<false>(x.a[m][t], x.a[m + h][t], 0u);
+                    for (int t = 0; t < 4; t++) sset(x.a[m], t, fg4<false>(sget(x.a[m], t), sget(x.a[m + h], t), 0u));
                     st(di + j0 + m * nl, x.a[m]);
                 }
             }
@@ -711,14 +774,15 @@ __device__ __forceinline__ void pop_chain(const PairCtx &c, int k, int n4, int u
         }
         return;
     }
-    if (ROOT && !chan_quad(c).al) pchain<D, ROOT, ISG0, false>(c, k, n4, ub, gm);
+    if constexpr (PAIR_S16) pchain<D, ROOT, ISG0, false>(c, k, n4, ub, gm);   // (int16 channel: element loads)
+    else if (ROOT && !chan_quad(c).al) pchain<D, ROOT, ISG0, false>(c, k, n4, ub, gm);
     else pchain<D, ROOT, ISG0, true>(c, k, n4, ub, gm);
 }
 
 // source dwords of a pruned-node op (REP / R1 / SPC): rows j, j + 1 (j even) of the parent's
 // two halves, slot format
 template <bool ROOT, bool SL>
-__device__ __forceinline__ void psrc2(const PairCtx &c, int s0, int n4, int j, u32 &a, u32 &b)
+__device__ __forceinline__ void psrc2(const PairCtx &c, int s0, int n4, int j, su_t &a, su_t &b)
 {
     if constexpr (ROOT) {
         a = c.chan2(j);
@@ -738,7 +802,7 @@ __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int 
 {
     u32 acc = 0;
     for (int j = 0; j < n4; j += 2) {
-        u32 a, b;
+        su_t a, b;
         psrc2<ROOT, SL>(c, s0, n4, j, a, b);
 #pragma unroll
         for (int o = 0; o < 2; o++) {
@@ -752,7 +816,7 @@ __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int 
         const Lanes ln = c.lanes();
         acc = 0;
         for (int j = 0; j < n4; j += 2) {
-            u32 a, b;
+            su_t a, b;
             psrc2<ROOT, SL>(c, s0, n4, j, a, b);
 #pragma unroll
             for (int o = 0; o < 2; o++) {
@@ -782,7 +846,7 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
                                             bool part)
 {
     u32 acc = 0, par = 0, klo = 0xFFFFFFFFu, khi = 0xFFFFFFFFu, ud = 0;
-    u32 da = 0, db = 0;
+    su_t da{}, db{};
     const int row = (int)c.row();
     const u32 ksub = SPC ? spc_sub((u32)row, c.lanes()) : 0u;
     for (int j = j0; j < j1; j++) {
@@ -954,13 +1018,13 @@ __device__ __forceinline__ bool pair_init(PairCtx &c, const signed char *llr, un
     const long f_lo = PAIR_SOLO ? pair : 2 * pair, f_hi = 2 * pair + 1;
     const long fl = f_lo < batch ? f_lo : (long)batch - 1, fh = f_hi < batch ? f_hi : (long)batch - 1;
     const int off = 16 * (int)c.row() + (int)c.lanes().pos;
-    c.chl = (const g_u8 *)llr + fl * (long)N + off;
-    c.chh = PAIR_SOLO ? c.chl + 64 : (const g_u8 *)llr + fh * (long)N + off;   // (solo: words 8 j + 4 + r)
+    c.chl = (const g_chan *)llr + fl * (long)N + off;
+    c.chh = PAIR_SOLO ? c.chl + 64 : (const g_chan *)llr + fh * (long)N + off;   // (solo: words 8 j + 4 + r)
     g_u32 *base = (g_u32 *)scratch + pair * (long)pair_dwords;
-    c.hs = base + 4 * lane;
-    c.hb = base + (slot_rows >> 1) * 64 + lane;   // slot_rows x 128 B = slot_rows / 2 dword rows
-    c.ls = lbase + 4 * lane;
-    c.lxo = ((slot_rows > lds_row0 ? slot_rows - lds_row0 : 0) >> 1) * 64;
+    c.hs = base + GD * lane;
+    c.hb = base + slot_rows * 8 * GD + lane;   // slot_rows x 128 B (16-bit slots: 256 B)
+    c.ls = lbase + GD * lane;
+    c.lxo = (slot_rows > lds_row0 ? slot_rows - lds_row0 : 0) * 8 * GD;
     return f_lo < batch;
 }
 

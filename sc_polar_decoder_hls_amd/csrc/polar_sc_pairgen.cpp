@@ -678,13 +678,17 @@ std::string pair_source(const polar_sc_plan &p)
 {
     std::ostringstream o;
     const bool solo = p.solo != 0;
+    const bool s16 = p.cfg.llr_bits > 8;   // 16-bit slot rows (polar_sc_pair.h SLOT16)
     const int wpr = solo ? 8 : 4;
     o << "#define POLAR_LANE_REMAP 1\n" << (solo ? "#define POLAR_SOLO 1\n" : "") << "#define POLAR_Q " << p.cfg.llr_bits
       << "\n#define POLAR_LPAR "
       << (p.cfg.par == 64 ? 6 : p.cfg.par == 32 ? 5 : 4)
       << "\n" << (p.cfg.extended ? "" : "#define POLAR_EXT 0\n")   // EXTENDED = 0: saturating leaves
       << "#include \"polar_sc_pair.h\"\n"
-      << "namespace polar {\n" << kPairCH;
+      << "namespace polar {\n"
+      // (16-bit slots, LLR_BITS 9: a row pair is two SM16 dwords, 8-row groups of 8 dwords per lane)
+      << (s16 ? "#define SLOT(j) (*(const su_t *)(src_ + ((j) >> 3) * 512 + (((j) >> 1) & 3) * 2))\n" : "")
+      << (s16 ? kPairCH + std::string(kPairCH).find('\n') + 1 : kPairCH);
     int lg = 0;
     while ((1 << lg) < p.sub_words) lg++;
     // the decoder variants the kernels call (SUB records: reserved[1] = root kind), and the
@@ -710,18 +714,29 @@ std::string pair_source(const polar_sc_plan &p)
     // which gives back the root rows exactly, -0 included)
     const int rp = p.sub_words / wpr / 2;   // row-pair dwords of the root slot
     const int tot = p.pair_fused ? 2 * rp : rp;
+    const int gd = s16 ? 8 : 4;             // dwords per lane of an 8-row group
     o << "extern \"C\" __global__ void __launch_bounds__(64) polar_sc_pair_subtest_kernel(\n"
       << "    const unsigned short *__restrict__ in, unsigned int *__restrict__ out, int id)\n{\n"
-      << "  __shared__ unsigned int rows_[" << (tot < 4 ? 4 : tot) << " * 64];\n"
+      << "  __shared__ unsigned int rows_[" << (tot < 4 ? 4 : tot) * gd / 4 << " * 64];\n"
       << "  const int lane = threadIdx.x & 63;\n";
-    if (p.pair_fused)
-        o << "  for (int i = " << rp << "; i < " << tot << "; i++) rows_[(i >> 2) * 256 + 4 * lane + (i & 3)] = QMAG * 0x01010101u;\n";
-    o << "  for (int i = 0; i < " << rp << "; i++) {\n"
-      << "    const unsigned int r0 = in[128 * i + lane], r1 = in[128 * i + 64 + lane];\n"
-      << "    rows_[(i >> 2) * 256 + 4 * lane + (i & 3)] = (r0 & 0xFFu) | ((r1 & 0xFFu) << 8) | ((r0 >> 8) << 16) |\n"
-      << "                                                ((r1 >> 8) << 24);\n"
-      << "  }\n"
-      << "  const unsigned int *src = rows_ + 4 * lane;\n"
+    if (!s16) {
+        if (p.pair_fused)
+            o << "  for (int i = " << rp << "; i < " << tot << "; i++) rows_[(i >> 2) * 256 + 4 * lane + (i & 3)] = QMAG * 0x01010101u;\n";
+        o << "  for (int i = 0; i < " << rp << "; i++) {\n"
+          << "    const unsigned int r0 = in[128 * i + lane], r1 = in[128 * i + 64 + lane];\n"
+          << "    rows_[(i >> 2) * 256 + 4 * lane + (i & 3)] = (r0 & 0xFFu) | ((r1 & 0xFFu) << 8) | ((r0 >> 8) << 16) |\n"
+          << "                                                ((r1 >> 8) << 24);\n"
+          << "  }\n";
+    } else {   // the SM8 test rows as SM16 pairs, two dwords per row pair
+        if (p.pair_fused)
+            o << "  for (int i = " << 2 * rp << "; i < " << 2 * tot << "; i++) rows_[(i >> 3) * 512 + 8 * lane + (i & 7)] = QMAG * 0x00010001u;\n";
+        o << "  for (int i = 0; i < " << 2 * rp << "; i++) {\n"
+          << "    const unsigned int v = in[64 * i + lane];\n"
+          << "    rows_[(i >> 3) * 512 + 8 * lane + (i & 7)] = (v & 0x7Fu) | ((v & 0x80u) << 8) | (((v >> 8) & 0x7Fu) << 16) |\n"
+          << "                                                ((v & 0x8000u) << 16);\n"
+          << "  }\n";
+    }
+    o << "  const unsigned int *src = rows_ + " << gd << " * lane;\n"
       << "  switch (id) {\n";
     for (size_t id = 0; id < p.subs.size(); id++)
         o << "  case " << id << ": polar_psub_" << id << (p.pair_fused ? "_F" : "") << "(src, (g_u32 *)out + lane, 0); return;\n";

@@ -18,6 +18,8 @@ struct DevState {
     void *ops = nullptr;          // schedule (interpreter kernels)
     void *scratch = nullptr;      // HBM stage scratch (interpreter, large N)
     size_t scratch_bytes = 0;
+    void *wide = nullptr;         // int16 copy of an int8 batch (pair plans of 9-bit LLRs)
+    size_t wide_bytes = 0;
     hipModule_t module = nullptr; // per-mask kernel
     hipFunction_t fn = nullptr;
     hipFunction_t fn_trace = nullptr;   // hybrid plans: the per-op monitor variant
@@ -161,6 +163,9 @@ struct polar_sc_plan {
     int pair_slot_rows = 0;          // stage-slot rows per pair / solo frame (levels of nodes G/2 .. sub_words, or 2 sub_words when fused)
     int pair_dwords = 0;             // HBM scratch per pair / frame: slot rows (128 B) + bit dwords (256 B)
     int wpr() const { return solo ? 8 : 4; }   // words of one (virtual) frame per slot row
+    // bytes of a slot row (64 lanes): SM8 pairs, or SM16 pairs for 9-bit LLRs (polar_sc_pair.h SLOT16)
+    int slot_row_bytes() const { return cfg.llr_bits > 8 ? 256 : 128; }
+    bool slot16() const { return pair && cfg.llr_bits > 8; }
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;
     mutable std::mutex host_mu;                             // polar_sc_decode_host staging

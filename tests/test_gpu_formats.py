@@ -1,8 +1,8 @@
 """GPU parity across the reference's swept datapath formats: PAR 4 / 8 / 16 / 32 / 64
 (polar_parameters.h:8; script_tests.sh:11,124 sweeps 16 and 64), CA2 vs SIGMAG (config.h:11;
 script/parser.sh:15,43), EXTENDED 0/1 (config.h:14) and LLR_BITS up to 9 (parser_comp.sh:12;
-int16 channel). Every format runs the schedule interpreter compiled by hipRTC with its
-POLAR_* switches and must equal the literal FSM at the same format bit for bit, on AWGN
+int16 channel). Formats without a generated kernel run the schedule interpreter compiled by
+hipRTC with their POLAR_* switches; every format must equal the literal FSM at the same format bit for bit, on AWGN
 frames, on the whole input range (incl. the -2^(Q-1) wrap of CA2) and under PRUNING_LEVEL 0 /
 1 / 2 configurations. Masks cover the LDS (N <= 4096) and HBM-scratch (N = 16384) storage."""
 import numpy as np
@@ -50,6 +50,8 @@ def test_formats_vs_oracle(pkg, cuda, oracle_mod, fmt):
                 assert dec.stats["kernel"] in (1, 3), (name, fmt, c7, dec.stats["kernel"])
             if par in (32, 64) and sigmag == 1 and q <= 8 and c7[0] != 1 and mask.size >= 2048:
                 assert dec.stats["kernel"] == 3, (name, fmt, c7, dec.stats["kernel"])   # the pair kernel
+            if par == 16 and sigmag == 1 and q == 9 and mask.size >= 2048:   # 16-bit slots
+                assert dec.stats["kernel"] == 3, (name, fmt, c7, dec.stats["kernel"])
 
 
 @pytest.mark.parametrize("q", [6, 9])
@@ -82,6 +84,34 @@ def test_int16_channel_hybrid_plans(pkg, cuda, oracle_mod, name):
     cuda.cuda.synchronize()
     assert (a.cpu().numpy() == b.cpu().numpy()).all()
     _assert_same(pkg.unpack_bits(b.cpu().numpy(), mask.size), oracle_mod.decode_fsm(mask, llr), "i16 " + name)
+
+
+@pytest.mark.parametrize("name", ["frozen_n_2048_k_1024", "frozen_n_16384_k_8192", "frozen_n_65536_k_32768", "struct"])
+def test_llr9_pair_kernel(pkg, cuda, oracle_mod, name):
+    """LLR_BITS 9 on the pair kernel (polar_sc_pair.h SLOT16: SM16 stage slots, the int16
+    channel): the whole 9-bit input range incl. -256 and +-255, both EXTENDED switches, the
+    int16 entry point and the int8 one (widened on the device), equal to the FSM at LLR_BITS 9."""
+    from sc_polar_decoder_hls_amd._plansets import struct_masks
+    mask = struct_masks(8192)[1] if name == "struct" else util.mask(name)
+    rng = np.random.default_rng(mask.size + 9)
+    awgn, _ = util.synth_frames(mask, 6, ebn0_db=1.0, seed=9)
+    awgn = np.clip(awgn.astype(np.int32) * 8, -255, 255)
+    edge = rng.integers(-256, 256, size=(3, mask.size))
+    edge[0, rng.integers(0, mask.size, 64)] = -256
+    llr = np.concatenate([awgn, edge]).astype(np.int16)
+    small = np.clip(llr, -128, 127).astype(np.int8)
+    for ext in (1, 0):
+        c = pkg.default_config()
+        c.llr_bits, c.extended = 9, ext
+        dec = pkg.Decoder(mask, config=c)
+        assert dec.stats["kernel"] == 3, dec.stats["kernel"]
+        out = dec.decode(cuda.from_numpy(llr).cuda())
+        out8 = dec.decode(cuda.from_numpy(small).cuda())
+        cuda.cuda.synchronize()
+        _assert_same(pkg.unpack_bits(out.cpu().numpy(), mask.size),
+                     oracle_mod.decode_fsm(mask, llr, llr_bits=9, extended=ext), "%s i16 ext %d" % (name, ext))
+        _assert_same(pkg.unpack_bits(out8.cpu().numpy(), mask.size),
+                     oracle_mod.decode_fsm(mask, small, llr_bits=9, extended=ext), "%s i8 ext %d" % (name, ext))
 
 
 def test_formats_noiseless_full_size(pkg, cuda):

@@ -42,6 +42,9 @@ def test_pair_plan_stats(pkg):
     assert s1["scratch_bytes_per_wave"] == (4096 - 256) // 4 * 128 + 4096 // 64 * 256
     assert "_F(c.slot_ptr" in pair(pkg, util.mask("frozen_n_65536_k_32768")).kernel_source()
     assert "_F(c.slot_ptr" not in pair(pkg, util.mask("frozen_n_65536_k_32768"), sub_root=1).kernel_source()
+    # automatic: fused from 16 subtrees per frame on (N = 16384, G = 4 S: slot roots)
+    assert "_F(c.slot_ptr" not in pair(pkg, util.mask("frozen_n_16384_k_8192")).kernel_source()
+    assert "_F(c.slot_ptr" in pair(pkg, util.mask("frozen_n_16384_k_8192"), sub_root=2).kernel_source()
     s = pair(pkg, util.mask("frozen_n_2048_k_1024")).stats
     assert s["sub_words"] == 64
     s = pair(pkg, util.mask("frozen_n_262144_k_131072"), tier_words=1024).stats

@@ -19,7 +19,21 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 CONFIGS = {"c3": ("frozen_n_65536_k_32768", 4096), "c5": ("frozen_n_262144_k_131072", 512),
            "c5_64": ("frozen_n_262144_k_131072", 64), "c3_2048": ("frozen_n_65536_k_32768", 2048),
            "c3_1024": ("frozen_n_65536_k_32768", 1024), "n16384_4096": ("frozen_n_16384_k_8192", 4096),
-           "n16384_256": ("frozen_n_16384_k_8192", 256), "n65536_256": ("frozen_n_65536_k_32768", 256)}
+           "n16384_256": ("frozen_n_16384_k_8192", 256), "n65536_256": ("frozen_n_65536_k_32768", 256),
+           # (bench.py's secondary entries: polar_sc_config fields as a third element)
+           "q8_4096": ("frozen_n_16384_k_14746", 4096, {"llr_bits": 8}),
+           "par64_4096": ("frozen_n_16384_k_8192", 4096, {"par": 64})}
+
+
+def config_of(pkg, name):
+    """the polar_sc_config of a CONFIGS entry (None: the reference's default)"""
+    fields = CONFIGS[name][2] if len(CONFIGS[name]) > 2 else None
+    if not fields:
+        return None
+    c = pkg.default_config()
+    for k, v in fields.items():
+        setattr(c, k, v)
+    return c
 DEFAULT_VARIANTS = "layout=1;layout=2;layout=2,sub_words=512"
 
 
@@ -51,27 +65,28 @@ def main():
         for name in args.configs.split(","):
             mask = util.mask(CONFIGS[name][0])
             for t in variants:
-                d = pkg.Decoder(mask, tuning=t)
+                d = pkg.Decoder(mask, config=config_of(pkg, name), tuning=t)
                 d.compile()
                 print("prewarmed", name, t, flush=True)
         return
     import torch
     from oracle import oracle
     for name in args.configs.split(","):
-        mname, batch = CONFIGS[name]
+        mname, batch = CONFIGS[name][:2]
+        cfg = config_of(pkg, name)
         mask = util.mask(mname)
         N, K = mask.size, int(mask.sum())
         llr, _ = pkg.csim_frames(N, batch, pkg.csim_sigma(2.5, K / N), seed=0xF0)
         decs = []
         for t in variants:
-            d = pkg.Decoder(mask, tuning=t)
+            d = pkg.Decoder(mask, config=cfg, tuning=t)
             d.prepare(batch)
             out = d.decode(llr)
             torch.cuda.synchronize()
             decs.append((t, d, out))
         ref = decs[0][2].cpu()
         sample = llr[: args.check].cpu().numpy()
-        want = oracle.decode_fsm(mask, sample)
+        want = oracle.decode_fsm(mask, sample, **(CONFIGS[name][2] if len(CONFIGS[name]) > 2 else {}))
         checks = []
         for t, d, out in decs:
             got = pkg.unpack_bits(out[: args.check].cpu().numpy(), N)

@@ -42,7 +42,8 @@ def main():
     print("launch_info " + json.dumps(dict(dec.launch_info(a.batch), mask=a.mask, batch=a.batch, tuning=tun,
                                            config=fmt)), flush=True)
     nb = a.rotate if a.rotate > 0 else max(1, min(8, -(-bench.ROTATE_BYTES // (a.batch * mask.size))))
-    llrs = [bench.gen_frames_torch(torch, mask, a.batch, a.ebn0, 0xF0 + b, dev)[0] for b in range(nb)]
+    llrs = [bench.widen_q9(torch, bench.gen_frames_torch(torch, mask, a.batch, a.ebn0, 0xF0 + b, dev)[0], fmt)
+            for b in range(nb)]
     out = torch.empty((a.batch, dec.words), dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     for i in range(a.reps):
