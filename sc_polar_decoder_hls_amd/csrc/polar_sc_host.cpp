@@ -863,9 +863,8 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // pair plans also take PAR 32 / 64 (the PAR word = one register of two / four device words;
     // the host expands its leaf into F / G / 16-LLR leaf records, par_expand: G_extended when
     // EXTENDED, the saturating G and POLAR_EXT 0 leaves when not)
-    // and 9-bit LLRs at PAR 16 (16-bit stage slots, the int16 channel: polar_sc_pair.h SLOT16)
-    const bool pair_fmt = dflt || ((c.par == 32 || c.par == 64) && c.sigmag == 1 && c.llr_bits <= 8) ||
-                          (c.par == 16 && c.sigmag == 1 && c.llr_bits == 9);
+    // and 9-bit LLRs (16-bit stage slots, the int16 channel: polar_sc_pair.h SLOT16)
+    const bool pair_fmt = dflt || ((c.par == 16 || c.par == 32 || c.par == 64) && c.sigmag == 1 && c.llr_bits <= 9);
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR
     // level's F / G / H then run inside the straight-line code instead of as interpreter ops
