@@ -217,15 +217,28 @@ struct Gen {
     {
         for (int k = 0; k < planes(words); k++) o << "  s" << LG << "[" << k << "] = 0u;\n";
         if (pack) {
+            // one SM8 lookup per channel byte (sign bit 7, magnitude below): the four bytes of
+            // a packed root register (a0 = word i lo, b0 = word j lo, a1 = word i hi, b1 = word
+            // j hi) give its magnitudes by one mask and the sign-plane bits of words i and j by
+            // one shift + and-or each (bits 7 / 23 and 15 / 31 land on bits i % 16 / 16 + i % 16)
             const int h = words / 2;
             for (int i = 0; i < h; i++) {
-                const int j = i + h;
-                o << "  { const u32 a0_ = chl[" << 16 * i << "], a1_ = chh[" << 16 * i << "], b0_ = chl[" << 16 * j
+                const int j = i + h, si = 7 - i % 16, sj = 15 - j % 16;
+                const std::string shi = si >= 0 ? "(r_ >> " + std::to_string(si) + ")" : "(r_ << " + std::to_string(-si) + ")";
+                o << "#ifndef POLAR_PRESPLIT_TABS\n"
+                  << "  { const u32 r_ = (u32)tab8_[chl[" << 16 * i << "]] | ((u32)tab8_[chl[" << 16 * j << "]] << 8) | ((u32)tab8_[chh["
+                  << 16 * i << "]] << 16) | ((u32)tab8_[chh[" << 16 * j << "]] << 24);\n"
+                  << "    pr[" << i << "] = r_ & (QMAG * 0x01010101u);\n"
+                  << "    s" << LG << "[" << i / 16 << "] |= " << shi << " & " << (0x00010001u << (i % 16)) << "u;\n"
+                  << "    s" << LG << "[" << j / 16 << "] |= (r_ >> " << sj << ") & " << (0x00010001u << (j % 16)) << "u; }\n"
+                  // (A/B: -DPOLAR_PRESPLIT_TABS, the separate magnitude and sign tables of round 2)
+                  << "#else\n"
+                  << "  { const u32 a0_ = chl[" << 16 * i << "], a1_ = chh[" << 16 * i << "], b0_ = chl[" << 16 * j
                   << "], b1_ = chh[" << 16 * j << "];\n"
                   << "    pr[" << i << "] = (u32)tabm_[a0_] | ((u32)tabm_[b0_] << 8) | ((u32)tabm_[a1_] << 16) | ((u32)tabm_[b1_] << 24);\n"
                   << "    s" << LG << "[" << i / 16 << "] |= ((u32)tabs_[a0_] | ((u32)tabs_[a1_] << 16)) << " << i % 16 << ";\n"
                   << "    s" << LG << "[" << j / 16 << "] |= ((u32)tabs_[b0_] | ((u32)tabs_[b1_] << 16)) << " << j % 16
-                  << "; }\n";
+                  << "; }\n#endif\n";
                 chunk_fence(i, h);
             }
             return;
@@ -478,9 +491,10 @@ struct Gen {
           << ") polar_sc_mask_kernel(\n"
           << "    const unsigned char *__restrict__ llr, unsigned short *__restrict__ out, int batch, int out_stride)\n{\n"
           << "  __shared__ uint4 stage_[" << wpb << " * 8 * " << FS / 16 << "];\n"
-          << "  __shared__ unsigned char tabm_[256], tabs_[256];   // channel byte -> |LLR|, sign (qconv_format)\n"
+          // channel byte -> SM8 (qconv_format; bit 7 sign), and -> |LLR|, sign for the unpacked root
+          << "  __shared__ unsigned char tab8_[256], tabm_[256], tabs_[256];\n"
           << "  for (u32 t_ = threadIdx.x; t_ < 256u; t_ += " << 64 * wpb << "u) { const u32 v_ = sm8_of_byte(t_);\n"
-          << "    tabm_[t_] = (unsigned char)(v_ & QMAG); tabs_[t_] = (unsigned char)(v_ >> 7); }\n"
+          << "    tab8_[t_] = (unsigned char)v_; tabm_[t_] = (unsigned char)(v_ & QMAG); tabs_[t_] = (unsigned char)(v_ >> 7); }\n"
           << "  __syncthreads();\n"
           << "  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR batch indices\n"
           << "  const long nw_ = ((long)batch + 7) / 8;\n"
