@@ -226,8 +226,16 @@ struct Gen {
                 const int j = i + h, si = 7 - i % 16, sj = 15 - j % 16;
                 const std::string shi = si >= 0 ? "(r_ >> " + std::to_string(si) + ")" : "(r_ << " + std::to_string(-si) + ")";
                 o << "#ifndef POLAR_PRESPLIT_TABS\n"
+                  // (byte packing by two v_perm_b32 + OR; -DPOLAR_PRESPLIT_SHIFT: by shifts, the compiler's
+                  // shift / OR3 forms)
+                  << "#ifndef POLAR_PRESPLIT_SHIFT\n"
+                  << "  { const u32 r_ = __builtin_amdgcn_perm((u32)tab8_[chl[" << 16 * j << "]], (u32)tab8_[chl[" << 16 * i
+                  << "]], 0x0C0C0400u) | __builtin_amdgcn_perm((u32)tab8_[chh[" << 16 * j << "]], (u32)tab8_[chh[" << 16 * i
+                  << "]], 0x04000C0Cu);\n"
+                  << "#else\n"
                   << "  { const u32 r_ = (u32)tab8_[chl[" << 16 * i << "]] | ((u32)tab8_[chl[" << 16 * j << "]] << 8) | ((u32)tab8_[chh["
                   << 16 * i << "]] << 16) | ((u32)tab8_[chh[" << 16 * j << "]] << 24);\n"
+                  << "#endif\n"
                   << "    pr[" << i << "] = r_ & (QMAG * 0x01010101u);\n"
                   << "    s" << LG << "[" << i / 16 << "] |= " << shi << " & " << (0x00010001u << (i % 16)) << "u;\n"
                   << "    s" << LG << "[" << j / 16 << "] |= (r_ >> " << sj << ") & " << (0x00010001u << (j % 16)) << "u; }\n"
