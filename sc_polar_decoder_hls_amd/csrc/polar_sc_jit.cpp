@@ -349,8 +349,17 @@ struct Gen {
             for (int k = 0; k < np; k++)
                 o << "    FS_[" << k << "] = " << P(sd, 16 * k) << " ^ " << P(sd, n + 16 * k) << ";\n";
             for (int i = 0; i < n; i++) {
-                o << "    acc_ = rep_acc(acc_, row_sum_biased(F_split_biased<" << i % 16 << ">(" << M(sd, i) << ", "
-                  << M(sd, n + i) << ", FS_[" << i / 16 << "])));\n";
+                const std::string t = "row_sum_biased(F_split_biased<" + std::to_string(i % 16) + ">(" + M(sd, i) + ", " +
+                                      M(sd, n + i) + ", FS_[" + std::to_string(i / 16) + "]))";
+                if (i + 1 < n) {
+                    o << "    acc_ = rep_acc(acc_, " << t << ");\n";
+                } else {
+                    // the last step without the clamp: a clamp keeps the sign and zero, and the
+                    // unclamped sum (|acc| <= 511 plus one word, <= 1007) fits the 16-bit half
+                    // (-DPOLAR_REP_CLAMP_LAST: clamped, for A/Bs)
+                    o << "#ifndef POLAR_REP_CLAMP_LAST\n    acc_ = pk_sub(pk_add(acc_, " << t << "), 0x20002000u);\n#else\n"
+                      << "    acc_ = rep_acc(acc_, " << t << ");\n#endif\n";
+                }
                 chunk_fence(i, n);
             }
             o << "    if (rep_any_zero(acc_)) {\n      acc_ = 0u;\n";
