@@ -345,11 +345,16 @@ struct Gen {
         }
         case POLAR_OP_REP: {
             // value chain in two's complement; the exact SM chain only when a total is 0
+            o << "#ifndef REP_FSB\n#ifndef POLAR_REP_FSB\n"
+                 "#define REP_FSB(I, a, b, fs) pk_mad_u16(pk_min(a, b), plane_mask<I>(fs) | 0x00010001u, 0x02000200u)\n"
+                 "#else\n#define REP_FSB(I, a, b, fs) F_split_biased<I>(a, b, fs)\n#endif\n#endif\n";
             o << "  { // REP n " << n << " pos " << op.pos << "\n    u32 acc_ = 0u, full_, FS_[" << np << "];\n";
             for (int k = 0; k < np; k++)
                 o << "    FS_[" << k << "] = " << P(sd, 16 * k) << " ^ " << P(sd, n + 16 * k) << ";\n";
             for (int i = 0; i < n; i++) {
-                const std::string t = "row_sum_biased(F_split_biased<" + std::to_string(i % 16) + ">(" + M(sd, i) + ", " +
+                // the F value + 512 per half as one multiply-add: |F| x (+1 / -1) + 512 (the sign
+                // plane's mask OR 1 is -1 / +1 per half; F_split_biased with -DPOLAR_REP_FSB)
+                const std::string t = "row_sum_biased(REP_FSB(" + std::to_string(i % 16) + ", " + M(sd, i) + ", " +
                                       M(sd, n + i) + ", FS_[" + std::to_string(i / 16) + "]))";
                 if (i + 1 < n) {
                     o << "    acc_ = rep_acc(acc_, " << t << ");\n";
