@@ -383,14 +383,23 @@ struct Gen {
             const bool spc = op.code == POLAR_OP_SPC;
             o << "  { // " << (spc ? "SPC" : "R1") << " n " << n << " pos " << op.pos << " upos " << op.upos << "\n";
             xplanes(sd, n, op.upos);
-            if (spc) o << "    u32 klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu, par_ = 0u;\n";
+            // SPC keys (|lambda|, word, bitrev4(position)): for nodes of <= 64 words both frames'
+            // keys fit the 16-bit halves of one register (|lambda| <= GSAT <= 63 in 6 bits, the
+            // word in 6, the position added after the loop), one packed min per word
+            // (-DPOLAR_SPC_KEY32: a 32-bit key per frame, for A/Bs)
+            const bool k16 = n <= 64;
+            if (spc) o << "    u32 klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu, par_ = 0u, kk_ = 0xFFFFFFFFu;\n";
             for (int i = 0; i < n; i++) {
-                if (spc)
+                if (spc) {
                     o << "    { const u32 l_ = G_split<" << i % 16 << ">(" << M(sd, i) << ", " << M(sd, n + i) << ", X_["
-                      << i / 16 << "], LT_[" << i / 16 << "]);\n"
-                      << "      klo_ = __builtin_elementwise_min(klo_, (l_ << 24) | " << (i << 4) << "u);\n"
-                      << "      khi_ = __builtin_elementwise_min(khi_, ((l_ >> 16) << 24) | " << (i << 4) << "u); }\n";
-                else
+                      << i / 16 << "], LT_[" << i / 16 << "]);\n";
+                    if (k16)
+                        o << "#ifndef POLAR_SPC_KEY32\n      kk_ = pk_min(kk_, pk_shl(l_, 10) | " << ((i << 4) * 0x00010001u)
+                          << "u);\n#else\n";
+                    o << "      klo_ = __builtin_elementwise_min(klo_, (l_ << 24) | " << (i << 4) << "u);\n"
+                      << "      khi_ = __builtin_elementwise_min(khi_, ((l_ >> 16) << 24) | " << (i << 4) << "u);\n"
+                      << (k16 ? "#endif\n" : "") << "    }\n";
+                } else
                     o << "    LT_[" << i / 16 << "] = plane_put<" << i % 16 << ">(LT_[" << i / 16 << "], pk_sub(" << M(sd, i)
                       << ", " << M(sd, n + i) << "));\n";
                 chunk_fence(i, n);
@@ -409,10 +418,15 @@ struct Gen {
                     const unsigned m = (1u << n) - 1u;
                     o << "    par_ &= 0x" << std::hex << (m | (m << 16)) << std::dec << "u;\n";
                 }
+                if (k16) o << "#ifndef POLAR_SPC_KEY32\n    klo_ = kk_ & 0xFFFFu; khi_ = kk_ >> 16;\n#endif\n";
                 o << "    par_ = ((__builtin_popcount(par_ & 0xFFFFu) & 1u) << 15) | ((__builtin_popcount(par_ >> 16) & 1u) << 31);\n"
                      "    par_ = row_xor(par_);\n"
-                     "    klo_ = row_min_u32(klo_ | ln.br); khi_ = row_min_u32(khi_ | ln.br);\n"
-                     "    const u32 ilo_ = (klo_ >> 4) & 0xFFFFFu, ihi_ = (khi_ >> 4) & 0xFFFFFu;\n"
+                     "    klo_ = row_min_u32(klo_ | ln.br); khi_ = row_min_u32(khi_ | ln.br);\n";
+                // the word index: bits 4.. of the key (16-bit keys: bits 4..9, |lambda| above)
+                if (k16) o << "#ifndef POLAR_SPC_KEY32\n    const u32 ilo_ = (klo_ >> 4) & 63u, ihi_ = (khi_ >> 4) & 63u;\n#else\n";
+                o << "    const u32 ilo_ = (klo_ >> 4) & 0xFFFFFu, ihi_ = (khi_ >> 4) & 0xFFFFFu;\n";
+                if (k16) o << "#endif\n";
+                o <<
                      "    const bool flo_ = (par_ & 0x8000u) && (klo_ & 15u) == ln.br;\n"
                      "    const bool fhi_ = (par_ & 0x80000000u) && (khi_ & 15u) == ln.br;\n";
                 if (n <= 16) {
