@@ -280,6 +280,8 @@ SECONDARY = (
     ("c5", "frozen_n_262144_k_131072", None, {}, "BASELINE configs[4]: N=262144 K=131072, 512 frames sharded over the GPUs"),
     ("c5_share64", "frozen_n_262144_k_131072", 64, {},
      "C5's 8-GPU share (64 frames) on one GPU: the per-GPU latency of configs[4] at 8 GPUs"),
+    ("c4_share", "FB_N1024_K512", 131072, {},
+     "C4's 8-GPU share (2^20 / 8 = 131072 frames of N=1024 K=512) on one GPU: the per-GPU work of configs[3] at 8 GPUs"),
     # script/script_tests.sh:11,124 runs PAR 16 and PAR 64; :7-9 the rate-0.9 codes at QUANT 8
     ("par16_n16384", "frozen_n_16384_k_8192", SWEEP_FRAMES, {},
      "PAR 16 (the shipped datapath) on N=16384 K=8192, %d frames per GPU: the PAR 64 entry's baseline" % SWEEP_FRAMES),
@@ -601,8 +603,8 @@ def main():
     if args.secondary and args.config == "c2" and not args.batch:
         secondary = {}
         for key, mname, pg, fmt, note in SECONDARY:
-            if key == "c5_share64" and world != 1:
-                continue   # at 8 GPUs the c5 entry already is the 64-frame share
+            if key in ("c5_share64", "c4_share") and world != 1:
+                continue   # 8-GPU shares, timed on one GPU (at N > 1 each rank's own share is the c2 / c5 work)
             secondary[key] = secondary_entry(torch, pkg, sharding, dist, coll_dev, args, key, mname, pg, fmt, note,
                                              rank, world, dev, stream)
         if "par16_n16384" in secondary and "par64_n16384" in secondary:

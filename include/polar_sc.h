@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define POLAR_SC_ABI_VERSION 4
+#define POLAR_SC_ABI_VERSION 5
 #define POLAR_SC_PAR 16
 
 /*
@@ -247,7 +247,12 @@ int polar_sc_decode_i16(const polar_sc_plan *plan, const int16_t *llr_dev, uint6
                         size_t batch, void *stream);
 
 /* Upload the schedule and reserve device scratch for up to max_batch frames on the
- * current device, so that later polar_sc_decode calls allocate nothing. */
+ * current device, so that later polar_sc_decode calls allocate nothing. An automatic-layout
+ * pair plan (polar_sc_launch_info.alt_layout != 0) decodes batches of at most alt_max_batch
+ * frames with its solo alternate: prepare sets up the plan that decodes max_batch frames,
+ * and the other one is set up by the first decode that needs it (call prepare once per batch
+ * class before graph capture; polar_sc_tuning.layout = 1 builds no alternate at all).
+ * polar_sc_plan_compile builds both kernels of such a plan. */
 int polar_sc_plan_prepare(const polar_sc_plan *plan, size_t max_batch);
 
 /* Host-pointer convenience: copies in, decodes, copies out, synchronises.
@@ -316,6 +321,12 @@ typedef struct polar_sc_launch_info {
                                    process, or a code object it cached) or
                                    POLAR_SC_COMPILER_HIPRTC (hipRTC: no clang driver, or a GPU
                                    already open and no cached clang object); 0 = none */
+    uint32_t alt_layout;        /* automatic-layout pair plans: the layout of the alternate
+                                   plan that decodes small batches (2 = solo), 0 = the plan
+                                   has none (forced layout, PAR != 16, LLR_BITS 9, or a
+                                   frame the solo code cannot take) */
+    uint64_t alt_max_batch;     /* batches of at most this many frames (2 per SIMD of `cus`
+                                   compute units) decode with the alternate; 0 = none */
 } polar_sc_launch_info;
 
 enum { POLAR_SC_COMPILER_CLANG = 1, POLAR_SC_COMPILER_HIPRTC = 2 };

@@ -99,7 +99,8 @@ class polar_sc_launch_info(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_uint32), ("regs", ctypes.c_uint32), ("regs_seg", ctypes.c_uint32),
                 ("waves_per_block", ctypes.c_uint32), ("blocks", ctypes.c_uint64), ("lds_bytes", ctypes.c_uint32),
                 ("lds_row0", ctypes.c_uint32), ("code_key", ctypes.c_uint64), ("layout", ctypes.c_uint32),
-                ("sub_words", ctypes.c_uint32), ("compiler", ctypes.c_uint32)]
+                ("sub_words", ctypes.c_uint32), ("compiler", ctypes.c_uint32), ("alt_layout", ctypes.c_uint32),
+                ("alt_max_batch", ctypes.c_uint64)]
 
 
 # exported symbols of include/polar_sc.h (tests check that the library exports all of them)
@@ -272,6 +273,19 @@ def _torch():
     return torch
 
 
+def _device_cus():
+    """compute units of torch's current GPU once torch has initialised it, else 0. Never
+    opens the GPU itself: a process with the GPU open compiles generated kernels with hipRTC
+    instead of the clang driver (polar_sc_jit.cpp)."""
+    try:
+        import torch
+        if torch.cuda.is_initialized():
+            return int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+    except Exception:
+        pass
+    return 0
+
+
 class Decoder:
     """A compiled decode plan for one frozen-bit table (== my_module after do_prunning).
 
@@ -343,9 +357,13 @@ class Decoder:
         _check("polar_sc_plan_compile", rc)
         return True
 
-    def launch_info(self, batch, cus=0):
+    def launch_info(self, batch, cus=None):
         """Launch shape of a decode of `batch` frames (polar_sc_plan_launch_info, host only:
-        compiles the generated kernel if needed) as a dict; code_key as 16 hex digits."""
+        compiles the generated kernel if needed) as a dict; code_key as 16 hex digits.
+        cus=None: the compute units of the current GPU when torch sees one (the count the
+        decode itself uses to pick the layout), else 0 (= 256, MI355X)."""
+        if cus is None:
+            cus = _device_cus()
         r = polar_sc_launch_info()
         _check("polar_sc_plan_launch_info", lib().polar_sc_plan_launch_info(self._plan, int(batch), int(cus),
                                                                             ctypes.byref(r)))

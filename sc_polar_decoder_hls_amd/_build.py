@@ -81,7 +81,7 @@ def build(force=False, verbose=False):
     ver = "".join(ch for ch in ver if ch.isalnum() or ch in " .-_()/+:")
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
            '-DPOLAR_ROCM_CLANG="%s"' % clang, '-DPOLAR_ROCM_CLANG_VERSION="%s"' % ver,
-           "-I" + os.path.join(ROOT, "include"), "-I" + GEN_DIR] + SOURCES + ["-o", tmp, "-lhiprtc"]
+           "-I" + os.path.join(ROOT, "include"), "-I" + GEN_DIR] + SOURCES + ["-o", tmp, "-lhiprtc", "-lz"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -157,7 +157,9 @@ def cpu_test_plans():
     return [("struct32768_0", struct_masks(32768)[0], {"kernel": 3, "layout": 1, "sub_words": sw, "chain_max": 4,
                                                        "sub_root": 1}) for sw in (64, 256)] + \
         [("struct16384_0", struct_masks(16384)[0], {"kernel": 3, "layout": 1, "sub_words": 64, "chain_max": 4,
-                                                    "sub_root": 1})]
+                                                    "sub_root": 1}),
+         # tests/test_solo.py::test_solo_plan_stats: a pair-tuned automatic plan and its solo alternate
+         ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), {"sub_words": 64, "waves_per_group": 2})]
 
 
 # ---- datapath formats (tests/test_gpu_formats.py): (PAR, SIGMAG, EXTENDED, LLR_BITS) ---------

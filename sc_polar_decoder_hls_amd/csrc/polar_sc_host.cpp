@@ -900,7 +900,9 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     bool use_pair = false;
     if (want_pair) {
         const int wpr = solo ? 8 : 4;
-        int S = std::min<int>(polar_host::PAIR_SUB_WORDS, (int)p->G / 2);
+        // default subtree size: 256 words (pair), 512 (solo: half the registers per word), both
+        // at most half the frame; one default for a forced and the automatic solo plan
+        int S = std::min<int>(solo ? polar_host::SOLO_SUB_WORDS_MAX : polar_host::PAIR_SUB_WORDS, (int)p->G / 2);
         if (t.sub_words) {
             // the halves of every upper node are whole 8-row slot groups: >= 32 words (pair),
             // >= 64 (solo); at most 256 (pair) / 512 (solo) words of register code
@@ -1056,14 +1058,16 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         s.lds_bytes_per_wave = (uint32_t)((p->pair_fused ? 2 : 1) * p->sub_words / p->wpr()) * (uint32_t)p->slot_row_bytes();
         s.scratch_bytes_per_wave = (uint64_t)p->pair_dwords * 4u;
     }
-    // automatic layout: a PAR 16 pair plan also holds its solo plan (subtrees of up to 512
-    // words), which small batches decode with (layout_for); none when the tuning cannot carry
-    // over (a subtree size below 64 words)
+    // automatic layout: a PAR 16 pair plan also holds its solo plan, which small batches decode
+    // with (layout_for). The alternate takes the solo defaults (subtrees of min(512, N / 32)
+    // words, automatic waves, LDS levels and subtree roots), not the pair plan's tuning, which
+    // was chosen for the other layout; only the way subtree decoders are built
+    // (sub_inline) carries over. polar_sc_tuning.layout = 1 builds no alternate.
     if (p->pair && !p->solo && t.layout == 0 && c.par == 16 && c.llr_bits <= 8) {
-        polar_sc_tuning ts = t;
+        polar_sc_tuning ts{};
         ts.layout = 2;
         ts.kernel = 3;
-        if (!ts.sub_words) ts.sub_words = (int32_t)std::min<uint32_t>(polar_host::SOLO_SUB_WORDS_MAX, p->G / 2);
+        ts.sub_inline = t.sub_inline;
         polar_sc_plan *a = nullptr;
         if (polar_sc_plan_create_tuned(&a, N, info_mask, &c, &ts) == 0) p->alt = a;
     }
@@ -1102,11 +1106,10 @@ int polar_sc_plan_prepare(const polar_sc_plan *p, size_t max_batch)
 {
     if (!p) return -EINVAL;
     DevState *st = nullptr;
-    if (p->alt) {   // the solo alternate takes the batches up to its threshold
-        const size_t cap = (size_t)polar_host::SOLO_FRAMES_PER_SIMD * (size_t)current_simds();
-        if (int rc = ensure_device(p->alt, std::min(max_batch ? max_batch : 1, cap), &st)) return rc;
-        if (max_batch && max_batch <= cap) return 0;
-    }
+    // automatic layout: only the plan that decodes max_batch frames (layout_for) gets its
+    // schedule and scratch here; the other one is set up by the first decode that uses it
+    // (a caller of large batches must not pay the solo scratch, ~0.6 GB at C5)
+    if (p->alt) p = layout_for(p, max_batch ? max_batch : 1, current_simds());
     return ensure_device(p, max_batch ? max_batch : 1, &st);
 }
 
@@ -1324,6 +1327,10 @@ int polar_sc_plan_launch_info(const polar_sc_plan *p, size_t batch, uint32_t cus
     polar_sc_launch_info r{};
     r.kernel = p->stats.kernel;
     const int simds = 4 * (int)(cus ? cus : 256u);
+    if (p->alt) {   // automatic layout: which batches the solo alternate takes on this device
+        r.alt_layout = p->alt->solo ? 2u : 1u;
+        r.alt_max_batch = (uint64_t)polar_host::SOLO_FRAMES_PER_SIMD * (uint64_t)simds;
+    }
     p = layout_for(p, batch, simds);   // (automatic layout: the plan that decodes this batch)
     r.layout = p->pair ? (p->solo ? 2u : 1u) : 0u;
     r.sub_words = (uint32_t)p->sub_words;

@@ -25,6 +25,7 @@
 #include <sys/wait.h>
 extern char **environ;   // (POSIX: the environment handed to the spawned compiler)
 #include <utime.h>
+#include <zlib.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -744,30 +745,61 @@ uint64_t code_key(const polar_sc_plan &p)
 }
 
 namespace {
+// cache entries: <key>.coz = "PSCZ" + the object's size (u64, little endian) + the object
+// deflated by zlib (code objects compress ~2.1x: the prewarmed set that travels with the library
+// to every GPU box is ~70 MB instead of ~150); a plain <key>.co (older caches) still loads
 std::string cache_path(const std::string &src, bool rtc = true)
 {
     const std::string dir = cache_dir();
     if (dir.empty()) return "";
     char name[40];
-    std::snprintf(name, sizeof name, "/%016llx.co", (unsigned long long)source_key(src, rtc));
+    std::snprintf(name, sizeof name, "/%016llx.coz", (unsigned long long)source_key(src, rtc));
     return dir + name;
+}
+
+bool read_all(const std::string &path, std::vector<char> &buf)
+{
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    buf.assign((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    return true;
 }
 
 bool cache_load(const std::string &path, std::vector<char> &code)
 {
     if (path.empty()) return false;
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return false;
-    std::vector<char> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    std::vector<char> buf;
+    std::string used = path;
+    if (read_all(path, buf) && buf.size() > 12 && std::memcmp(buf.data(), "PSCZ", 4) == 0) {
+        uint64_t n = 0;
+        std::memcpy(&n, buf.data() + 4, 8);
+        if (n < 4 || n > (1ull << 32)) return false;
+        std::vector<char> out(n);
+        uLongf len = (uLongf)n;
+        if (uncompress((Bytef *)out.data(), &len, (const Bytef *)buf.data() + 12, (uLong)(buf.size() - 12)) != Z_OK ||
+            len != n)
+            return false;
+        buf.swap(out);
+    } else {
+        used = path.substr(0, path.size() - 1);   // <key>.co: an uncompressed entry
+        if (!read_all(used, buf)) return false;
+    }
     if (buf.size() < 4 || std::memcmp(buf.data(), "\x7f" "ELF", 4) != 0) return false;
     code.swap(buf);
-    (void)utime(path.c_str(), nullptr);   // mark as in use (stale entries can be pruned by age)
+    (void)utime(used.c_str(), nullptr);   // mark as in use (stale entries can be pruned by age)
     return true;
 }
 
-void cache_store(const std::string &path, const std::vector<char> &code)
+void cache_store(const std::string &path, const std::vector<char> &obj)
 {
     if (path.empty()) return;
+    uLongf clen = compressBound((uLong)obj.size());
+    std::vector<char> code(12 + clen);
+    if (compress2((Bytef *)code.data() + 12, &clen, (const Bytef *)obj.data(), (uLong)obj.size(), 6) != Z_OK) return;
+    code.resize(12 + clen);
+    const uint64_t n = obj.size();
+    std::memcpy(code.data(), "PSCZ", 4);
+    std::memcpy(code.data() + 4, &n, 8);
     const size_t slash = path.rfind('/');
     (void)mkdir(path.substr(0, slash).c_str(), 0755);
     // unique per process and call: prewarm compiles from several threads, and two of them may
@@ -891,15 +923,29 @@ int offline_compile(const std::string &src, std::vector<char> &code, std::string
         posix_spawn_file_actions_init(&fa);
         posix_spawn_file_actions_addopen(&fa, 1, lg.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
         posix_spawn_file_actions_adddup2(&fa, 1, 2);
+        // the driver in a process group of its own, so that a timeout kills the tools it spawned
+        // (lld, the offload bundler, a non-integrated cc1) with it
+        posix_spawnattr_t sa;
+        posix_spawnattr_init(&sa);
+        posix_spawnattr_setflags(&sa, POSIX_SPAWN_SETPGROUP);
+        posix_spawnattr_setpgroup(&sa, 0);
+        // the driver's own temporaries (offload objects, bundles) go to the scratch directory too,
+        // so that a killed compile leaves nothing behind
+        const std::string tmpenv = "TMPDIR=" + dir;
+        std::vector<const char *> envp;
+        for (char **e = environ; *e; ++e)
+            if (std::strncmp(*e, "TMPDIR=", 7) != 0) envp.push_back(*e);
+        envp.push_back(tmpenv.c_str());
+        envp.push_back(nullptr);
         pid_t pid;
-        if (posix_spawn(&pid, clang.c_str(), &fa, nullptr, (char *const *)argv.data(), environ) == 0) {
+        if (posix_spawn(&pid, clang.c_str(), &fa, &sa, (char *const *)argv.data(), (char *const *)envp.data()) == 0) {
             int status = 0;
             pid_t w = 0;
             // bounded wait: a hung compiler must not hang the decode (it is killed, and the
             // caller falls back to hipRTC)
             for (long waited_ms = 0; (w = waitpid(pid, &status, WNOHANG)) == 0; waited_ms += 20) {
                 if (waited_ms >= 1000l * clang_timeout_s()) {
-                    kill(pid, SIGKILL);
+                    kill(-pid, SIGKILL);   // the whole group (pgid == the driver's pid)
                     w = waitpid(pid, &status, 0);
                     log += "clang driver killed after " + std::to_string(clang_timeout_s()) + " s\n";
                     status = -1;
@@ -917,11 +963,16 @@ int offline_compile(const std::string &src, std::vector<char> &code, std::string
             }
         }
         posix_spawn_file_actions_destroy(&fa);
+        posix_spawnattr_destroy(&sa);
         std::ifstream lf(lg);
         log.assign((std::istreambuf_iterator<char>(lf)), std::istreambuf_iterator<char>());
     }
-    for (const char *f : {"/k.hip", "/k.co", "/log", "/polar_sc_device.h", "/polar_sc_pair.h", "/polar_sc_interp.h"})
-        std::remove((dir + f).c_str());
+    if (DIR *d = opendir(dir.c_str())) {   // every file the compile left (a flat directory)
+        while (dirent *e = readdir(d))
+            if (std::strcmp(e->d_name, ".") != 0 && std::strcmp(e->d_name, "..") != 0)
+                std::remove((dir + "/" + e->d_name).c_str());
+        closedir(d);
+    }
     rmdir(dir.c_str());
     return rc;
 }
@@ -938,9 +989,13 @@ int rtc_compile(const std::string &src, std::vector<char> &code, std::string &lo
         std::string key = src + "\n// offline clang driver: " + clang_identity() + "\n";
         for (const std::string &w : extra) key += "// " + w + "\n";
         const std::string opath = cache_path(key, false);
-        if (cache_load(opath, code) || offline_compile(src, code, log, extra) == 0) {
+        if (cache_load(opath, code)) {
             if (compiler) *compiler = POLAR_SC_COMPILER_CLANG;
-            if (!opath.empty()) cache_store(opath, code);
+            return 0;
+        }
+        if (offline_compile(src, code, log, extra) == 0) {   // (a hit is not stored again: ADVICE r05)
+            if (compiler) *compiler = POLAR_SC_COMPILER_CLANG;
+            cache_store(opath, code);
             return 0;
         }
         if (!extra.empty()) {

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol(pkg):
     missing = [f for f in decl if not hasattr(lib, f)]
     assert not missing, missing
     assert set(decl) == set(pkg.EXPORTS)
-    assert lib.polar_sc_abi_version() == 4
+    assert lib.polar_sc_abi_version() == 5
 
 
 def test_no_oracle_in_product():

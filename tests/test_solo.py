@@ -33,17 +33,30 @@ def test_solo_plan_stats(pkg):
     m = util.mask("frozen_n_65536_k_32768")
     d = solo(pkg, m)
     s = d.stats
-    assert (s["kernel"], s["sub_words"], s["storage"]) == (3, 256, 1)
+    # default subtree size of a solo plan: min(512, N / 32) words, forced or automatic
+    assert (s["kernel"], s["sub_words"], s["storage"]) == (3, 512, 1)
     # per frame: (G - S) / 8 slot rows of 128 B + G / 128 bit rows of 256 B (solo plans keep the
     # subtree roots in a slot level of their own; sub_root 2 reads them as F / G of the parents)
-    assert s["scratch_bytes_per_wave"] == (4096 - 256) // 8 * 128 + 4096 // 128 * 256
-    assert s["lds_bytes_per_wave"] == 256 // 8 * 128
+    assert s["scratch_bytes_per_wave"] == (4096 - 512) // 8 * 128 + 4096 // 128 * 256
+    assert s["lds_bytes_per_wave"] == 512 // 8 * 128
     s2 = solo(pkg, m, sub_root=2).stats
-    assert s2["scratch_bytes_per_wave"] == (4096 - 512) // 8 * 128 + 4096 // 128 * 256
+    assert s2["scratch_bytes_per_wave"] == (4096 - 1024) // 8 * 128 + 4096 // 128 * 256
+    s3 = solo(pkg, m, sub_words=256).stats
+    assert s3["scratch_bytes_per_wave"] == (4096 - 256) // 8 * 128 + 4096 // 128 * 256
     assert "#define POLAR_SOLO 1" in d.kernel_source()
     assert "POLAR_SOLO" not in pkg.Decoder(m).kernel_source()
-    info = d.launch_info(64)
+    info = d.launch_info(64, cus=256)
     assert info["blocks"] == 64 and info["waves_per_block"] == 8, info   # one block per frame
+    assert info["alt_layout"] == 0 and info["alt_max_batch"] == 0   # a forced layout has no alternate
+    # the automatic layout: the solo alternate takes batches of <= 2 frames per SIMD, with the
+    # solo defaults whatever the pair plan's tuning
+    for tun in (None, {"sub_words": 64, "waves_per_group": 2}):
+        a = pkg.Decoder(m, tuning=tun)
+        for cus, b in ((256, 2048), (64, 512)):
+            i1, i2 = a.launch_info(b, cus=cus), a.launch_info(b + 1, cus=cus)
+            assert (i1["alt_layout"], i1["alt_max_batch"]) == (2, b), (tun, i1)
+            assert (i1["layout"], i1["sub_words"], i2["layout"]) == (2, 512, 1), (tun, i1, i2)
+    assert pkg.Decoder(m, tuning={"layout": 1}).launch_info(64, cus=256)["alt_layout"] == 0
     assert solo(pkg, m, sub_words=512).stats["sub_words"] == 512
     with pytest.raises(pkg.PolarError):
         solo(pkg, util.mask("frozen_n_4096_k_2048"), sub_words=32)    # < 64: 8-row slot groups

@@ -19,8 +19,29 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 
 
+def read_code(path):
+    """the ELF code object of a cache entry: <key>.coz ("PSCZ", u64 size, zlib stream,
+    polar_sc_jit.cpp cache_store) or a plain object file"""
+    import struct
+    import zlib
+    data = open(path, "rb").read()
+    if data[:4] == b"PSCZ":
+        n, = struct.unpack_from("<Q", data, 4)
+        data = zlib.decompress(data[12:])
+        assert len(data) == n, path
+    return data
+
+
+def cache_entries(d):
+    return glob.glob(os.path.join(d, "*.coz")) + glob.glob(os.path.join(d, "*.co"))
+
+
 def kernels(path):
-    notes = subprocess.run([READELF, "--notes", path], capture_output=True, text=True).stdout
+    import tempfile
+    with tempfile.NamedTemporaryFile(suffix=".co") as f:
+        f.write(read_code(path))
+        f.flush()
+        notes = subprocess.run([READELF, "--notes", f.name], capture_output=True, text=True).stdout
     out = []
     for blk in re.split(r"\n\s+- \.agpr_count:", notes)[1:]:
         agpr = int(blk.split()[0])
@@ -36,7 +57,7 @@ def code_key(path):
     """polar_sc_jit.cpp code_key restated: FNV-1a (64-bit) over the PROGBITS sections that are
     executable or named .rodata, in section order, as 16 hex digits."""
     import struct
-    data = open(path, "rb").read()
+    data = read_code(path)
     shoff, = struct.unpack_from("<Q", data, 0x28)
     shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
     secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
@@ -52,7 +73,7 @@ def code_key(path):
 
 def find_code(cache, key):
     """The code object in `cache` whose machine code has this code_key."""
-    for co in sorted(glob.glob(os.path.join(cache, "*.co")), key=os.path.getmtime, reverse=True):
+    for co in sorted(cache_entries(cache), key=os.path.getmtime, reverse=True):
         if code_key(co) == key:
             return co
     return None
@@ -72,7 +93,7 @@ def over_budget(vgpr, agpr, wg):
 def main():
     d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "sc_polar_decoder_hls_amd", "lib", "rtc_cache")
     bad = 0
-    for co in sorted(glob.glob(os.path.join(d, "*.co"))):
+    for co in sorted(cache_entries(d)):
         for name, vgpr, agpr, wg in kernels(co):
             over, total = over_budget(vgpr, agpr, wg)
             if over or agpr:

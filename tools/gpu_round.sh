@@ -43,7 +43,7 @@ for step in "$@"; do
     timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/bench_steps20.json" 2> "$OUT/bench_steps20.err"
     echo "bench steps20 ok" ;;
   prof)
-    for c in "c2 FB_N1024_K512 65536 10" "c3 frozen_n_65536_k_32768 4096 4" "c5 frozen_n_262144_k_131072 512 3" \
+    for c in "c2 FB_N1024_K512 65536 10" "c4share FB_N1024_K512 131072 10" "c3 frozen_n_65536_k_32768 4096 4" "c5 frozen_n_262144_k_131072 512 3" \
              "c5b64 frozen_n_262144_k_131072 64 3" "par16 frozen_n_16384_k_8192 4096 5" \
              "par64 frozen_n_16384_k_8192 4096 5 par=64" "q8 frozen_n_16384_k_14746 4096 5 llr_bits=8" \
              "q9 frozen_n_16384_k_8192 4096 5 llr_bits=9"; do
