@@ -109,7 +109,7 @@ typedef struct polar_sc_tuning {
                                  wave in the 16-bit halves, four words per register), 2 = solo
                                  (one frame per wave, the halves carry words 8 j + 4 h + r:
                                  eight words per register, half the instructions per frame on
-                                 nodes of >= 16 words; PAR 16 only) */
+                                 nodes of >= 16 words; PAR 16 SIGMAG only, LLR_BITS <= 9) */
     int32_t sub_root;         /* pair plans: where a generated subtree decoder reads its root.
                                  0 = automatic (2 in the frame-pair layout when the frame
                                  has at least 16 subtrees, 1 otherwise),

@@ -33,6 +33,15 @@ def hipcc():
     return "hipcc"
 
 
+def strip_comments(src):
+    """the device header as embedded for run-time compiles: without its // comments and blank
+    lines, so that editing a comment does not change the code-object cache keys (polar_sc_jit.cpp
+    source_key hashes the embedded text); the headers hold no string literal with '//'"""
+    import re
+    lines = (re.sub(r"\s*//.*$", "", line).rstrip() for line in src.split("\n"))
+    return "\n".join(line for line in lines if line) + "\n"
+
+
 def needs_build():
     if not os.path.exists(LIB):
         return True
@@ -63,7 +72,7 @@ def build(force=False, verbose=False):
                             (INTERP_H, "polar_sc_interp_src.inc", "kPolarInterpSrc"),
                             (PAIR_H, "polar_sc_pair_src.inc", "kPolarPairSrc")):
         with open(path) as f:
-            src = f.read()
+            src = strip_comments(f.read())
         assert ")POLARSRC\"" not in src
         with open(os.path.join(GEN_DIR, inc), "w") as f:
             f.write("static const char " + name + "[] = R\"POLARSRC(" + src + ")POLARSRC\";\n")
@@ -132,8 +141,11 @@ def _run_pool(items, procs, verbose):
     # compile in-process)
     from concurrent.futures import ProcessPoolExecutor, as_completed
     from concurrent.futures.process import BrokenProcessPool
+    # (python -c has no __main__ file and spawns fine; python - / a REPL names one that is
+    # not a file, which spawned children would try to import)
     main = sys.modules.get("__main__")
-    if not os.path.isfile(getattr(main, "__file__", "") or ""):
+    mfile = getattr(main, "__file__", None)
+    if mfile is not None and not os.path.isfile(mfile):
         for r in map(_compile_item, items):
             _report(r, verbose)
         return

@@ -162,6 +162,60 @@ def cpu_test_plans():
          ("frozen_n_65536_k_32768", mask("frozen_n_65536_k_32768"), {"sub_words": 64, "waves_per_group": 2})]
 
 
+# ---- CA2 on the pair kernel (tests/test_ca2.py) -------------------------------------------------
+def ca2_first_mask(N):
+    """the rate-1/2 reference mask of N with information bits in its first 16-LLR word, so that
+    leaf 0 is decoded and meets MIN (-2^(Q-1)) on the leftmost path"""
+    m = mask("frozen_n_%d_k_%d" % (N, N // 2)).copy()
+    m[:16] = np.random.default_rng(N).integers(0, 2, 16)
+    m[[3, 5, 11, 15]] = 1
+    return m
+
+
+def ca2_gpu_items():
+    """(id, mask, CA2 config fields, tuning) of the CA2 pair-kernel GPU tests"""
+    out = []
+    for n in ("frozen_n_2048_k_1024", "frozen_n_16384_k_8192", "frozen_n_65536_k_32768"):
+        out.append((n, mask(n), {}, None))
+    for N in (2048, 16384):
+        out.append(("first%d" % N, ca2_first_mask(N), {}, None))
+    for i, m in enumerate(struct_masks(8192)):
+        out += [("struct8192_%d_s%d" % (i, sw), m, {}, {"kernel": 3, "layout": 1, "sub_words": sw}) for sw in (32, 256)]
+    fm = ca2_first_mask(16384)
+    for par in (16, 32, 64):
+        for q in (5, 6, 7, 8, 9):
+            if q == 9 and par == 64:
+                continue
+            for ext in (1, 0):
+                out.append(("first16384_p%d_q%d_e%d" % (par, q, ext), fm, {"par": par, "llr_bits": q, "extended": ext}, None))
+    out.append(("first16384_pl0", fm, {"pruning_level": 0}, None))
+    out.append(("first2048_p64_pl0", ca2_first_mask(2048), {"par": 64, "pruning_level": 0}, None))
+    for wpg in (1, 2, 4, 8):
+        out.append(("wave_mask_w%d" % wpg, wave_mask(), {}, {"kernel": 3, "layout": 1, "waves_per_group": wpg, "sub_words": 64}))
+    out.append(("first16384_fused", fm, {}, {"kernel": 3, "layout": 1, "sub_root": 2}))
+    out.append(("tier32768", mask("frozen_n_32768_k_29492"), {}, {"kernel": 3, "layout": 1, "tier_words": 512,
+                                                                   "sub_words": 128}))
+    return out
+
+
+# ---- LLR_BITS 9 (tests/test_gpu_formats.py test_llr9_pair_kernel, tests/test_solo.py q9 tests):
+# automatic plans, which hold the solo alternate for small batches ----------------------------
+Q9_MASKS = ("frozen_n_2048_k_1024", "frozen_n_16384_k_8192", "frozen_n_65536_k_32768", "frozen_n_262144_k_131072")
+
+
+def q9_items():
+    out = []
+    for ext in (1, 0):
+        out += [(n, mask(n), {"llr_bits": 9, "extended": ext}, None) for n in Q9_MASKS]
+        out.append(("struct8192_1", struct_masks(8192)[1], {"llr_bits": 9, "extended": ext}, None))
+    return out
+
+
+def ca2_items():
+    """ca2_gpu_items as prewarm items (CA2 config fields)"""
+    return [(n, m, dict(f, sigmag=0), t) for n, m, f, t in ca2_gpu_items()]
+
+
 # ---- datapath formats (tests/test_gpu_formats.py): (PAR, SIGMAG, EXTENDED, LLR_BITS) ---------
 FORMATS = [
     (16, 0, 1, 6), (16, 0, 1, 8), (16, 0, 0, 6), (16, 1, 0, 6), (16, 1, 1, 9), (16, 0, 1, 9),
@@ -268,3 +322,5 @@ def prewarm_all(verbose=False):
     # generated kernels (one code object per mask and configuration); the interpreter formats
     # share one per format
     _build.prewarm_items(sweep_items(), verbose=verbose)
+    _build.prewarm_items(ca2_items(), verbose=verbose)
+    _build.prewarm_items(q9_items(), verbose=verbose)

@@ -59,6 +59,10 @@ constexpr u32 GSAT = CA2 ? (1u << (QB - 1)) - 1u : (1u << (QB - 2)) - 1u;
 // qfull_adder_sat_sm<Q+L+1> -> 2^(Q+L-1)-1 (511 at Q 6, PAR 16); CA2 qadd<Q+L+1> -> 2^(Q+L)-1
 constexpr u32 REPSAT = CA2 ? (1u << (QB + LPAR)) - 1u : (1u << (QB + LPAR - 1)) - 1u;
 constexpr u32 GSAT2 = GSAT * 0x00010001u;
+// magnitude field of a stage value in the split / slot forms of the generated kernels: SIGMAG
+// magnitudes stay <= QMAG; CA2 keeps |MIN| = 2^(Q-1), the absorbing value of F_function_C2's
+// qabs wrap (functions.h:48-61, scalar.h:42-49), as magnitude 2^(Q-1) with the sign set
+constexpr u32 VMAG = CA2 ? (1u << QB) - 1u : QMAG;
 
 // ---------------------------------------------------------------------------------------
 // packed 16-bit helpers (v_pk_* on gfx950)
@@ -71,6 +75,7 @@ __device__ __forceinline__ u32 pk_max_u16(u32 a, u32 b) { return U(__builtin_ele
 // a * b + c per 16-bit half, modulo 2^16 (v_pk_mad_u16)
 __device__ __forceinline__ u32 pk_mad_u16(u32 a, u32 b, u32 c) { return U(V(a) * V(b) + V(c)); }
 __device__ __forceinline__ u32 pk_sub(u32 a, u32 b) { return U(V(a) - V(b)); }
+__device__ __forceinline__ u32 pk_mul_lo(u32 a, u32 b) { return U(V(a) * V(b)); }
 __device__ __forceinline__ u32 pk_sra(u32 a, short s)
 {
     i16x2 x = __builtin_bit_cast(i16x2, a);
@@ -529,6 +534,128 @@ template <int I>
 __device__ __forceinline__ u32 F_split_sm(u32 ma, u32 mb, u32 FS)
 {
     return pk_min(ma, mb) | (plane_mask<I>(FS) & SGN);
+}
+
+// ---------------------------------------------------------------------------------------
+// CA2 (config.h:11) on the split / SM16 forms of the generated pair kernels (POLAR_CA2). The
+// two's complement values are kept as magnitude + sign, with two conventions
+// (functions.h:48-118; F_function_C2, G_function_C2, G_simplified_C2):
+//   * a zero magnitude is the value 0 whatever its sign bit: F_function_C2 / G_function_C2
+//     never make a -0, the ops below read such a sign as don't-care, and hard decisions mask
+//     it (ca2_nzs);
+//   * MIN of width w, -2^(w-1) -- the pattern qabs leaves negative (scalar.h:42-49) -- is
+//     magnitude 2^(w-1) with the sign set. F_function_C2 returns it whenever an operand is MIN
+//     (the signed min takes the negative qabs, and its negation wraps to itself). Only the
+//     leftmost path can hold MIN (the channel, then F of F ...: G_function_C2 saturates to
+//     +-(2^(Q-1) - 1)) and the first PAR word, where G_extended_C2 of two MINs is the MIN one
+//     bit wider; the generators give those F ops the key min below (MIN -> key 0).
+// G_function_C2 / G_extended_C2 are the SIGMAG split code with the CA2 clamp (GSAT): b + a'
+// has magnitude |mb +- ma|, and the SM sign rule gives its sign whenever it is not 0.
+// ---------------------------------------------------------------------------------------
+// sign masks S (0xFFFF per negative half) of the values (M, S) with the zeros made positive
+__device__ __forceinline__ u32 ca2_nzs(u32 M, u32 S) { return pk_mul_lo(pk_min(M, 0x00010001u), S); }
+// bit 15 / 31 set where the magnitude is not 0 (hard decision mask of an SM16 pair)
+__device__ __forceinline__ u32 ca2_nz(u32 m) { return pk_sub(0u, m & MAG); }
+// F_function_C2 magnitude at width MW: min over m ^ 2^(MW-1) (MIN -> 0, m < 2^(MW-1) -> m + 2^(MW-1))
+template <int MW>
+__device__ __forceinline__ u32 pk_min_key(u32 a, u32 b)
+{
+    constexpr u32 K2 = (1u << (MW - 1)) * 0x00010001u;
+    return pk_min(a ^ K2, b ^ K2) ^ K2;
+}
+// bit 15 / 31 set where an F_function_C2 magnitude of width MW is MIN (magnitudes <= 2^(MW-1))
+template <int MW>
+__device__ __forceinline__ u32 ca2_minbit(u32 m) { return pk_add(m, (0x8000u - (1u << (MW - 1))) * 0x00010001u); }
+// F_function_C2 on SM16 pairs of width MW (the result's sign: MIN, else the xor; 0 don't-care)
+template <int MW>
+__device__ __forceinline__ u32 F_ca2(u32 a, u32 b)
+{
+    const u32 m = pk_min_key<MW>(a & MAG, b & MAG);
+    return m | (((a ^ b) | ca2_minbit<MW>(m)) & SGN);
+}
+// F_root / F on split words / the REP value with MIN absorbing (the leftmost path)
+template <int I, int MW>
+__device__ __forceinline__ u32 F_root_min(u32 a, u32 b, u32 &S)
+{
+    const u32 m = pk_min_key<MW>(a & MAG, b & MAG);
+    S = plane_put<I>(S, (a ^ b) | ca2_minbit<MW>(m));
+    return m;
+}
+template <int I, int MW>
+__device__ __forceinline__ u32 F_split_min(u32 ma, u32 mb, u32 &MP)
+{
+    const u32 m = pk_min_key<MW>(ma, mb);
+    MP = plane_put<I>(MP, ca2_minbit<MW>(m));
+    return m;
+}
+template <int I, int MW>
+__device__ __forceinline__ u32 F_split_biased_min(u32 ma, u32 mb, u32 FS)
+{
+    const u32 m = pk_min_key<MW>(ma, mb), s = plane_mask<I>(FS) | pk_sra(ca2_minbit<MW>(m), 15);
+    return pk_add(pk_sub(m ^ s, s), 0x02000200u);
+}
+// channel pair (16-bit halves, low Q bits two's complement) -> SM16: qconv_format (SIGMAG,
+// conv_pair) or, CA2, the value itself as magnitude + sign (Adapt_format leaves it, library.h:18-28)
+__device__ __forceinline__ u32 chan_sm16(u32 raw)
+{
+    if constexpr (CA2) {
+        constexpr u32 QM = (1u << QB) - 1u, QP = 1u << QB;
+        const u32 t = raw & (QM * 0x00010001u), s = (t << (16 - QB)) & SGN;
+        return s | bsel(pk_sra(s, 15), pk_sub(QP * 0x00010001u, t), t);
+    } else {
+        return conv_pair(raw);
+    }
+}
+
+// Leaf Spec_P16_ext / Spec_P16 in CA2 (functions.h:366-546 with F_function_C2, G_extended_C2
+// or G_function_C2, F_simplified_C2 / G_simplified_C2, :89-118) on split words with the
+// conventions above (the recursion of functions.h:413-492). MW != 0: the leaf can hold
+// MIN of width MW (the first PAR word), its F ops take the key min and its exact G children
+// MIN one bit wider. Unlike SIGMAG an all-information block of 4+ LLRs is not its hard
+// decisions (a zero F value decides 0, not the sign xor), so only 2-LLR blocks take them.
+template <u32 FB, int B, int W, int MW>
+__device__ __forceinline__ u32 leaf_ca2(u32 M, u32 S, const Lanes &ln)
+{
+    constexpr u32 bm = ((1u << W) - 1u) << B;
+    constexpr u32 sub = FB & bm;
+    if constexpr (sub == 0u) {
+        return 0u;
+    } else if constexpr (W == 2) {
+        if constexpr (sub == bm) {
+            return ca2_nzs(M, S);                                  // x = (sign a, sign b)
+        } else if constexpr ((sub >> B) == 1u) {
+            const u32 T = ca2_nzs(M, S);                           // (1, 0): x = [sa ^ sb, 0]
+            return (T ^ xorlane<1>(T)) & ln.a1;
+        } else {
+            const u32 v = pk_sub(M ^ S, S);                        // (0, 1): x = [u1, u1], u1 = a + b < 0
+            return pk_sra(pk_add(v, xorlane<1>(v)), 15);
+        }
+    } else {
+        constexpr int H = W / 2;
+        const u32 PM = xorlane<H>(M), PS = xorlane<H>(S);
+        const u32 SX = S ^ PS;
+        u32 Mf, SF;
+        if constexpr (MW != 0) {
+            Mf = pk_min_key<MW>(M, PM);
+            SF = SX | pk_sra(ca2_minbit<MW>(Mf), 15);
+        } else {
+            Mf = pk_min(M, PM);
+            SF = SX;
+        }
+        const u32 xa = leaf_ca2<FB, B, H, MW>(Mf, SF, ln);
+        const u32 x = opaque(SX ^ xorlane<H>(xa));                 // sign(a') ^ sign(b)
+        const u32 lt = opaque(pk_sra(pk_sub(PM, M), 15));
+        u32 Mb = pk_mad_u16(MW != 0 ? pk_min(M, PM) : Mf, x | 0x00010001u, pk_max_u16(M, PM));
+        if constexpr (!EXT) Mb = pk_min(Mb, GSAT2);
+        const u32 xb = leaf_ca2<FB, B + H, H, (MW != 0 && EXT) ? MW + 1 : 0>(Mb, S ^ (x & ~lt), ln);
+        return bselo(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
+    }
+}
+template <u32 FB, int MW>
+__device__ __forceinline__ u32 leaf_gen_ca2(u32 M, u32 S, const Lanes &ln)
+{
+    static_assert(((FB >> 16) & 7u) == 0u, "CA2 pair plans: plain leaves only");
+    return leaf_ca2<FB & 0xFFFFu, 0, 16, MW>(M, S, ln);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -864,7 +864,16 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // the host expands its leaf into F / G / 16-LLR leaf records, par_expand: G_extended when
     // EXTENDED, the saturating G and POLAR_EXT 0 leaves when not)
     // and 9-bit LLRs (16-bit stage slots, the int16 channel: polar_sc_pair.h SLOT16)
-    const bool pair_fmt = dflt || ((c.par == 16 || c.par == 32 || c.par == 64) && c.sigmag == 1 && c.llr_bits <= 9);
+    // and CA2 (polar_sc_pair.h POLAR_CA2: the split code on magnitude + sign, MIN absorbing on
+    // the leftmost path) with plain leaves (PRUNING_LEVEL 0 / 2; the PRUNING_LEVEL 1 decoders of
+    // CA2 stay on the interpreter), except 9-bit LLRs at PAR 64, whose 16-bit REP accumulator
+    // (2^15 - 1) leaves no headroom in a 16-bit half
+    bool leaf_kinds = false;
+    for (const polar_sc_op &o : p->ops)
+        if ((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && ((o.fb >> 16) & 7u) != 0u) leaf_kinds = true;
+    const bool pair_par = c.par == 16 || c.par == 32 || c.par == 64;
+    const bool pair_fmt = dflt || (pair_par && c.sigmag == 1 && c.llr_bits <= 9) ||
+                          (pair_par && c.sigmag == 0 && !leaf_kinds && c.llr_bits <= 9 && !(c.llr_bits == 9 && c.par == 64));
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR
     // level's F / G / H then run inside the straight-line code instead of as interpreter ops
@@ -889,9 +898,10 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
         delete p;
         return rc;
     }
-    // solo layout (one frame per wave, 8 words per register): PAR 16 only; a forced solo
-    // layout the plan cannot take is an error
-    const bool solo_ok = c.par == 16 && c.llr_bits <= 8;
+    // solo layout (one frame per wave, 8 words per register): PAR 16 SIGMAG (8-bit slot rows,
+    // or 16-bit ones for 9-bit LLRs; the half ops of 8-word nodes have no CA2 form); a forced
+    // solo layout the plan cannot take is an error
+    const bool solo_ok = c.par == 16 && c.sigmag == 1 && c.llr_bits <= 9;
     if ((t.layout != 0 && !want_pair) || (t.layout == 2 && !solo_ok)) {
         delete p;
         return -ENOTSUP;
@@ -1063,7 +1073,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // words, automatic waves, LDS levels and subtree roots), not the pair plan's tuning, which
     // was chosen for the other layout; only the way subtree decoders are built
     // (sub_inline) carries over. polar_sc_tuning.layout = 1 builds no alternate.
-    if (p->pair && !p->solo && t.layout == 0 && c.par == 16 && c.llr_bits <= 8) {
+    if (p->pair && !p->solo && t.layout == 0 && c.par == 16 && c.sigmag == 1 && c.llr_bits <= 9) {
         polar_sc_tuning ts{};
         ts.layout = 2;
         ts.kernel = 3;

@@ -37,6 +37,12 @@
 // Only REP and SPC combine the halves (word order / tie order across h), and the channel rows
 // (real words 8 j + 4 h + r: 128-byte row stride, half h at + 64) and the output differ.
 // Nodes of 8 words and below are handled in the generated subtree code (polar_sc_pairgen.cpp).
+//
+// CA2 plans (POLAR_CA2, config.h:11): the same layout and code on magnitude + sign with the
+// conventions of polar_sc_device.h (a zero's sign is don't-care; MIN = magnitude 2^(Q-1) with
+// the sign set): slot values keep Q magnitude bits, the upper F takes the key min (MIN
+// absorbing, F4 / F_pair), hard decisions mask zeros, REP needs no exact-SM fallback (a zero
+// total decides 0). 8-bit LLRs keep 16-bit slot rows (|MIN| = 128 does not fit an SM8 byte).
 #pragma once
 
 #include "polar_sc_device.h"
@@ -231,13 +237,13 @@ constexpr int PAIR_MAX_WAVES = 8;   // launch bound 512 threads: <= 256 VGPRs pe
 // row (odd ? 2 i + 1 : 2 i) of a slot dword as the SM16 pair of the register code
 __device__ __forceinline__ u32 prow8(u32 d, bool odd)
 {
-    return __builtin_amdgcn_perm(d, d, odd ? 0x03030101u : 0x02020000u) & ((0x8000u | QMAG) * 0x00010001u);
+    return __builtin_amdgcn_perm(d, d, odd ? 0x03030101u : 0x02020000u) & ((0x8000u | VMAG) * 0x00010001u);
 }
 // two SM16 pairs (rows 2 i, 2 i + 1) -> slot dword
 __device__ __forceinline__ u32 ppack8(u32 v0, u32 v1)
 {
-    const u32 t0 = (v0 & (QMAG * 0x00010001u)) | ((v0 >> 8) & 0x00800080u);   // SM8 in bytes 0, 2
-    const u32 t1 = (v1 & (QMAG * 0x00010001u)) | ((v1 >> 8) & 0x00800080u);
+    const u32 t0 = (v0 & (VMAG * 0x00010001u)) | ((v0 >> 8) & 0x00800080u);   // SM8 in bytes 0, 2
+    const u32 t1 = (v1 & (VMAG * 0x00010001u)) | ((v1 >> 8) & 0x00800080u);
     return __builtin_amdgcn_perm(t1, t0, 0x06020400u);
 }
 // the partial sums of local words q .. q + 15 as one dword (bit i = word q + i of the low
@@ -266,8 +272,8 @@ __device__ __forceinline__ u32 ubits4(u32 dword, int q)
 }
 
 // SWAR on four SM8 bytes (sign bit 7, magnitude bits 0..6): exact while two magnitudes sum
-// below 128
-constexpr bool PAIR_SWAR = 2u * QMAG < 128u;
+// below 128 (CA2: |MIN| = 2^(Q-1) included, LLR_BITS <= 6)
+constexpr bool PAIR_SWAR = 2u * (CA2 ? QMAG + 1u : QMAG) < 128u;
 constexpr u32 B_SGN = 0x80808080u, B_MAG = 0x7F7F7F7Fu, B_ONE = 0x01010101u;
 // 0x7F in the bytes whose bit 7 is set, 0 elsewhere
 __device__ __forceinline__ u32 bmask7(u32 t)
@@ -276,12 +282,20 @@ __device__ __forceinline__ u32 bmask7(u32 t)
     return g - (g >> 7);
 }
 __device__ __forceinline__ u32 bsel7(u32 m, u32 a, u32 b) { return (m & a) | (~m & b); }   // v_bfi
-// F_sm on four bytes: min of the magnitudes, xor of the signs
+// F_sm on four bytes: min of the magnitudes, xor of the signs. CA2: F_function_C2 -- the min
+// of the keys m ^ 2^(Q-1) (MIN -> key 0 wins), the sign set for MIN
 __device__ __forceinline__ u32 F4(u32 a, u32 b)
 {
-    const u32 ma = a & B_MAG, mb = b & B_MAG;
-    const u32 ge = bmask7((ma | B_SGN) - mb);   // |a| >= |b|
-    return ((a ^ b) & B_SGN) | bsel7(ge, mb, ma);
+    if constexpr (CA2) {
+        constexpr u32 KB = (1u << (QB - 1)) * B_ONE;
+        const u32 ka = (a & B_MAG) ^ KB, kb = (b & B_MAG) ^ KB;    // keys <= 2^Q - 1 < 128
+        const u32 k = bsel7(bmask7((ka | B_SGN) - kb), kb, ka);   // min key
+        return (((a ^ b) | ~(k + 0x7F7F7F7Fu)) & B_SGN) | (k ^ KB);   // bit 7 of k + 127: k != 0
+    } else {
+        const u32 ma = a & B_MAG, mb = b & B_MAG;
+        const u32 ge = bmask7((ma | B_SGN) - mb);   // |a| >= |b|
+        return ((a ^ b) & B_SGN) | bsel7(ge, mb, ma);
+    }
 }
 // G_sm<GSAT> on four bytes; u: flip flags at the sign bits
 __device__ __forceinline__ u32 G4(u32 a, u32 b, u32 u)
@@ -294,13 +308,31 @@ __device__ __forceinline__ u32 G4(u32 a, u32 b, u32 u)
     m = bsel7(bmask7((m | B_SGN) - SATV), SATV, m);             // min(m, GSAT)
     return ((b ^ (x & t1)) & B_SGN) | m;                        // |a| < |b| ? sign(b) : sign(a')
 }
-// channel bytes (two's complement, low Q bits) -> SM8: conv_pair on four bytes
+// channel bytes (two's complement, low Q bits) -> SM8: conv_pair on four bytes; CA2: the
+// value as magnitude + sign (MIN -> magnitude 2^(Q-1))
 __device__ __forceinline__ u32 conv4(u32 raw)
 {
     constexpr u32 QM = (1u << QB) - 1u, QP = 1u << QB;
     const u32 t = raw & (QM * B_ONE), v = QP * B_ONE - t;       // QP - t in [1, QP] per byte
-    const u32 mn = bsel7(bmask7((t | B_SGN) - v), v, t);        // min(t, QP - t)
-    return ((t + (127u - QP / 2u) * B_ONE) & B_SGN) | (mn & (QMAG * B_ONE));   // sign: t > QP / 2
+    if constexpr (CA2) {
+        const u32 sg = (t << (8 - QB)) & B_SGN;                   // bit Q-1 -> bit 7
+        return sg | bsel7(bmask7(sg), v, t);
+    } else {
+        const u32 mn = bsel7(bmask7((t | B_SGN) - v), v, t);        // min(t, QP - t)
+        return ((t + (127u - QP / 2u) * B_ONE) & B_SGN) | (mn & (QMAG * B_ONE));   // sign: t > QP / 2
+    }
+}
+// F of two SM16 pairs of the stage width: F_sm, or F_function_C2 with MIN absorbing
+__device__ __forceinline__ u32 F_pair(u32 a, u32 b)
+{
+    if constexpr (CA2) return F_ca2<QB>(a, b);
+    else return F_sm(a, b);
+}
+// hard decisions (bits 15 / 31) of an SM16 pair: the signs; CA2: of the nonzero values
+__device__ __forceinline__ u32 hard_pair(u32 v)
+{
+    if constexpr (CA2) return v & ca2_nz(v) & SGN;
+    else return v & SGN;
 }
 // F / G of a slot dword pair (either arithmetic)
 template <bool ISG>
@@ -313,7 +345,7 @@ __device__ __forceinline__ u32 fg4_8(u32 a, u32 b, u32 u)
         return ppack8(G_sm<GSAT>(prow8(a, false), prow8(b, false), (u << 8) & SGN),
                       G_sm<GSAT>(prow8(a, true), prow8(b, true), u & SGN));
     } else {
-        return ppack8(F_sm(prow8(a, false), prow8(b, false)), F_sm(prow8(a, true), prow8(b, true)));
+        return ppack8(F_pair(prow8(a, false), prow8(b, false)), F_pair(prow8(a, true), prow8(b, true)));
     }
 }
 
@@ -325,12 +357,21 @@ __device__ __forceinline__ u32 fg4_8(u32 a, u32 b, u32 u)
 // row pair as su_t and an 8-row group as sg_t; u flags of a row pair keep the SM8 positions
 // (bits 7 / 23 row 2 i, 15 / 31 row 2 i + 1, ubits4).
 // ---------------------------------------------------------------------------------------
-constexpr bool PAIR_S16 = SLOT16;
+#if POLAR_Q > 8 || (POLAR_CA2 && POLAR_Q > 7)
+#define POLAR_PAIR_S16 1
+#else
+#define POLAR_PAIR_S16 0
+#endif
+constexpr bool PAIR_S16 = POLAR_PAIR_S16 != 0;   // (9-bit LLRs; CA2 8-bit LLRs: |MIN| = 128)
 constexpr int GD = PAIR_S16 ? 8 : 4;   // dwords per lane of an 8-row group
 #if POLAR_Q > 8
+typedef short chan_el;                 // int16 channel (polar_sc_decode_i16)
+#else
+typedef unsigned char chan_el;
+#endif
+#if POLAR_PAIR_S16
 typedef u32x2 su_t;
 typedef u32x8 sg_t;
-typedef short chan_el;                 // int16 channel (polar_sc_decode_i16)
 __device__ __forceinline__ u32 prow(su_t d, bool odd) { return odd ? d.y : d.x; }
 __device__ __forceinline__ su_t ppack(u32 v0, u32 v1) { return su_t{v0, v1}; }
 __device__ __forceinline__ su_t sget(const sg_t &g, int t) { return su_t{g[2 * t], g[2 * t + 1]}; }
@@ -343,12 +384,11 @@ template <bool ISG>
 __device__ __forceinline__ su_t fg4(su_t a, su_t b, u32 u)
 {
     if constexpr (ISG) return su_t{G_sm<GSAT>(a.x, b.x, (u << 8) & SGN), G_sm<GSAT>(a.y, b.y, u & SGN)};
-    else return su_t{F_sm(a.x, b.x), F_sm(a.y, b.y)};
+    else return su_t{F_pair(a.x, b.x), F_pair(a.y, b.y)};
 }
 #else
 typedef u32 su_t;
 typedef u32x4 sg_t;
-typedef unsigned char chan_el;
 __device__ __forceinline__ u32 prow(su_t d, bool odd) { return prow8(d, odd); }
 __device__ __forceinline__ su_t ppack(u32 v0, u32 v1) { return ppack8(v0, v1); }
 __device__ __forceinline__ su_t sget(const sg_t &g, int t) { return g[t]; }
@@ -422,13 +462,13 @@ struct PairCtx {
 #if POLAR_Q > 8
         const u32 r0 = (u32)(unsigned short)chl[ROWB * j] | ((u32)(unsigned short)chh[ROWB * j] << 16);
         const u32 r1 = (u32)(unsigned short)chl[ROWB * j + ROWB] | ((u32)(unsigned short)chh[ROWB * j + ROWB] << 16);
-        return ppack(conv_pair(r0), conv_pair(r1));
+        return ppack(chan_sm16(r0), chan_sm16(r1));
 #else
         const u32 lo = (u32)chl[ROWB * j] | ((u32)chl[ROWB * j + ROWB] << 8);
         const u32 hi = (u32)chh[ROWB * j] | ((u32)chh[ROWB * j + ROWB] << 8);
         const u32 raw = lo | (hi << 16);
         if constexpr (PAIR_SWAR) return conv4(raw);
-        else return ppack(conv_pair(raw & 0x00FF00FFu), conv_pair((raw >> 8) & 0x00FF00FFu));
+        else return ppack(chan_sm16(raw & 0x00FF00FFu), chan_sm16((raw >> 8) & 0x00FF00FFu));
 #endif
     }
     // channel rows j .. j + 7 (j a multiple of 8) as an 8-row group, element loads (chan2)
@@ -488,7 +528,7 @@ __device__ __forceinline__ u32 quad_transpose(u32 x, const ChanQ &q) { return qu
 __device__ __forceinline__ u32 chan_conv(u32 raw)
 {
     if constexpr (PAIR_SWAR) return conv4(raw);
-    else return ppack8(conv_pair(raw & 0x00FF00FFu), conv_pair((raw >> 8) & 0x00FF00FFu));
+    else return ppack8(chan_sm16(raw & 0x00FF00FFu), chan_sm16((raw >> 8) & 0x00FF00FFu));
 }
 // channel rows j .. j + 7 (j a multiple of 8) as four slot dwords, aligned frames
 __device__ __forceinline__ u32x4 chan8a(const ChanQ &q, int j)
@@ -504,8 +544,8 @@ __device__ __forceinline__ u32x4 chan8a(const ChanQ &q, int j)
 }
 __device__ __forceinline__ sg_t chan8(const PairCtx &c, const ChanQ &q, int j)
 {
-#if POLAR_Q > 8
-    (void)q;   // int16 channel: element loads
+#if POLAR_PAIR_S16
+    (void)q;   // int16 channel / 16-bit slots: element loads
     return c.chan8b(j);
 #else
     if (!q.al) return c.chan8b(j);
@@ -806,13 +846,15 @@ __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int 
         psrc2<ROOT, SL>(c, s0, n4, j, a, b);
 #pragma unroll
         for (int o = 0; o < 2; o++) {
-            const u32 lam = F_sm(prow(a, o), prow(b, o)), sg = pk_sra(lam, 15);
+            const u32 lam = F_pair(prow(a, o), prow(b, o)), sg = pk_sra(lam, 15);
             const X4 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
             if constexpr (PAIR_SOLO) acc = rep_acc_solo(acc, t.t0, t.t1, t.t2, t.t3);
             else acc = rep_acc_rows(acc, t.t0, t.t1, t.t2, t.t3);
         }
     }
-    if (PAIR_SOLO ? rep_any_zero_lo(acc) : rep_any_zero(acc)) {
+    // (CA2: the exact sums of ADD_TREE_{n}_CA2 / VECTOR_ADD are this chain, and a zero total
+    // decides 0: no fallback)
+    if (!CA2 && (PAIR_SOLO ? rep_any_zero_lo(acc) : rep_any_zero(acc))) {
         const Lanes ln = c.lanes();
         acc = 0;
         for (int j = 0; j < n4; j += 2) {
@@ -857,7 +899,7 @@ __device__ __forceinline__ void pr1spc_body(const PairCtx &c, int s0, int n4, in
             if (j == j0 || ((ub + j) & 15) == 0) ud = c.bld((ub + j) >> 4);
             u = ubit_p(ud, ub + j);
         }
-        const u32 lam = G_sm<GSAT>(a, b, u), h = lam & SGN;
+        const u32 lam = G_sm<GSAT>(a, b, u), h = hard_pair(lam);
         const int q = (l0 + j) & 15;
         acc |= h >> (15 - q);
         if (q == 15 || j + 1 == j1) {

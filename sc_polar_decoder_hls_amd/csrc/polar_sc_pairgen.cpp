@@ -19,6 +19,7 @@
 #include <stdexcept>
 #include <sstream>
 #include <string>
+#include <tuple>
 #include <vector>
 
 namespace polar_host {
@@ -37,9 +38,25 @@ struct PairGen {
     std::map<int, std::string> small1;     // result masks of 1-word nodes, by word position
     std::map<int, std::string> small2;     // result masks of 2-word nodes (row r: word r & 1)
     int nvar = 0;
+    // CA2 plans (POLAR_CA2; polar_sc_device.h): hard decisions mask zeros, REP has no exact-SM
+    // fallback, and in the decoder of the leftmost subtree (`left`, the _L variant) the F-type
+    // ops that can meet MIN take the key min: those of the first PAR word (pos < p16 words),
+    // which include the leftmost path
+    bool ca2 = false, left = false;
+    int q = 6, p16 = 1;
 
     PairGen(const std::vector<polar_sc_op> &ops_, int lg, bool solo_ = false)
         : ops(ops_), LG(lg), solo(solo_), wpr(solo_ ? 8 : 4) {}
+
+    // MIN width of an F-type op's operands (0: they cannot hold MIN); fb bits 20..23 = operand
+    // width above LLR_BITS (PAR > 16 leaf expansion), GLEAF: + 1 behind an exact G
+    int min_width(const polar_sc_op &op, bool gleaf = false) const
+    {
+        if (!ca2 || !left || op.pos >= p16) return 0;
+        return q + (int)((op.fb >> 20) & 15u) + (gleaf && (op.fb & FB_EXACT) ? 1 : 0);
+    }
+    // hard decision masks of a G result (sign plane / masks h, magnitude l) in CA2: zeros decide 0
+    std::string hard_plane(const std::string &h, const std::string &nzp) const { return ca2 ? "(" + h + ") & " + nzp : h; }
 
     // registers of a node of 2^sd words
     int regs(int sd) const { return solo ? (sd >= 3 ? 1 << (sd - 3) : 1) : (sd >= 2 ? 1 << (sd - 2) : 1); }
@@ -127,10 +144,12 @@ struct PairGen {
         const bool root = pd == LG;   // the subtree root: SM16 words re-read from its stage slot
         if (root && (op.code == POLAR_OP_REP || op.code == POLAR_OP_R1 || op.code == POLAR_OP_SPC)) root_split(2 * n4);
         if (root && op.code == POLAR_OP_F) {
+            const int mw = min_width(op);
             o << "  { // F n " << op.n << " (root)\n    u32 P_[" << np << "] = {};\n";
             for (int i = 0; i < n4; i++) {
-                o << "    " << M(cd, i) << " = F_root<" << i % 16 << ">(CH(" << i << "), CH(" << n4 + i << "), P_[" << i / 16
-                  << "]);\n";
+                o << "    " << M(cd, i) << " = " << (mw ? "F_root_min<" : "F_root<") << i % 16
+                  << (mw ? ", " + std::to_string(mw) : std::string()) << ">(CH(" << i << "), CH(" << n4 + i << "), P_["
+                  << i / 16 << "]);\n";
                 chunk_fence(i, n4);
             }
             for (int k = 0; k < np; k++) o << "    s" << cd << "[" << k << "] = P_[" << k << "];\n";
@@ -150,17 +169,25 @@ struct PairGen {
             return;
         }
         switch (op.code) {
-        case POLAR_OP_F:
+        case POLAR_OP_F: {
+            const int mw = min_width(op);
             o << "  { // F n " << op.n << "\n";
+            if (mw) o << "    u32 MP_[" << np << "] = {};\n";
             for (int i = 0; i < n4; i++) {
-                o << "    " << M(cd, i) << " = pk_min(" << M(pd, i) << ", " << M(pd, n4 + i) << ");\n";
+                if (mw)
+                    o << "    " << M(cd, i) << " = F_split_min<" << i % 16 << ", " << mw << ">(" << M(pd, i) << ", "
+                      << M(pd, n4 + i) << ", MP_[" << i / 16 << "]);\n";
+                else
+                    o << "    " << M(cd, i) << " = pk_min(" << M(pd, i) << ", " << M(pd, n4 + i) << ");\n";
                 chunk_fence(i, n4);
             }
             for (int k = 0; k < np; k++)
-                o << "    s" << cd << "[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << ";\n";
+                o << "    s" << cd << "[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k)
+                  << (mw ? " | MP_[" + std::to_string(k) + "]" : std::string()) << ";\n";
             o << "  }\n";
             clobber_parent(pd, n4);
             break;
+        }
         case POLAR_OP_G:
             o << "  { // G n " << op.n << " upos " << op.upos << "\n    u32 X_[" << np << "], LT_[" << np << "] = {};\n";
             for (int k = 0; k < np; k++)
@@ -182,17 +209,22 @@ struct PairGen {
             for (int k = 0; k < np; k++)
                 o << "    FS_[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << ";\n";
             // (solo: the words of a register in order 8 i + r, then 8 i + 4 + r, into the low half)
+            const int mw = min_width(op);
             for (int i = 0; i < n4; i++) {
-                o << "    { const X4 t_ = rows4(row_sum_biased(F_split_biased<" << i % 16 << ">(" << M(pd, i) << ", "
-                  << M(pd, n4 + i) << ", FS_[" << i / 16 << "])));\n"
+                o << "    { const X4 t_ = rows4(row_sum_biased(" << (mw ? "F_split_biased_min<" : "F_split_biased<") << i % 16
+                  << (mw ? ", " + std::to_string(mw) : std::string()) << ">(" << M(pd, i) << ", " << M(pd, n4 + i)
+                  << ", FS_[" << i / 16 << "])));\n"
                   << "      acc_ = " << (solo ? "rep_acc_solo" : "rep_acc_rows") << "(acc_, t_.t0, t_.t1, t_.t2, t_.t3); }\n";
                 chunk_fence(i, n4);
             }
-            o << "    if (" << (solo ? "rep_any_zero_lo" : "rep_any_zero") << "(acc_)) {\n      acc_ = 0u;\n";
-            for (int i = 0; i < n4; i++)
-                o << "      acc_ = " << (solo ? "rep_sm_solo" : "rep_sm_rows") << "(acc_, F_split_sm<" << i % 16 << ">("
-                  << M(pd, i) << ", " << M(pd, n4 + i) << ", FS_[" << i / 16 << "]), ln);\n";
-            o << "    }\n    const u32 full_ = pk_sra(" << (solo ? "bcast_lo(acc_)" : "acc_") << ", 15);\n";
+            if (!ca2) {   // (CA2: the two's complement chain is exact and a zero total decides 0)
+                o << "    if (" << (solo ? "rep_any_zero_lo" : "rep_any_zero") << "(acc_)) {\n      acc_ = 0u;\n";
+                for (int i = 0; i < n4; i++)
+                    o << "      acc_ = " << (solo ? "rep_sm_solo" : "rep_sm_rows") << "(acc_, F_split_sm<" << i % 16 << ">("
+                      << M(pd, i) << ", " << M(pd, n4 + i) << ", FS_[" << i / 16 << "]), ln);\n";
+                o << "    }\n";
+            }
+            o << "    const u32 full_ = pk_sra(" << (solo ? "bcast_lo(acc_)" : "acc_") << ", 15);\n";
             for (int j = 0; j < n4; j += 16) put_mask(l0 + j, n4 < 16 ? n4 : 16, "full_");
             o << "  }\n";
             clobber_parent(pd, n4);
@@ -203,25 +235,37 @@ struct PairGen {
             const bool spc = op.code == POLAR_OP_SPC;
             o << "  { // " << (spc ? "SPC" : "R1") << " n " << op.n << " upos " << op.upos << "\n    u32 X_[" << np
               << "], LT_[" << np << "] = {};\n";
+            if (ca2) o << "    u32 NZ_[" << np << "] = {};\n";
             for (int k = 0; k < np; k++)
                 o << "    X_[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << " ^ " << U(ub, k) << ";\n";
             if (spc) o << "    u32 klo_ = 0xFFFFFFFFu, khi_ = 0xFFFFFFFFu, par_ = 0u;\n    const u32 rw_ = spc_sub(c.row, ln);\n";
             for (int i = 0; i < n4; i++) {
                 // key: (|lambda|, word, bitrev4(position)); solo: word 8 i + 4 h + r (bit 6 = h)
+                // (CA2: the nonzero plane of the G magnitudes)
+                const std::string nzput = ca2 ? "      NZ_[" + std::to_string(i / 16) + "] = plane_put<" +
+                                                    std::to_string(i % 16) + ">(NZ_[" + std::to_string(i / 16) +
+                                                    "], pk_sub(0u, l_));\n"
+                                              : std::string();
                 if (spc)
                     o << "    { const u32 l_ = G_split<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i) << ", X_["
-                      << i / 16 << "], LT_[" << i / 16 << "]);\n"
+                      << i / 16 << "], LT_[" << i / 16 << "]);\n" << nzput
                       << "      klo_ = __builtin_elementwise_min(klo_, (l_ << 24) | rw_ | " << (solo ? i << 7 : i << 6)
                       << "u);\n"
                       << "      khi_ = __builtin_elementwise_min(khi_, ((l_ >> 16) << 24) | rw_ | "
                       << (solo ? (i << 7) | 64 : i << 6) << "u); }\n";
+                else if (ca2)
+                    o << "    { const u32 l_ = G_split<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i) << ", X_["
+                      << i / 16 << "], LT_[" << i / 16 << "]);\n" << nzput << "    }\n";
                 else
                     o << "    LT_[" << i / 16 << "] = plane_put<" << i % 16 << ">(LT_[" << i / 16 << "], pk_sub(" << M(pd, i)
                       << ", " << M(pd, n4 + i) << "));\n";
                 chunk_fence(i, n4);
             }
             for (int k = 0; k < np; k++) {
-                o << "    { const u32 h_ = " << P(pd, n4 + 16 * k) << " ^ (X_[" << k << "] & ~LT_[" << k << "]);\n";
+                o << "    { const u32 h_ = "
+                  << hard_plane(P(pd, n4 + 16 * k) + " ^ (X_[" + std::to_string(k) + "] & ~LT_[" + std::to_string(k) + "])",
+                                "NZ_[" + std::to_string(k) + "]")
+                  << ";\n";
                 put(l0 + 16 * k, n4 < 16 ? n4 : 16, "h_");
                 if (spc) o << "      par_ ^= h_; }\n";
                 else o << "    }\n";
@@ -383,10 +427,17 @@ struct PairGen {
         const int n = op.n;
         const char *sw = swp(pd);
         switch (op.code) {
-        case POLAR_OP_F:
+        case POLAR_OP_F: {
+            const int mw = min_width(op);
             o << "  { // F n " << n << "\n    const X2 m_ = " << sw << "(" << M(pd, 0) << "), s_ = " << sw << "(s" << pd
-              << "[0]);\n    " << M(cd, 0) << " = pk_min(m_.a, m_.b); s" << cd << "[0] = s_.a ^ s_.b;\n  }\n";
+              << "[0]);\n    " << M(cd, 0);
+            if (mw)
+                o << " = pk_min_key<" << mw << ">(m_.a, m_.b); s" << cd << "[0] = (s_.a ^ s_.b) | plane_put<0>(0u, ca2_minbit<"
+                  << mw << ">(" << M(cd, 0) << "));\n  }\n";
+            else
+                o << " = pk_min(m_.a, m_.b); s" << cd << "[0] = s_.a ^ s_.b;\n  }\n";
             break;
+        }
         case POLAR_OP_G:
             // (G_extended inside a PAR 64 word, fb bit 19: no clamp)
             o << "  { // G n " << n << " upos " << op.upos << ((op.fb & FB_EXACT) ? " exact" : "") << "\n    const X2 m_ = "
@@ -400,7 +451,11 @@ struct PairGen {
             const std::string x = var("x");
             o << "  u32 " << x << ";\n  { // " << (f ? "F" : "G") << "+leaf pos " << op.pos << " fb 0x" << std::hex << op.fb
               << std::dec << "\n    const X2 m_ = swap16(" << M(pd, 0) << "), s_ = swap16(s" << pd << "[0]);\n";
-            if (f) {
+            const int mw = min_width(op, !f);
+            if (f && mw) {
+                o << "    const u32 M_ = pk_min_key<" << mw << ">(m_.a, m_.b), S_ = plane_mask<0>(s_.a ^ s_.b) | pk_sra(ca2_minbit<"
+                  << mw << ">(M_), 15);\n";
+            } else if (f) {
                 o << "    const u32 M_ = pk_min(m_.a, m_.b), S_ = plane_mask<0>(s_.a ^ s_.b);\n";
             } else {
                 o << "    const u32 xm_ = opaque(plane_mask<0>(s_.a ^ s_.b ^ " << small_u(1, op.upos) << "));\n"
@@ -409,22 +464,32 @@ struct PairGen {
                                          : "    const u32 M_ = pk_min(bsel(xm_, pk_abs_i16(d_), pk_add(m_.a, m_.b)), GSAT2);\n")
                   << "    const u32 S_ = plane_mask<0>(s_.b) ^ (xm_ & ~pk_sra(d_, 15));\n";
             }
-            o << "    " << x << " = leaf_gen<0x" << std::hex << (op.fb & 0x7FFFFu) << std::dec << "u>(M_, S_, ln);\n  }\n";
+            if (ca2)
+                o << "    " << x << " = leaf_gen_ca2<0x" << std::hex << (op.fb & 0xFFFFu) << std::dec << "u, " << mw
+                  << ">(M_, S_, ln);\n  }\n";
+            else
+                o << "    " << x << " = leaf_gen<0x" << std::hex << (op.fb & 0x7FFFFu) << std::dec << "u>(M_, S_, ln);\n  }\n";
             small1[op.pos] = x;
             break;
         }
         case POLAR_OP_REP: {
             const std::string x = var("x");
+            const int mw = min_width(op);
             o << "  u32 " << x << ";\n  { // REP n " << n << "\n    const X2 m_ = " << sw << "(" << M(pd, 0)
               << "), s_ = " << sw << "(s" << pd << "[0]);\n    const u32 FS_ = s_.a ^ s_.b;\n"
-              << "    const u32 t_ = row_sum_biased(F_split_biased<0>(m_.a, m_.b, FS_));\n";
+              << "    const u32 t_ = row_sum_biased("
+              << (mw ? "F_split_biased_min<0, " + std::to_string(mw) + ">" : std::string("F_split_biased<0>"))
+              << "(m_.a, m_.b, FS_));\n";
             // (2 words: two PAR 16 words in order, or one PAR 32 word -- rep2_acc / rep2_sm)
             if (n == 1) o << "    u32 acc_ = rep_acc(0u, t_);\n";
             else o << "    u32 acc_ = rep2_acc(t_);\n";
-            o << "    if (rep_any_zero(acc_)) {\n";
-            if (n == 1) o << "      acc_ = G_sm<REPSAT>(row_add_tree(F_split_sm<0>(m_.a, m_.b, FS_), ln), 0u, 0u);\n";
-            else o << "      acc_ = rep2_sm(F_split_sm<0>(m_.a, m_.b, FS_), ln);\n";
-            o << "    }\n    " << x << " = pk_sra(acc_, 15);\n  }\n";
+            if (!ca2) {
+                o << "    if (rep_any_zero(acc_)) {\n";
+                if (n == 1) o << "      acc_ = G_sm<REPSAT>(row_add_tree(F_split_sm<0>(m_.a, m_.b, FS_), ln), 0u, 0u);\n";
+                else o << "      acc_ = rep2_sm(F_split_sm<0>(m_.a, m_.b, FS_), ln);\n";
+                o << "    }\n";
+            }
+            o << "    " << x << " = pk_sra(acc_, 15);\n  }\n";
             (n == 1 ? small1 : small2)[op.pos] = x;
             break;
         }
@@ -435,12 +500,16 @@ struct PairGen {
             o << "  u32 " << x << ";\n  { // " << (spc ? "SPC" : "R1") << " n " << n << "\n    const X2 m_ = " << sw << "("
               << M(pd, 0) << "), s_ = " << sw << "(s" << pd << "[0]);\n    u32 LT_ = 0u; const u32 X_ = s_.a ^ s_.b ^ "
               << small_u(n, op.upos) << ";\n";
-            if (!spc) {
+            if (!spc && ca2) {
+                o << "    const u32 l_ = G_split<0>(m_.a, m_.b, X_, LT_);\n"
+                  << "    " << x << " = ca2_nzs(l_, plane_mask<0>(s_.b ^ (X_ & ~LT_)));\n  }\n";
+            } else if (!spc) {
                 o << "    LT_ = plane_put<0>(0u, pk_sub(m_.a, m_.b));\n"
                   << "    " << x << " = plane_mask<0>(s_.b ^ (X_ & ~LT_));\n  }\n";
             } else {
                 o << "    const u32 l_ = G_split<0>(m_.a, m_.b, X_, LT_);\n"
-                  << "    const u32 h_ = plane_mask<0>(s_.b ^ (X_ & ~LT_));\n"
+                  << "    const u32 h_ = " << (ca2 ? "ca2_nzs(l_, plane_mask<0>(s_.b ^ (X_ & ~LT_)))" : "plane_mask<0>(s_.b ^ (X_ & ~LT_))")
+                  << ";\n"
                   << "    u32 par_ = row_xor(h_);\n";
                 // key bits below the magnitude: bitrev4(position), and for 2 words the word
                 // (PAR 16: above it; PAR 32: below it, spc_sub2)
@@ -525,7 +594,7 @@ struct PairGen {
               << "ub_ + ((j) & ~1)) : 0u), ((j) & 1) != 0)\n";
         // (plain arguments: a PairCtx passed by reference would live on the private stack)
         o << "__device__ " << (inl ? "__forceinline__" : "__noinline__") << " void polar_psub_" << id
-          << (kind == 1 ? "_F" : kind == 2 ? "_G" : "") << "(const u32 *src_, g_u32 *hb_, int l0"
+          << (kind == 1 ? "_F" : kind == 2 ? "_G" : "") << (left ? "_L" : "") << "(const u32 *src_, g_u32 *hb_, int l0"
           << (kind == 2 ? ", int ub_" : "") << ")\n{\n"
           << "  const u32 lane_ = threadIdx.x & 63u;\n  Lanes ln; ln.init(lane_ & 15u);\n"
           << "  struct { u32 row; } c; c.row = lane_ >> 4;\n  u32 bw[" << nbw << "] = {};\n";
@@ -561,8 +630,10 @@ const char *const kPairCH = "#define SLOT(j) src_[((j) >> 3) * 256 + (((j) >> 1)
 
 // upper-level record -> call of a polar_sc_pair.h loop function
 // (wpr: words per slot row of one (virtual) frame -- 4 pair, 8 solo)
-void upper_call(std::ostringstream &o, const polar_sc_op &op, int wpr)
+// ca2: the SUB at word 0 calls the _L variant of its decoder (PairGen::left)
+void upper_call(std::ostringstream &o, const polar_sc_op &op, int wpr, bool ca2)
 {
+    const char *lv = ca2 && op.pos == 0 ? "_L" : "";
     const int n4 = op.n / wpr, l0 = op.pos / wpr, ub = op.upos >= 0 ? op.upos / wpr : -1;
     o << "    c.sync(); ";
     switch (op.code) {
@@ -575,9 +646,9 @@ void upper_call(std::ostringstream &o, const polar_sc_op &op, int wpr)
     case POLAR_OP_H0: o << "pop_h<true>(c, " << l0 << ", " << n4 << ");"; break;
     case POLAR_OP_SUB:
         if (op.reserved[1] == 0)
-            o << "if (c.lead()) polar_psub_" << op.fb << "(c.slot_ptr(c.lvl_row(" << op.level << ")), c.hb, " << l0 << ");";
+            o << "if (c.lead()) polar_psub_" << op.fb << lv << "(c.slot_ptr(c.lvl_row(" << op.level << ")), c.hb, " << l0 << ");";
         else   // the root as F / G of the parent's slot rows (pair_fused)
-            o << "if (c.lead()) polar_psub_" << op.fb << (op.reserved[1] == 1 ? "_F" : "_G") << "(c.slot_ptr(c.lvl_row("
+            o << "if (c.lead()) polar_psub_" << op.fb << (op.reserved[1] == 1 ? "_F" : "_G") << lv << "(c.slot_ptr(c.lvl_row("
               << op.level - 1 << ")), c.hb, " << l0 << (op.reserved[1] == 2 ? ", " + std::to_string(ub) : std::string())
               << ");";
         break;
@@ -630,7 +701,8 @@ void chain_call(std::ostringstream &o, const std::vector<polar_sc_op> &ops, size
 
 // one decode kernel: a block of W waves per frame pair; `seg` selects the schedule segment
 // (the cases between POLAR_OP_SEGEND records; 0 when the plan has no grid tier)
-void pair_kernel(std::ostringstream &o, const char *name, const std::vector<polar_sc_op> &ops, int cmax, bool solo)
+void pair_kernel(std::ostringstream &o, const char *name, const std::vector<polar_sc_op> &ops, int cmax, bool solo,
+                 bool ca2)
 {
     const int wpr = solo ? 8 : 4;
     o << "extern \"C\" __global__ void __launch_bounds__(" << 64 * PAIR_WAVES_MAX << ") " << name << "(\n"
@@ -657,7 +729,7 @@ void pair_kernel(std::ostringstream &o, const char *name, const std::vector<pola
             i += (size_t)d - 1;
             continue;
         }
-        upper_call(o, op, wpr);
+        upper_call(o, op, wpr, ca2);
     }
     o << "    c.sync();\n";
     if (solo)
@@ -678,9 +750,11 @@ std::string pair_source(const polar_sc_plan &p)
 {
     std::ostringstream o;
     const bool solo = p.solo != 0;
-    const bool s16 = p.cfg.llr_bits > 8;   // 16-bit slot rows (polar_sc_pair.h SLOT16)
+    const bool ca2 = p.cfg.sigmag == 0;
+    const bool s16 = p.wide_slots();   // 16-bit slot rows (polar_sc_pair.h POLAR_PAIR_S16)
     const int wpr = solo ? 8 : 4;
-    o << "#define POLAR_LANE_REMAP 1\n" << (solo ? "#define POLAR_SOLO 1\n" : "") << "#define POLAR_Q " << p.cfg.llr_bits
+    o << "#define POLAR_LANE_REMAP 1\n" << (solo ? "#define POLAR_SOLO 1\n" : "") << (ca2 ? "#define POLAR_CA2 1\n" : "")
+      << "#define POLAR_Q " << p.cfg.llr_bits
       << "\n#define POLAR_LPAR "
       << (p.cfg.par == 64 ? 6 : p.cfg.par == 32 ? 5 : 4)
       << "\n" << (p.cfg.extended ? "" : "#define POLAR_EXT 0\n")   // EXTENDED = 0: saturating leaves
@@ -693,20 +767,25 @@ std::string pair_source(const polar_sc_plan &p)
     while ((1 << lg) < p.sub_words) lg++;
     // the decoder variants the kernels call (SUB records: reserved[1] = root kind), and the
     // subtest kernel's (kind 1 of a fused plan: its root rows fed through F with +QMAG)
-    std::set<std::pair<int, int>> need;
+    // (CA2: the decoder of the subtree at word 0 also as its _L variant, PairGen::left)
+    std::set<std::tuple<int, int, bool>> need;
     for (const std::vector<polar_sc_op> *ops : {&p.pair_ops, &p.pair_tier.seg_ops})
         for (const polar_sc_op &op : *ops)
-            if (op.code == POLAR_OP_SUB) need.insert({(int)op.fb, op.reserved[1]});
-    for (size_t id = 0; id < p.subs.size(); id++) need.insert({(int)id, p.pair_fused ? 1 : 0});
+            if (op.code == POLAR_OP_SUB) need.insert({(int)op.fb, op.reserved[1], ca2 && op.pos == 0});
+    for (size_t id = 0; id < p.subs.size(); id++) need.insert({(int)id, p.pair_fused ? 1 : 0, false});
     for (const auto &v : need) {
-        PairGen g(p.subs[v.first], lg, solo);
-        g.sub_function(v.first, p.tune.sub_inline == 2, v.second);
+        PairGen g(p.subs[std::get<0>(v)], lg, solo);
+        g.ca2 = ca2;
+        g.left = std::get<2>(v);
+        g.q = p.cfg.llr_bits;
+        g.p16 = (int)p.p16;
+        g.sub_function(std::get<0>(v), p.tune.sub_inline == 2, std::get<1>(v));
         o << g.o.str();
     }
     o << "}  // namespace polar\nusing namespace polar;\n";
     // the decode kernel over the whole schedule, and (grid-tier plans) the segment kernel
     const int cmax = p.tune.chain_max ? p.tune.chain_max : PAIR_CHAIN_MAX;
-    pair_kernel(o, "polar_sc_pair_kernel", p.pair_ops, cmax, solo);
+    pair_kernel(o, "polar_sc_pair_kernel", p.pair_ops, cmax, solo, ca2);
     // test hook (polar_sc_debug_subtree): subtree decoder `id` on 64 lanes of root slot rows
     // in[64 j + lane] (u16 SM8 pairs, repacked into row-pair dwords in LDS), its partial-sum
     // dwords to out[64 d + lane]
@@ -742,7 +821,7 @@ std::string pair_source(const polar_sc_plan &p)
         o << "  case " << id << ": polar_psub_" << id << (p.pair_fused ? "_F" : "") << "(src, (g_u32 *)out + lane, 0); return;\n";
     o << "  default: return;\n  }\n}\n";
     if (!p.pair_tier.steps.empty()) {
-        pair_kernel(o, "polar_sc_pair_seg_kernel", p.pair_tier.seg_ops, cmax, solo);
+        pair_kernel(o, "polar_sc_pair_seg_kernel", p.pair_tier.seg_ops, cmax, solo, ca2);
         o << "extern \"C\" __global__ void __launch_bounds__(256) polar_sc_pair_tier_kernel(\n"
           << "    const signed char *__restrict__ llr, unsigned int *__restrict__ scratch, int N, int batch, int pair_dwords,\n"
           << "    int slot_rows, int code_g, int k, int n4, int ub, int cw)\n{\n"

@@ -164,8 +164,10 @@ struct polar_sc_plan {
     int pair_dwords = 0;             // HBM scratch per pair / frame: slot rows (128 B) + bit dwords (256 B)
     int wpr() const { return solo ? 8 : 4; }   // words of one (virtual) frame per slot row
     // bytes of a slot row (64 lanes): SM8 pairs, or SM16 pairs for 9-bit LLRs (polar_sc_pair.h SLOT16)
-    int slot_row_bytes() const { return cfg.llr_bits > 8 ? 256 : 128; }
-    bool slot16() const { return pair && cfg.llr_bits > 8; }
+    // 16-bit slot rows: 9-bit LLRs, and CA2 8-bit LLRs (|MIN| = 128 does not fit an SM8 byte)
+    bool wide_slots() const { return cfg.llr_bits > 8 || (cfg.sigmag == 0 && cfg.llr_bits > 7); }
+    int slot_row_bytes() const { return wide_slots() ? 256 : 128; }
+    bool slot16() const { return pair && cfg.llr_bits > 8; }   // (the kernel reads the int16 channel)
     mutable std::mutex mu;
     mutable std::map<int, polar_host::DevState> dev;
     mutable std::mutex host_mu;                             // polar_sc_decode_host staging

@@ -15,11 +15,30 @@ import numpy as np
 U32 = np.uint32
 LANE = np.arange(64, dtype=np.int64)
 SGN, MAG = 0x80008000, 0x7FFF7FFF
-QB = 6
-QMAG = (1 << (QB - 1)) - 1
-GSAT = (1 << (QB - 2)) - 1
-REPSAT = (1 << (QB + 4 - 1)) - 1
-GSAT2 = GSAT * 0x00010001
+# the datapath format of the emulated source (configure): LLR_BITS, CA2, EXTENDED (PAR 16)
+QB, CA2, EXT, WIDE = 6, False, True, False
+QMAG = GSAT = REPSAT = GSAT2 = VMAG = 0
+
+
+def configure(q=6, ca2=False, ext=True):
+    """polar_sc_device.h's format constants for LLR_BITS q, CA2 / SIGMAG, EXTENDED (PAR 16)"""
+    global QB, CA2, EXT, WIDE, QMAG, GSAT, REPSAT, GSAT2, VMAG
+    QB, CA2, EXT = q, bool(ca2), bool(ext)
+    WIDE = QB > 8 or (CA2 and QB > 7)   # 16-bit slot rows (polar_sc_pair.h POLAR_PAIR_S16)
+    QMAG = (1 << (QB - 1)) - 1
+    GSAT = (1 << (QB - 1)) - 1 if CA2 else (1 << (QB - 2)) - 1
+    REPSAT = (1 << (QB + 4)) - 1 if CA2 else (1 << (QB + 4 - 1)) - 1
+    GSAT2 = GSAT * 0x00010001
+    VMAG = (1 << QB) - 1 if CA2 else QMAG
+
+
+def configure_from(src):
+    """configure() from the #defines of a generated source"""
+    m = re.search(r"#define POLAR_Q (\d+)", src)
+    configure(int(m.group(1)) if m else 6, "#define POLAR_CA2 1" in src, "#define POLAR_EXT 0" not in src)
+
+
+configure()
 
 
 def V(x):
@@ -66,6 +85,10 @@ def pk_sub(a, b):
 
 def pk_mad_u16(a, b, c):
     return pk(lo(a) * lo(b) + lo(c), hi(a) * hi(b) + hi(c))
+
+
+def pk_mul_lo(a, b):
+    return pk(lo(a) * lo(b), hi(a) * hi(b))
 
 
 def pk_sra(a, s):
@@ -172,6 +195,66 @@ def G_split(I, ma, mb, X, LT):
     d = pk_sub(ma, mb)
     LT = plane_put(I, LT, d)
     return pk_min(bsel(xm, pk_abs_i16(d), pk_add(ma, mb)), GSAT2), LT
+
+
+# ---- CA2 on split words (polar_sc_device.h): a zero's sign is don't-care, MIN of width w is
+# magnitude 2^(w-1) with the sign set; F ops that can meet it take the key min
+def ca2_nzs(M, S):
+    return pk_mul_lo(pk_min(M, 0x00010001), S)
+
+
+def ca2_nz(m):
+    return pk_sub(0, V(m) & MAG)
+
+
+def pk_min_key(MW, a, b):
+    K2 = (1 << (MW - 1)) * 0x00010001
+    return V(pk_min(V(a) ^ K2, V(b) ^ K2)) ^ K2
+
+
+def ca2_minbit(MW, m):
+    return pk_add(m, (0x8000 - (1 << (MW - 1))) * 0x00010001)
+
+
+def F_ca2(MW, a, b):
+    a, b = V(a), V(b)
+    m = pk_min_key(MW, a & MAG, b & MAG)
+    return m | (((a ^ b) | ca2_minbit(MW, m)) & SGN)
+
+
+def F_root_min(I, MW, a, b, S):
+    a, b = V(a), V(b)
+    m = pk_min_key(MW, a & MAG, b & MAG)
+    return m, plane_put(I, S, (a ^ b) | ca2_minbit(MW, m))
+
+
+def F_split_min(I, MW, ma, mb, MP):
+    m = pk_min_key(MW, ma, mb)
+    return m, plane_put(I, MP, ca2_minbit(MW, m))
+
+
+def F_split_biased_min(I, MW, ma, mb, FS):
+    m = pk_min_key(MW, ma, mb)
+    s = V(plane_mask(I, FS)) | pk_sra(ca2_minbit(MW, m), 15)
+    return pk_add(pk_sub(m ^ s, s), 0x02000200)
+
+
+def chan_sm16(raw):
+    """channel pair -> SM16 (conv_pair, or CA2 magnitude + sign)"""
+    if not CA2:
+        return conv_pair(raw)
+    QM, QP = (1 << QB) - 1, 1 << QB
+    t = V(raw) & (QM * 0x00010001)
+    sg = (t << (16 - QB)) & SGN
+    return sg | bsel(pk_sra(sg, 15), pk_sub(QP * 0x00010001, t), t)
+
+
+def F_pair(a, b):
+    return F_ca2(QB, a, b) if CA2 else F_sm(a, b)
+
+
+def hard_pair(v):
+    return (V(v) & ca2_nz(v) & SGN) if CA2 else (V(v) & SGN)
 
 
 def G_split_x(I, ma, mb, X, LT):
@@ -350,8 +433,46 @@ def leaf_ms(FB, B, W, M, S, ln):
     x = SF ^ xorlane(H, xa)
     lt = pk_sra(pk_sub(PM, M), 15)
     Mb = pk_mad_u16(Mf, x | 0x00010001, pk_max_u16(M, PM))
+    if not EXT:
+        Mb = pk_min(Mb, GSAT2)
     xb = leaf_ms(FB, B + H, H, Mb, V(S) ^ (x & ~lt), ln)
     return bsel(ln.a[H], xa ^ xorlane(H, xb), xb)
+
+
+def leaf_ca2(FB, B, W, MW, M, S, ln):
+    """polar_sc_device.h leaf_ca2"""
+    bm = ((1 << W) - 1) << B
+    sub = FB & bm
+    if sub == 0:
+        return V(0)
+    if W == 2:
+        if sub == bm:
+            return ca2_nzs(M, S)
+        if (sub >> B) == 1:
+            T = ca2_nzs(M, S)
+            return (T ^ xorlane(1, T)) & ln.a[1]
+        v = pk_sub(V(M) ^ V(S), S)
+        return pk_sra(pk_add(v, xorlane(1, v)), 15)
+    H = W // 2
+    PM, PS = xorlane(H, M), xorlane(H, S)
+    SX = V(S) ^ PS
+    if MW:
+        Mf = pk_min_key(MW, M, PM)
+        SF = SX | pk_sra(ca2_minbit(MW, Mf), 15)
+    else:
+        Mf, SF = pk_min(M, PM), SX
+    xa = leaf_ca2(FB, B, H, MW, Mf, SF, ln)
+    x = SX ^ xorlane(H, xa)
+    lt = pk_sra(pk_sub(PM, M), 15)
+    Mb = pk_mad_u16(pk_min(M, PM) if MW else Mf, x | 0x00010001, pk_max_u16(M, PM))
+    if not EXT:
+        Mb = pk_min(Mb, GSAT2)
+    xb = leaf_ca2(FB, B + H, H, MW + 1 if (MW and EXT) else 0, Mb, V(S) ^ (x & ~lt), ln)
+    return bsel(ln.a[H], xa ^ xorlane(H, xb), xb)
+
+
+def leaf_gen_ca2(FB, MW, M, S, ln):
+    return leaf_ca2(FB & 0xFFFF, 0, 16, MW, M, S, ln)
 
 
 def leaf_gen(FB, M, S, ln):
@@ -365,16 +486,20 @@ def sm8_pair(l, h):
     l, h = V(l).astype(np.int64), V(h).astype(np.int64)
     b0, b1 = l & 0xFF, h & 0xFF
     r = b0 | (b0 << 8) | (b1 << 16) | (b1 << 24)
-    return (r & ((0x8000 | QMAG) * 0x00010001)).astype(U32)
+    return (r & ((0x8000 | VMAG) * 0x00010001)).astype(U32)
 
 
 def slot_unpack(h):
+    if WIDE:   # 16-bit slots hold the SM16 pair itself
+        return V(h)
     return sm8_pair(h, V(h) >> 8)
 
 
 def slot_pack(v):
+    if WIDE:
+        return V(v)
     v = V(v).astype(np.int64)
-    t = (v & (QMAG * 0x00010001)) | ((v >> 8) & 0x00800080)
+    t = (v & (VMAG * 0x00010001)) | ((v >> 8) & 0x00800080)
     return ((t & 0xFF) | (((t >> 16) & 0xFF) << 8)).astype(U32)
 
 
@@ -387,7 +512,7 @@ def conv_pair(raw):
 
 
 # ---- transpiler of a generated subtree decoder ------------------------------------------
-_REF_FNS = ("F_root", "G_root", "G_split", "G_split_x")
+_REF_FNS = ("F_root", "G_root", "G_split", "G_split_x", "F_root_min", "F_split_min")
 
 
 def _split_top(s, sep=","):
@@ -452,7 +577,7 @@ def _stmt(st):
 
 def _assign(lhs, op, rhs):
     rhs = rhs.strip()
-    m = re.match(r"^(%s)<(\d+)>\((.*)\)$" % "|".join(_REF_FNS), rhs, re.S)
+    m = re.match(r"^(%s)<([\d, ]+)>\((.*)\)$" % "|".join(_REF_FNS), rhs, re.S)
     if m:
         args = _split_top(m.group(3))
         ref = args[-1]
@@ -464,17 +589,19 @@ def _assign(lhs, op, rhs):
     return ["%s = V(%s %s (%s))" % (lhs, lhs, op[0], _expr(rhs))]
 
 
-def transpile_sub(src, sid):
+def transpile_sub(src, sid, left=False):
     """Python source of subtree decoder `sid` of a generated pair source: a function
-    sub_<sid>(CH, BST, BSTM, ln, c)."""
+    sub_<sid>(CH, BST, BSTM, ln, c). left: its _L variant (CA2, the subtree at word 0)."""
     # (fused plans have only the variants that read the root as F / G of the parent, _F / _G;
     # their bodies are the same code on CH(j), which the emulation supplies)
-    for name in ("void polar_psub_%d(" % sid, "void polar_psub_%d_F(" % sid, "void polar_psub_%d_G(" % sid):
+    sfx = "_L" if left else ""
+    for name in ("void polar_psub_%d%s(" % (sid, sfx), "void polar_psub_%d_F%s(" % (sid, sfx),
+                 "void polar_psub_%d_G%s(" % (sid, sfx)):
         if name in src:
             start = src.index(name)
             break
     else:
-        raise ValueError("pair_emu: no decoder %d in the source" % sid)
+        raise ValueError("pair_emu: no decoder %d%s in the source" % (sid, sfx))
     body_start = src.index("{", start) + 1
     depth, i = 1, body_start
     while depth:
@@ -526,12 +653,18 @@ class Sub:
     """Compiled Python subtree decoders of one generated pair source."""
 
     def __init__(self, src, nsubs):
+        configure_from(src)
         self.fns = {}
         g = dict(globals())
         for sid in range(nsubs):
             code = transpile_sub(src, sid)
             exec(compile(code, "<psub_%d>" % sid, "exec"), g)
             self.fns[sid] = g["sub_%d" % sid]
+        for m in re.finditer(r"void polar_psub_(\d+)(?:_[FG])?_L\(", src):   # CA2 leftmost variants
+            sid = int(m.group(1))
+            code = transpile_sub(src, sid, left=True).replace("def sub_%d(" % sid, "def sub_%d_L(" % sid)
+            exec(compile(code, "<psub_%d_L>" % sid, "exec"), g)
+            self.fns[(sid, "L")] = g["sub_%d_L" % sid]
 
 
 class Ctx:
@@ -550,7 +683,7 @@ def decode(dec, llr):
     src = dec.kernel_source()
     st = dec.stats
     S = st["sub_words"]
-    subs = Sub(src, st["n_sub_kinds"])
+    subs = Sub(src, st["n_sub_kinds"])   # (configures the format of the source)
     upper = _upper_ops(src)
     N = dec.N
     G = N // 16
@@ -578,12 +711,12 @@ def _upper_ops(src):
     k0 = src.index("polar_sc_pair_kernel(")
     body = src[k0:src.index("pair_out(", k0)]
     ops = []
-    for m in re.finditer(r"(pop_fg_split<(\w+)>|pop_rep|pop_r1spc<(\w+)>|pop_h<(\w+)>|polar_psub_(\d+)(?:_([FG]))?|"
+    for m in re.finditer(r"(pop_fg_split<(\w+)>|pop_rep|pop_r1spc<(\w+)>|pop_h<(\w+)>|polar_psub_(\d+)(?:_([FG]))?(_L)?|"
                          r"pop_chain<(\d+), (\w+), (\w+)>)\(([^;]*)\);", body):
-        args = [a.strip() for a in _split_top(m.group(10))]
+        args = [a.strip() for a in _split_top(m.group(11))]
         if m.group(1).startswith("pop_chain"):
             # a fused descent: record 0 (F, or G with partial sums at ub), then F / zero-u G
-            d, isg0 = int(m.group(7)), m.group(9) == "true"
+            d, isg0 = int(m.group(8)), m.group(10) == "true"
             k, n4, ub, gm = int(args[1]), int(args[2]), int(args[3]), int(args[4].rstrip("u"))
             ops.append(("G" if isg0 else "F", k, n4, ub))
             for i in range(1, d):
@@ -604,9 +737,9 @@ def _upper_ops(src):
                 isg = m.group(6) == "G"
                 nq = None   # (the decoder's root rows: half the parent's, filled in _decode_pair)
                 ops.append(("FG_ROOT", isg, lvl, int(args[3]) if isg else -1))
-                ops.append(("SUB", int(m.group(5)), lvl + 1, int(args[2])))
+                ops.append(("SUB", int(m.group(5)), lvl + 1, int(args[2]), bool(m.group(7))))
             else:
-                ops.append(("SUB", int(m.group(5)), lvl, int(args[2])))
+                ops.append(("SUB", int(m.group(5)), lvl, int(args[2]), bool(m.group(7))))
     return ops
 
 
@@ -622,9 +755,9 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
     def chan(j):
         if solo:   # row j: words 8 j + 4 h + r
             off = 16 * (8 * j + row) + pos
-            return conv_pair((c0[off] & 0xFF) | ((c0[off + 64] & 0xFF) << 16))
+            return chan_sm16((c0[off] & 0xFFFF) | ((c0[off + 64] & 0xFFFF) << 16))
         off = 16 * (4 * j + row) + pos
-        return conv_pair((c0[off] & 0xFF) | ((c1[off] & 0xFF) << 16))
+        return chan_sm16((c0[off] & 0xFFFF) | ((c1[off] & 0xFFFF) << 16))
 
     def src(k, j):
         return chan(j) if k == 0 else slot_unpack(slots[k][j])
@@ -654,7 +787,7 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
             for j in range(n4):
                 a, b = src(k, j), src(k, n4 + j)
                 if kind == "F":
-                    r = F_sm(a, b)
+                    r = F_pair(a, b)
                 else:
                     r = G_sm(GSAT, a, b, ubit(ub + j) if ub >= 0 else 0)
                 outk.append(slot_pack(r))
@@ -662,7 +795,7 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
         elif kind == "REP":
             _, k, n4, l0 = op
             acc = V(0)
-            lams = [F_sm(src(k, j), src(k, n4 + j)) for j in range(n4)]
+            lams = [F_pair(src(k, j), src(k, n4 + j)) for j in range(n4)]
             for lam in lams:
                 sg = pk_sra(lam, 15)
                 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200)))
@@ -670,7 +803,7 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
                     acc = rep_acc_solo(acc, t.t0, t.t1, t.t2, t.t3)
                 else:
                     acc = rep_acc(rep_acc(rep_acc(rep_acc(acc, t.t0), t.t1), t.t2), t.t3)
-            if (rep_any_zero_lo if solo else rep_any_zero)(acc):
+            if not CA2 and (rep_any_zero_lo if solo else rep_any_zero)(acc):
                 acc = V(0)
                 for lam in lams:
                     if solo:
@@ -690,7 +823,7 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
             khi = V(0xFFFFFFFF)
             for j in range(n4):
                 lam = G_sm(GSAT, src(k, j), src(k, n4 + j), ubit(ub + j) if ub >= 0 else 0)
-                h = lam & SGN
+                h = hard_pair(lam)
                 q = (l0 + j) & 15
                 acc = acc | (h >> (15 - q))
                 if q == 15 or j + 1 == n4:
@@ -752,7 +885,7 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
                 sh = (d >> n4) & mm
                 bits[l0 >> 4] = ((d & ~mm) | sh) if kind == "H0" else (d ^ sh)
         elif kind == "SUB":
-            _, sid, k, l0 = op
+            _, sid, k, l0, left = op
             rows = slots[k]
 
             def CH(j, rows=rows):
@@ -765,7 +898,7 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
                 mm = V(m) << (l0 & 15)
                 bits[l0 >> 4] = (bits[l0 >> 4] & ~mm) | ((V(v) << (l0 & 15)) & mm)
 
-            subs.fns[sid](CH, BST, BSTM, ln, c)
+            subs.fns[(sid, "L") if left else sid](CH, BST, BSTM, ln, c)
     return bits
 
 

@@ -56,15 +56,19 @@ def test_tuning_validation_and_no_environment(pkg, monkeypatch):
     with pytest.raises(pkg.PolarError) as e:
         pkg.Decoder(util.mask("frozen_n_16384_k_8192"), config=c64, tuning={"layout": 2})
     assert e.value.rc == -95
-    # 9-bit LLRs: the pair kernel with 16-bit stage slots (frame-pair layout only)
+    # 9-bit LLRs: the pair kernel with 16-bit stage slots (both layouts since round 6)
     c9 = pkg.default_config()
     c9.llr_bits = 9
     d9 = pkg.Decoder(util.mask("frozen_n_16384_k_8192"), config=c9)
     assert d9.stats["kernel"] == 3 and "#define POLAR_Q 9" in d9.kernel_source()
     assert d9.stats["scratch_bytes_per_wave"] == (1024 - 256) // 4 * 256 + 1024 // 64 * 256   # 256 B slot rows
     assert pkg.Decoder(util.mask("FB_N1024_K512"), config=c9).stats["kernel"] != 1   # (per-mask: LLR_BITS <= 8)
+    assert pkg.Decoder(util.mask("frozen_n_16384_k_8192"), config=c9, tuning={"layout": 2}).stats["kernel"] == 3
+    # CA2: no solo layout (the half ops of 8-word nodes have no CA2 form)
+    ca2 = pkg.default_config()
+    ca2.sigmag = 0
     with pytest.raises(pkg.PolarError) as e:
-        pkg.Decoder(util.mask("frozen_n_16384_k_8192"), config=c9, tuning={"layout": 2})
+        pkg.Decoder(util.mask("frozen_n_16384_k_8192"), config=ca2, tuning={"layout": 2})
     assert e.value.rc == -95
     with pytest.raises(KeyError):
         pkg.make_tuning({"wpg": 1})

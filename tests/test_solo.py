@@ -162,3 +162,84 @@ def test_solo_misaligned_channel(pkg, cuda, oracle_mod):
     out = solo(pkg, mask).decode(view)
     cuda.cuda.synchronize()
     _assert_same(pkg.unpack_bits(out.cpu().numpy(), mask.size), oracle_mod.decode_fsm(mask, llr), "solo misaligned")
+
+
+# ---- 9-bit LLRs (LLR_BITS 9, parser_comp.sh:12): 16-bit slot rows, the int16 channel ------------
+def q9_frames(mask, n_awgn, n_edge, seed):
+    rng = np.random.default_rng(seed)
+    awgn, _ = util.synth_frames(mask, n_awgn, ebn0_db=1.0, seed=seed)
+    awgn = np.clip(awgn.astype(np.int32) * 8, -255, 255)
+    edge = rng.integers(-256, 256, size=(n_edge, mask.size))
+    edge[:, rng.integers(0, mask.size, 64)] = -256
+    edge[:, rng.integers(0, mask.size, 64)] = 0
+    return np.concatenate([awgn, edge]).astype(np.int16)
+
+
+def q9cfg(pkg, ext=1):
+    c = pkg.default_config()
+    c.llr_bits, c.extended = 9, ext
+    return c
+
+
+def test_solo_q9_plans(pkg):
+    """9-bit plans take the solo layout (forced, and as the automatic alternate of small
+    batches); CA2 plans do not (the half ops of 8-word nodes have no CA2 form)."""
+    m = util.mask("frozen_n_16384_k_8192")
+    d = pkg.Decoder(m, config=q9cfg(pkg), tuning={"kernel": 3, "layout": 2})
+    assert "#define POLAR_SOLO 1" in d.kernel_source() and "#define POLAR_Q 9" in d.kernel_source()
+    a = pkg.Decoder(m, config=q9cfg(pkg))
+    i1, i2 = a.launch_info(64, cus=256), a.launch_info(4096, cus=256)
+    assert (i1["layout"], i1["alt_layout"], i2["layout"]) == (2, 2, 1), (i1, i2)
+    c = pkg.default_config()
+    c.sigmag = 0
+    with pytest.raises(pkg.PolarError):
+        pkg.Decoder(m, config=c, tuning={"kernel": 3, "layout": 2})
+    assert pkg.Decoder(m, config=c).launch_info(64, cus=256)["alt_layout"] == 0
+
+
+@pytest.mark.parametrize("N", [2048, 8192])
+def test_solo_q9_emulated(pkg, oracle_mod, N):
+    """CPU: the solo code at LLR_BITS 9 (16-bit slot rows) emulated equals the FSM."""
+    import pair_emu
+    for i, mask in enumerate([util.mask("frozen_n_%d_k_%d" % (N, N // 2))] + list(struct_masks(N))[:2]):
+        llr = q9_frames(mask, 1, 2, seed=N + i)
+        for ext in (1, 0):
+            ref = oracle_mod.decode_fsm(mask, llr, llr_bits=9, extended=ext)
+            dec = pkg.Decoder(mask, config=q9cfg(pkg, ext), tuning={"kernel": 3, "layout": 2, "sub_words": 64})
+            _assert_same(pair_emu.decode(dec, llr), ref, "emulated solo q9 N=%d mask %d ext %d" % (N, i, ext))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["frozen_n_2048_k_1024", "frozen_n_16384_k_8192", "frozen_n_65536_k_32768", "struct"])
+def test_solo_q9_parity(pkg, cuda, oracle_mod, name):
+    """LLR_BITS 9 in the solo layout: the automatic plan decodes these small batches solo; the
+    whole 9-bit range incl. -256, both EXTENDED switches, int16 and int8 entry points."""
+    mask = struct_masks(8192)[1] if name == "struct" else util.mask(name)
+    llr = q9_frames(mask, 4, 3, seed=mask.size + 90)
+    small = np.clip(llr, -128, 127).astype(np.int8)
+    for ext in (1, 0):
+        dec = pkg.Decoder(mask, config=q9cfg(pkg, ext))
+        assert dec.launch_info(llr.shape[0])["layout"] == 2
+        out = dec.decode(cuda.from_numpy(llr).cuda())
+        out8 = dec.decode(cuda.from_numpy(small).cuda())
+        cuda.cuda.synchronize()
+        _assert_same(pkg.unpack_bits(out.cpu().numpy(), mask.size),
+                     oracle_mod.decode_fsm(mask, llr, llr_bits=9, extended=ext), "solo q9 %s ext %d" % (name, ext))
+        _assert_same(pkg.unpack_bits(out8.cpu().numpy(), mask.size),
+                     oracle_mod.decode_fsm(mask, small, llr_bits=9, extended=ext), "solo q9 i8 %s ext %d" % (name, ext))
+
+
+@pytest.mark.gpu
+def test_solo_q9_c5_share(pkg, cuda, oracle_mod):
+    """The C5 8-GPU share shape (64 frames of N = 262144) at LLR_BITS 9: solo, sampled against the
+    FSM, the rest of the batch equal to the sampled frames' repeats."""
+    mask = util.mask("frozen_n_262144_k_131072")
+    base = q9_frames(mask, 1, 1, seed=262)
+    llr = np.concatenate([base] * 32)
+    dec = pkg.Decoder(mask, config=q9cfg(pkg))
+    assert dec.launch_info(64)["layout"] == 2
+    out = dec.decode(cuda.from_numpy(llr).cuda())
+    cuda.cuda.synchronize()
+    _assert_same(pkg.unpack_bits(out[:2].cpu().numpy(), mask.size), oracle_mod.decode_fsm(mask, base, llr_bits=9),
+                 "C5 share q9")
+    assert (out.view(32, 2, -1) == out[:2].unsqueeze(0)).all()

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--mask", default="frozen_n_16384_k_8192")
     ap.add_argument("--frames", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--formats", default="",
+                    help="only these formats: 'par,sigmag,extended,llr_bits;...' (the shipped one is always first)")
     args = ap.parse_args()
     import torch
     import sc_polar_decoder_hls_amd as pkg
@@ -39,7 +41,11 @@ def main():
     N, K = mask.size, int(mask.sum())
     llr8, _ = pkg.csim_frames(N, args.frames, pkg.csim_sigma(2.5, K / N), seed=0xF0)
     base_ms = None
-    for fmt in formats():
+    fmts = formats()
+    if args.formats:
+        keep = [tuple(int(x) for x in f.split(",")) for f in args.formats.split(";")]
+        fmts = [fmts[0]] + [dict(par=p, sigmag=sg, extended=e, llr_bits=q) for p, sg, e, q in keep]
+    for fmt in fmts:
         cfg = pkg.default_config()
         for k, v in fmt.items():
             setattr(cfg, k, v)
@@ -59,7 +65,8 @@ def main():
         if base_ms is None:
             base_ms = ms
         st = dec.stats
-        print(json.dumps({"mask": args.mask, "frames": args.frames, "format": fmt, "kernel": st["kernel"],
+        lay = dec.launch_info(args.frames).get("layout") if st["kernel"] == 3 else None
+        print(json.dumps({"mask": args.mask, "frames": args.frames, "format": fmt, "kernel": st["kernel"], "layout": lay,
                           "ms": round(ms, 4), "info_bits_per_s": args.frames * K / (ms * 1e-3),
                           "vs_shipped": round(ms / base_ms, 3)}), flush=True)
         dec.close()

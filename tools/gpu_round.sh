@@ -48,19 +48,34 @@ for step in "$@"; do
              "par64 frozen_n_16384_k_8192 4096 5 par=64" "q8 frozen_n_16384_k_14746 4096 5 llr_bits=8" \
              "q9 frozen_n_16384_k_8192 4096 5 llr_bits=9"; do
       set -- $c
+      case " ${PROF_ONLY:-$1} " in *" $1 "*) ;; *) continue ;; esac   # PROF_ONLY="c2 c4share": a subset
       mkdir -p "$OUT/$1"
       prof "$@"
     done ;;
   benchprof)
-    for c in "c2 --config c2" "c3 --config c3" "c5 --config c5" "c5b64 --config c5 --batch 64"; do
+    for c in "c2 --config c2" "c3 --config c3" "c5 --config c5" "c5b64 --config c5 --batch 64" \
+             "c4share --config c2 --batch 131072"; do
       set -- $c
       name=$1; shift
+      case " ${PROF_ONLY:-$name} " in *" $name "*) ;; *) continue ;; esac
       ( cd /tmp && export TMPDIR=/tmp &&
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/bench_$name" -o trace --output-format csv -- \
           python3 "$ROOT/bench.py" --no-secondary --no-ebn0-sweep --no-cpu-baseline "$@" \
           > "$OUT/bench_$name.json" 2> "$OUT/bench_$name.err" )
       echo "bench $name traced"
     done ;;
+  formats)
+    # every swept datapath format on N = 16384 x 4096 frames (CA2 on the pair kernel), then the
+    # C5 8-GPU share shape at LLR_BITS 9 (the solo layout)
+    timeout -k 10 600 python -u tools/format_speed.py > "$OUT/format_speed.jsonl" 2> "$OUT/format_speed.err"
+    timeout -k 10 300 python -u tools/format_speed.py --mask frozen_n_262144_k_131072 --frames 64 --steps 5 \
+      --formats "16,1,1,9;16,1,0,9" > "$OUT/format_speed_c5b64_q9.jsonl" 2> "$OUT/format_speed_c5b64_q9.err"
+    echo "formats ok" ;;
+  layout)
+    # pair vs solo around the automatic switch point (2 frames per SIMD = 2048 frames)
+    timeout -k 10 900 python -u tools/layout_ab.py --steps 10 --rounds 2 --configs c3_2048,c3_3072,c3,c5_1024,c5_2048 \
+      --variants "layout=1;layout=2" > "$OUT/layout_ab.jsonl" 2> "$OUT/layout_ab.err"
+    echo "layout ok" ;;
   stamps)
     for b in "$ROOT"/build_tools/pair_stamps_*; do
       case "$b" in *.hip) continue;; esac

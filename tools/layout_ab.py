@@ -18,7 +18,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 CONFIGS = {"c3": ("frozen_n_65536_k_32768", 4096), "c5": ("frozen_n_262144_k_131072", 512),
            "c5_64": ("frozen_n_262144_k_131072", 64), "c3_2048": ("frozen_n_65536_k_32768", 2048),
-           "c3_1024": ("frozen_n_65536_k_32768", 1024), "n16384_4096": ("frozen_n_16384_k_8192", 4096),
+           "c3_1024": ("frozen_n_65536_k_32768", 1024), "c3_3072": ("frozen_n_65536_k_32768", 3072),
+           "c5_1024": ("frozen_n_262144_k_131072", 1024), "c5_2048": ("frozen_n_262144_k_131072", 2048),
+           "n16384_4096": ("frozen_n_16384_k_8192", 4096),
            "n16384_256": ("frozen_n_16384_k_8192", 256), "n65536_256": ("frozen_n_65536_k_32768", 256),
            # (bench.py's secondary entries: polar_sc_config fields as a third element)
            "q8_4096": ("frozen_n_16384_k_14746", 4096, {"llr_bits": 8}),

@@ -97,6 +97,21 @@ def drop_subtree_fences(src):
     return "\n".join(out)
 
 
+def synthetic_roots(src):
+    """A/B variant (C3 wait attribution): every subtree decoder reads its
+    root rows from a register expression of the lane and row instead of its stage slot (and,
+    for fused roots, the parent's slot rows and partial sums): the same straight-line code with
+    no root loads, so the subtree time left is issue time at the same occupancy, and the
+    difference to the real kernel is the time the decoders wait for their root reads (LDS /
+    HBM). The decoded bits are not meaningful."""
+    out = []
+    for line in src.split("\n"):
+        if line.startswith("#define CH(j)"):
+            line = "#define CH(j) ((((u32)(j) * 0x00050003u) ^ (lane_ * 0x00070009u)) & 0x801F801Fu)"
+        out.append(line)
+    return "\n".join(out)
+
+
 def build(mask_name, batch, tuning, variant=""):
     import sc_polar_decoder_hls_amd as pkg
     import util
@@ -107,6 +122,8 @@ def build(mask_name, batch, tuning, variant=""):
     src = dec.kernel_source()
     if variant == "nofence":
         src = drop_subtree_fences(src)
+    elif variant == "synroot":
+        src = synthetic_roots(src)
     N, G, S = mask.size, mask.size // 16, st["sub_words"]
     # launch shape of the library's own decision (polar_sc_plan_launch_info)
     info = dec.launch_info(batch)
@@ -170,7 +187,7 @@ if __name__ == "__main__":
     ap.add_argument("--mask", default="frozen_n_65536_k_32768")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--tuning", default="")
-    ap.add_argument("--variant", default="", choices=["", "nofence"])
+    ap.add_argument("--variant", default="", choices=["", "nofence", "synroot"])
     a = ap.parse_args()
     tun = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, a.tuning.split(",")))}
     build(a.mask, a.batch, tun, a.variant)
