@@ -553,7 +553,9 @@ __device__ __forceinline__ u32 F_split_sm(u32 ma, u32 mb, u32 FS)
 // has magnitude |mb +- ma|, and the SM sign rule gives its sign whenever it is not 0.
 // ---------------------------------------------------------------------------------------
 // sign masks S (0xFFFF per negative half) of the values (M, S) with the zeros made positive
-__device__ __forceinline__ u32 ca2_nzs(u32 M, u32 S) { return pk_mul_lo(pk_min(M, 0x00010001u), S); }
+// (the 1 hidden from the optimiser: it rewrites min(M, 1) as M != 0, v_cmp + v_cndmask per half
+// + v_perm, 6 instructions for 1)
+__device__ __forceinline__ u32 ca2_nzs(u32 M, u32 S) { return pk_mul_lo(pk_min(M, opaque(0x00010001u)), S); }
 // bit 15 / 31 set where the magnitude is not 0 (hard decision mask of an SM16 pair)
 __device__ __forceinline__ u32 ca2_nz(u32 m) { return pk_sub(0u, m & MAG); }
 // F_function_C2 magnitude at width MW: min over m ^ 2^(MW-1) (MIN -> 0, m < 2^(MW-1) -> m + 2^(MW-1))
@@ -607,12 +609,35 @@ __device__ __forceinline__ u32 chan_sm16(u32 raw)
     }
 }
 
+// An all-information block of a CA2 leaf without MIN: its SC decisions depend on the signs and
+// zeros of its LLRs only. With u = the left decisions, G never cancels (a nonzero F value decides
+// its sign xor, so a' takes the sign of b; with a zero F value one operand is 0): the G value is
+// 0 iff both operands are, else it has b's sign, or a' = sign(a) ^ u when b is 0. So the
+// recursion runs on (sign, zero) masks: F = (sa ^ sb, za | zb), G = (zb ? sa ^ u : sb, za & zb),
+// a 2-LLR block decides its true signs. Checked exhaustively against the SC recursion for 4 LLRs
+// in [-3, 3] and 8 LLRs in [-2, 2], and on the device against the FSM (tests/test_ca2.py).
+// S: sign masks (don't-care on zeros), Z: 0xFFFF where the magnitude is 0.
+template <int W>
+__device__ __forceinline__ u32 ca2_allinfo(u32 S, u32 Z, const Lanes &ln)
+{
+    if constexpr (W == 2) {
+        return S & ~Z;
+    } else {
+        constexpr int H = W / 2;
+        const u32 PS = xorlane<H>(S), PZ = xorlane<H>(Z);
+        const u32 xa = ca2_allinfo<H>(S ^ PS, Z | PZ, ln);               // valid on a-lanes
+        const u32 u = xorlane<H>(xa);                                     // (b-lanes: S = sb, PS = sa)
+        const u32 xb = ca2_allinfo<H>(bselo(Z, PS ^ u, S), Z & PZ, ln);  // valid on b-lanes
+        return bselo(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
+    }
+}
+
 // Leaf Spec_P16_ext / Spec_P16 in CA2 (functions.h:366-546 with F_function_C2, G_extended_C2
 // or G_function_C2, F_simplified_C2 / G_simplified_C2, :89-118) on split words with the
 // conventions above (the recursion of functions.h:413-492). MW != 0: the leaf can hold
 // MIN of width MW (the first PAR word), its F ops take the key min and its exact G children
 // MIN one bit wider. Unlike SIGMAG an all-information block of 4+ LLRs is not its hard
-// decisions (a zero F value decides 0, not the sign xor), so only 2-LLR blocks take them.
+// decisions (a zero F value decides 0, not the sign xor): without MIN it takes ca2_allinfo.
 template <u32 FB, int B, int W, int MW>
 __device__ __forceinline__ u32 leaf_ca2(u32 M, u32 S, const Lanes &ln)
 {
@@ -620,6 +645,8 @@ __device__ __forceinline__ u32 leaf_ca2(u32 M, u32 S, const Lanes &ln)
     constexpr u32 sub = FB & bm;
     if constexpr (sub == 0u) {
         return 0u;
+    } else if constexpr (sub == bm && W >= 4 && MW == 0) {
+        return ca2_allinfo<W>(S, opaque(pk_sra(pk_sub(M, 0x00010001u), 15)), ln);   // (zero masks: M - 1 < 0)
     } else if constexpr (W == 2) {
         if constexpr (sub == bm) {
             return ca2_nzs(M, S);                                  // x = (sign a, sign b)

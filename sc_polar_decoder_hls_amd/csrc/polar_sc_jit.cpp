@@ -1259,8 +1259,14 @@ PairShape pair_shape(const polar_sc_plan &p, long batch, int simds, int regs, in
     const long cus = simds > 0 ? simds / 4 : 256;
     int W = p.tune.waves_per_group;
     if (W == 0) {
+        // more waves per pair while the batch leaves SIMDs without 2 waves, but never past one
+        // dispatch round: the blocks must all be resident at once (512 / regs waves per SIMD).
+        // Same box (profiles/r06_v3 layout_ab): 1536 pairs at W = 2 (3072 waves of 248 registers,
+        // two rounds) 1.27 ms, where 2048 pairs at W = 1 take 0.83 ms
+        const long sm = simds > 0 ? simds : 1024;
+        const long wps = regs > 0 ? std::max(1, 512 / regs) : 2;
         W = 1;
-        while (W < PAIR_WAVES_MAX && sh.pairs * W < 2 * (simds > 0 ? simds : 1024)) W *= 2;
+        while (W < PAIR_WAVES_MAX && sh.pairs * W < 2 * sm && sh.pairs * 2 * W <= sm * wps) W *= 2;
     }
     if (W > PAIR_WAVES_MAX) W = PAIR_WAVES_MAX;
     const bool tier = !p.pair_tier.steps.empty();

@@ -439,12 +439,27 @@ def leaf_ms(FB, B, W, M, S, ln):
     return bsel(ln.a[H], xa ^ xorlane(H, xb), xb)
 
 
+def ca2_allinfo(W, S, Z, ln):
+    """polar_sc_device.h ca2_allinfo: an all-information CA2 block on (sign, zero) masks"""
+    S, Z = V(S), V(Z)
+    if W == 2:
+        return S & ~Z
+    H = W // 2
+    PS, PZ = xorlane(H, S), xorlane(H, Z)
+    xa = ca2_allinfo(H, S ^ PS, Z | PZ, ln)
+    u = xorlane(H, xa)
+    xb = ca2_allinfo(H, bsel(Z, PS ^ u, S), Z & PZ, ln)
+    return bsel(ln.a[H], xa ^ xorlane(H, xb), xb)
+
+
 def leaf_ca2(FB, B, W, MW, M, S, ln):
     """polar_sc_device.h leaf_ca2"""
     bm = ((1 << W) - 1) << B
     sub = FB & bm
     if sub == 0:
         return V(0)
+    if sub == bm and W >= 4 and MW == 0:
+        return ca2_allinfo(W, S, pk_sra(pk_sub(M, 0x00010001), 15), ln)
     if W == 2:
         if sub == bm:
             return ca2_nzs(M, S)

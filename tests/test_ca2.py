@@ -124,3 +124,39 @@ def test_ca2_pair_kernel_full_batch(pkg, cuda, oracle_mod):
         out = dec.decode(cuda.from_numpy(np.where(x == 1, -17, 17).astype(np.int8)).cuda())
         cuda.cuda.synchronize()
         assert (pkg.unpack_bits(out.cpu().numpy(), mask.size) == x).all(), par
+
+
+def test_ca2_leaf_vs_oracle(pkg, oracle_mod):
+    """CPU: the CA2 leaf of the generated code (leaf_ca2, incl. the all-information blocks on
+    sign / zero masks, ca2_allinfo) emulated on 64 lanes equals the oracle's Spec_P16_ext in CA2
+    (oracle/polar_oracle.c spec_pn) on words with dense zeros, for every pattern class."""
+    import pair_emu
+    pair_emu.configure(6, ca2=True, ext=True)
+    try:
+        ln = pair_emu.Lanes()
+        rng = np.random.default_rng(16)
+        pats = [0xFFFF, 0xFFFE, 0xFF00, 0xF0F0, 0xFEE8, 0xE800, 0x8000, 0xFFF0, 0xCCCC, 0xFF0F] + \
+            [int(x) for x in rng.integers(0, 1 << 16, 20)]
+        pos = pair_emu.lane_pos(pair_emu.LANE & 15)
+        row = pair_emu.LANE >> 4
+        for fb in pats:
+            for trial in range(6):
+                p0 = (0.1, 0.3, 0.6)[trial % 3]
+                v = rng.integers(-31, 32, size=(2, 4, 16))
+                v[rng.random(v.shape) < p0] = 0
+                val = v[:, row, pos]                       # [frame, lane]
+                M = pair_emu.pk(np.abs(val[0]), np.abs(val[1]))
+                # (odd trials: zeros carry a set sign bit, which the split code must ignore)
+                neg = (val < 0) | ((val == 0) & (trial % 2 == 1) & (rng.random(val.shape) < 0.5))
+                S = pair_emu.pk(np.where(neg[0], 0xFFFF, 0), np.where(neg[1], 0xFFFF, 0))
+                x = pair_emu.V(pair_emu.leaf_gen_ca2(fb, 0, M, S, ln)).astype(np.int64)
+                with oracle_mod._format(6, 16, 0, 1):
+                    for f in range(2):
+                        for r in range(4):
+                            want = oracle_mod.leaf16(v[f, r] & 63, fb)
+                            got = 0
+                            for L in range(16 * r, 16 * r + 16):
+                                got |= ((x[L] >> (15 + 16 * f)) & 1) << int(pos[L])
+                            assert got == want, (hex(fb), trial, f, r, v[f, r].tolist(), hex(got), hex(want))
+    finally:
+        pair_emu.configure()

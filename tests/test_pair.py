@@ -45,6 +45,10 @@ def test_pair_plan_stats(pkg):
     # automatic: fused from 16 subtrees per frame on (N = 16384, G = 4 S: slot roots)
     assert "_F(c.slot_ptr" not in pair(pkg, util.mask("frozen_n_16384_k_8192")).kernel_source()
     assert "_F(c.slot_ptr" in pair(pkg, util.mask("frozen_n_16384_k_8192"), sub_root=2).kernel_source()
+    # waves per pair: more while the batch leaves SIMDs without 2 waves, never past one dispatch
+    # round (1536 pairs x 2 waves of 248 registers would be two rounds at 2 waves per SIMD)
+    c3 = pair(pkg, util.mask("frozen_n_65536_k_32768"))
+    assert [c3.launch_info(b, cus=256)["waves_per_block"] for b in (4096, 3072, 2048, 512)] == [1, 1, 2, 8]
     s = pair(pkg, util.mask("frozen_n_2048_k_1024")).stats
     assert s["sub_words"] == 64
     s = pair(pkg, util.mask("frozen_n_262144_k_131072"), tier_words=1024).stats

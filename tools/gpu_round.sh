@@ -73,7 +73,8 @@ for step in "$@"; do
     echo "formats ok" ;;
   layout)
     # pair vs solo around the automatic switch point (2 frames per SIMD = 2048 frames)
-    timeout -k 10 900 python -u tools/layout_ab.py --steps 10 --rounds 2 --configs c3_2048,c3_3072,c3,c5_1024,c5_2048 \
+    timeout -k 10 900 python -u tools/layout_ab.py --steps 10 --rounds 2 \
+      --configs "${LAYOUT_CONFIGS:-c3_2048,c3_3072,c3,c5_1024,c5_2048}" \
       --variants "layout=1;layout=2" > "$OUT/layout_ab.jsonl" 2> "$OUT/layout_ab.err"
     echo "layout ok" ;;
   stamps)

@@ -140,7 +140,7 @@ def census(asm):
     funcs = {}
     cur, cls = None, None
     for line in asm.split("\n"):
-        m = re.match(r"^(_Z\w*polar_psub_(\d+(?:_[FG])?)\w*):", line)   # (_F / _G: fused-root variants)
+        m = re.match(r"^(_Z\w*polar_psub_(\d+(?:_[FG])?(?:_L)?)\w*):", line)   # (_F / _G: fused roots; _L: CA2 leftmost)
         if m:
             cur = m.group(2)
             funcs[cur] = (collections.Counter(), collections.Counter())
@@ -170,11 +170,17 @@ def main():
     ap.add_argument("--mask", default="frozen_n_262144_k_131072")
     ap.add_argument("--tuning", default="")
     ap.add_argument("--source", help="census of this generated source file instead of the plan's")
+    ap.add_argument("--config", default="", help="polar_sc_config fields, e.g. sigmag=0,par=64")
     args = ap.parse_args()
     import sc_polar_decoder_hls_amd as pkg
     import util
     tun = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in args.tuning.split(",") if kv)
-    dec = pkg.Decoder(util.mask(args.mask), tuning=tun or None)
+    cfg = None
+    if args.config:
+        cfg = pkg.default_config()
+        for kv in args.config.split(","):
+            setattr(cfg, kv.split("=")[0], int(kv.split("=")[1]))
+    dec = pkg.Decoder(util.mask(args.mask), config=cfg, tuning=tun or None)
     src = open(args.source).read() if args.source else dec.kernel_source()
     if "polar_sc_mask_kernel(" in src:   # per-mask kernel: one straight-line function
         marked, nmark = mark_mask_kernel(src)
@@ -186,7 +192,7 @@ def main():
         for c, v in sorted(tot_v.items(), key=lambda kv: -kv[1]):
             print("%-14s %10d %5.1f%% %10d" % (c, v, 100.0 * v / max(nv, 1), tot_a[c]))
         return
-    calls = collections.Counter(re.findall(r"polar_psub_(\d+(?:_[FG])?)\(c\.slot_ptr", src.split("polar_sc_pair_subtest_kernel")[0]))
+    calls = collections.Counter(re.findall(r"polar_psub_(\d+(?:_[FG])?(?:_L)?)\(c\.slot_ptr", src.split("polar_sc_pair_subtest_kernel")[0]))
     marked, nmark = mark(src)
     with tempfile.TemporaryDirectory() as tmp:
         asm = compile_asm(marked, tmp)

@@ -112,6 +112,24 @@ def synthetic_roots(src):
     return "\n".join(out)
 
 
+def synthetic_bits(src):
+    """A/B variant: the fused-root G decoders take the partial sums of their root G from a
+    register expression instead of the pair's HBM bit dwords (the LDS / HBM slot reads stay)"""
+    return src.replace("ubits4(hb_[((ub_ + ((j) & ~1)) >> 4) * 64], ub_ + ((j) & ~1))",
+                       "ubits4(lane_ * 0x9E3779B9u ^ (u32)(j), ub_ + ((j) & ~1))")
+
+
+def synthetic_slots(src):
+    """A/B variant: the root rows' slot reads (SLOT(j): the parent level in LDS or HBM) from a
+    register expression (the partial-sum reads of G roots stay)"""
+    out = []
+    for line in src.split("\n"):
+        if line.startswith("#define SLOT(j)") and "su_t" not in line:
+            line = "#define SLOT(j) ((((u32)(j) * 0x05030201u) ^ (lane_ * 0x01070309u)) & 0x9F9F9F9Fu)"
+        out.append(line)
+    return "\n".join(out)
+
+
 def build(mask_name, batch, tuning, variant=""):
     import sc_polar_decoder_hls_amd as pkg
     import util
@@ -124,6 +142,10 @@ def build(mask_name, batch, tuning, variant=""):
         src = drop_subtree_fences(src)
     elif variant == "synroot":
         src = synthetic_roots(src)
+    elif variant == "synbits":
+        src = synthetic_bits(src)
+    elif variant == "synslot":
+        src = synthetic_slots(src)
     N, G, S = mask.size, mask.size // 16, st["sub_words"]
     # launch shape of the library's own decision (polar_sc_plan_launch_info)
     info = dec.launch_info(batch)
@@ -187,7 +209,7 @@ if __name__ == "__main__":
     ap.add_argument("--mask", default="frozen_n_65536_k_32768")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--tuning", default="")
-    ap.add_argument("--variant", default="", choices=["", "nofence", "synroot"])
+    ap.add_argument("--variant", default="", choices=["", "nofence", "synroot", "synbits", "synslot"])
     a = ap.parse_args()
     tun = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, a.tuning.split(",")))}
     build(a.mask, a.batch, tun, a.variant)
