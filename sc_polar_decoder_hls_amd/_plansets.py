@@ -198,6 +198,33 @@ def ca2_gpu_items():
     return out
 
 
+# ---- PAR 4 / 8 on the pair kernel (tests/test_par48.py) ---------------------------------
+def par48_gpu_items():
+    """(id, mask, config fields, tuning) of the PAR 4 / 8 pair-kernel GPU tests"""
+    out = []
+    for par in (4, 8):
+        P = {"par": par}
+        for n in ("frozen_n_2048_k_1024", "frozen_n_16384_k_8192", "frozen_n_65536_k_32768"):
+            out.append(("%s_p%d" % (n, par), mask(n), P, None))
+        rng = np.random.default_rng(480 + par)
+        pm = planted_mask(rng, 16384, par)
+        for c7 in (SHIPPED_C7, (1, 1, 1, 1, 1, 1, 0), (0, 0, 0, 0, 0, 0, 0), (2, 1, 1, 1, 1, 1, 1)):
+            out.append(("planted16384_p%d_pl%d_%d" % (par, c7[0], sum(c7)), pm, dict(c7_fields(c7), **P), None))
+        for q in (5, 8, 9):
+            for ext in (1, 0):
+                out.append(("planted16384_p%d_q%d_e%d" % (par, q, ext), pm, dict(P, llr_bits=q, extended=ext), None))
+        for i, m in enumerate(struct_masks(8192)):
+            out += [("struct8192_%d_p%d_s%d" % (i, par, sw), m, P, {"kernel": 3, "layout": 1, "sub_words": sw})
+                    for sw in (32, 256)]
+        for wpg in (1, 8):
+            out.append(("wave_mask_p%d_w%d" % (par, wpg), wave_mask(), P,
+                        {"kernel": 3, "layout": 1, "waves_per_group": wpg, "sub_words": 64}))
+        out.append(("planted16384_p%d_fused" % par, pm, P, {"kernel": 3, "layout": 1, "sub_root": 2}))
+        out.append(("tier32768_p%d" % par, mask("frozen_n_32768_k_29492"), P,
+                    {"kernel": 3, "layout": 1, "tier_words": 512, "sub_words": 128}))
+    return out
+
+
 # ---- LLR_BITS 9 (tests/test_gpu_formats.py test_llr9_pair_kernel, tests/test_solo.py q9 tests):
 # automatic plans, which hold the solo alternate for small batches ----------------------------
 Q9_MASKS = ("frozen_n_2048_k_1024", "frozen_n_16384_k_8192", "frozen_n_65536_k_32768", "frozen_n_262144_k_131072")
@@ -286,8 +313,8 @@ def sweep_items():
         out += [(n, mask(n), c7_fields(c7), None) for n in SWEEP_MASKS]
         out += [("planted%d" % N, sweep_planted_mask(N), c7_fields(c7), None) for N in PLANTED_N]
     # script_tests.sh:105-106's loop at PAR 16, QUANT 8 on the default (pair) kernel
-    out += [("frozen_n_32768_k_29492", mask("frozen_n_32768_k_29492"), dict(c7_fields(c7), llr_bits=8), None)
-            for c7 in PRUNING_SWEEP]
+    out += [("frozen_n_32768_k_29492", mask("frozen_n_32768_k_29492"), dict(c7_fields(c7), llr_bits=8, par=par), None)
+            for c7 in PRUNING_SWEEP for par in (16, 8, 4)]
     for q in (5, 7, 8):
         for c7 in (SHIPPED_C7, (1, 1, 1, 1, 1, 1, 0)):
             out += [(n, mask(n), dict(c7_fields(c7), llr_bits=q), None) for n in QBITS_MASKS]
@@ -324,3 +351,4 @@ def prewarm_all(verbose=False):
     _build.prewarm_items(sweep_items(), verbose=verbose)
     _build.prewarm_items(ca2_items(), verbose=verbose)
     _build.prewarm_items(q9_items(), verbose=verbose)
+    _build.prewarm_items(par48_gpu_items(), verbose=verbose)

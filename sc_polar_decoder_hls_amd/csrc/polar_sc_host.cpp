@@ -349,11 +349,13 @@ void emit_word(std::vector<polar_sc_op> &out, const polar_sc_plan &p, int code, 
 void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int level, uint32_t g0, uint32_t cnt,
                   bool is_root, SubCtx *sc)
 {
-    // (sc->words counts device words; g0 / cnt count PAR groups of p16 words: PAR 64 -> 4)
-    if (sc && !is_root && cnt * p.p16 == sc->words) {
+    // (sc->words counts device words; g0 / cnt count PAR groups of p16 words: PAR 64 -> 4, or
+    // of 1 / ppw words: PAR 4 -> 1 / 4)
+    const uint32_t cnt_words = p.ppw > 1 ? cnt / p.ppw : cnt * p.p16;
+    if (sc && !is_root && cnt_words == sc->words) {
         std::vector<polar_sc_op> sub;
         compile_node(p, sub, level, g0, cnt, false, nullptr);
-        const int w0 = (int)(g0 * p.p16);
+        const int w0 = (int)(p.ppw > 1 ? g0 / p.ppw : g0 * p.p16);
         for (polar_sc_op &o : sub) {
             o.level -= level;
             o.pos -= w0;
@@ -370,7 +372,7 @@ void compile_node(const polar_sc_plan &p, std::vector<polar_sc_op> &out, int lev
             id = it->second;
         }
         sc->calls++;
-        emit(out, polar_host::POLAR_OP_SUB, level, (int)(cnt * p.p16), w0, -1, (uint32_t)id);
+        emit(out, polar_host::POLAR_OP_SUB, level, (int)cnt_words, w0, -1, (uint32_t)id);
         return;
     }
     const uint32_t h = cnt / 2;
@@ -868,11 +870,14 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // the leftmost path) with plain leaves (PRUNING_LEVEL 0 / 2; the PRUNING_LEVEL 1 decoders of
     // CA2 stay on the interpreter), except 9-bit LLRs at PAR 64, whose 16-bit REP accumulator
     // (2^15 - 1) leaves no headroom in a 16-bit half
+    // and PAR 4 / 8 SIGMAG (the PAR words = lane groups of a device word: every one-word leaf
+    // record decodes its whole word tree with the frozen bits and group classes as template
+    // constants, polar_sc_device.h word_gen; REP over the groups, polar_sc_pair.h rep_groups_*)
     bool leaf_kinds = false;
     for (const polar_sc_op &o : p->ops)
         if ((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && ((o.fb >> 16) & 7u) != 0u) leaf_kinds = true;
     const bool pair_par = c.par == 16 || c.par == 32 || c.par == 64;
-    const bool pair_fmt = dflt || (pair_par && c.sigmag == 1 && c.llr_bits <= 9) ||
+    const bool pair_fmt = dflt || ((pair_par || c.par == 4 || c.par == 8) && c.sigmag == 1 && c.llr_bits <= 9) ||
                           (pair_par && c.sigmag == 0 && !leaf_kinds && c.llr_bits <= 9 && !(c.llr_bits == 9 && c.par == 64));
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR

@@ -365,225 +365,8 @@ __device__ __forceinline__ uint32_t leaf_kind_dp(uint32_t L, uint32_t kind, cons
     }
 }
 
-// bit reversal of the low `bits` bits
-__device__ __forceinline__ uint32_t bitrev_n(uint32_t v, int bits)
-{
-    return bits ? (__builtin_bitreverse32(v) >> (32 - bits)) : 0u;
-}
-// SPC search key of device word i (the lane's bitrev4 position is ORed in later, shifted by
-// LPAR - 4): PAR word index, then bitrev_{LPAR}(position in the PAR word) -- the order of the
-// Min_Mask_{PAR} tournament within a PAR word plus the strict '<' across PAR words
-// PAR < 16: the PAR words of device word i are its lane groups: key i << 4, the lane part
-// (spc_lane_key) carries the group and bitrev_{LPAR}(position in the group)
-__device__ __forceinline__ uint32_t spc_word_key(int i)
-{
-    if constexpr (LPAR < 4) return (uint32_t)i << 4;
-    else return ((uint32_t)(i / P16) << LPAR) | bitrev_n((uint32_t)(i % P16), LPAR - 4);
-}
-// device word of a min key
-__device__ __forceinline__ int spc_key_word(uint32_t key)
-{
-    const uint32_t k = key & 0xFFFFFFu;
-    if constexpr (LPAR < 4) return (int)(k >> 4);
-    else return (int)((k >> LPAR) * P16 + bitrev_n(k & (uint32_t)(P16 - 1), LPAR - 4));
-}
-// the lane's part of an SPC key and the mask that isolates it
-__device__ __forceinline__ uint32_t spc_lane_key(const Lanes &ln)
-{
-    if constexpr (LPAR < 4)
-        return (ln.pos & ~(uint32_t)((1 << LPAR) - 1)) | bitrev_n(ln.pos & (uint32_t)((1 << LPAR) - 1), LPAR);
-    else
-        return ln.br << (LPAR - 4);
-}
-constexpr uint32_t SPC_LANE_BITS = LPAR < 4 ? 15u : (15u << (LPAR - 4));
-// |lambda| of a (saturated) G output as the SPC trees compare it (VECTOR_ABS_SM / qabs)
-__device__ __forceinline__ uint32_t spc_mag(uint32_t lam)
-{
-    if constexpr (CA2) return pk_abs_i16(lam);
-    else return lam & MAG;
-}
-
-constexpr bool DEFAULT_FMT = !CA2 && LPAR == 4 && QB <= 8;
-constexpr int PARW = 1 << LPAR;   // PAR in lanes (PAR < 16: a lane group of a device word)
-
-// ---------------------------------------------------------------------------------------
-// PAR 4 / 8 (LPAR < 4): PPW PAR words share a device word as aligned lane groups
-// ---------------------------------------------------------------------------------------
-// one level of the exact pair tree ADD_TREE_{PAR} (functions.h:3036-3083): partners at position
-// distance D, the lower lane as operand a; butterfly, so both partners hold the pair total
-template <int D>
-__device__ __forceinline__ uint32_t tree_step(uint32_t v, const Lanes &ln)
-{
-    const uint32_t p = xorlane<D>(v);
-    if constexpr (CA2) return pk_add(v, p);
-    else return G_sm<0>(bsel(ln.template amask<D>(), v, p), bsel(ln.template amask<D>(), p, v), 0u);
-}
-// pair-tree levels at distances W/2 .. DMIN (DMIN 2: REP2, the even / odd classes)
-template <int W, int DMIN>
-__device__ __forceinline__ uint32_t add_tree_w(uint32_t v, const Lanes &ln)
-{
-    if constexpr (W / 2 >= DMIN) return add_tree_w<W / 2, DMIN>(tree_step<W / 2>(v, ln), ln);
-    else return v;
-}
-template <int W, int DMIN>
-__device__ __forceinline__ uint32_t xor_tree_w(uint32_t v)
-{
-    if constexpr (W / 2 >= DMIN) return xor_tree_w<W / 2, DMIN>(v ^ xorlane<W / 2>(v));
-    else return v;
-}
-template <int W, int DMIN>
-__device__ __forceinline__ uint32_t min_tree_w(uint32_t v)
-{
-    if constexpr (W / 2 >= DMIN) return min_tree_w<W / 2, DMIN>(__builtin_elementwise_min(v, xorlane<W / 2>(v)));
-    else return v;
-}
-// REP accumulator step (ADDER_TREE_{PAR} accumulate, functions.h:3163-3320): acc + T,
-// saturated at REPSAT (SIGMAG: qfull_adder_sat_sm; CA2: qadd)
-__device__ __forceinline__ uint32_t rep_sat_add(uint32_t acc, uint32_t t)
-{
-    if constexpr (CA2) {
-        const uint32_t d = pk_add(acc, t);
-        return pk_min_i16(pk_max_i16(d, (0x10000u - REPSAT) * 0x00010001u), REPSAT * 0x00010001u);
-    } else {
-        return G_sm<REPSAT>(t, acc, 0u);
-    }
-}
-// the saturating chain over CNT consecutive lane groups (PARW lanes each) in group order;
-// t = each lane's group total, gr = the lane's group index relative to the first one
-template <int CNT>
-__device__ __forceinline__ uint32_t group_chain(uint32_t acc, uint32_t t, uint32_t gr)
-{
-    if constexpr (CNT == 1) {
-        return rep_sat_add(acc, t);
-    } else if constexpr (CNT == 2) {
-        const uint32_t o = xorlane<PARW>(t);
-        acc = rep_sat_add(acc, (gr & 1u) ? o : t);
-        return rep_sat_add(acc, (gr & 1u) ? t : o);
-    } else {   // CNT == 4 (PAR 4, a whole word): the totals of groups gr ^ 1, ^ 2, ^ 3
-        uint32_t v[4];
-        v[0] = t;
-        v[1] = xorlane<PARW>(t);
-        v[2] = xorlane<2 * PARW>(t);
-        v[3] = xorlane<PARW>(v[2]);
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++) {
-            const uint32_t k = (gr & 3u) ^ j;
-            acc = rep_sat_add(acc, k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3]);
-        }
-        return acc;
-    }
-}
-// PRUNING_LEVEL 1 leaf decoders of one PAR word of W (= PAR) lanes (library.h:187-280):
-// REP / REP2 / SPC / SPC2 / R1, as leaf_kind_dp over a lane group
-template <int W>
-__device__ __forceinline__ uint32_t leaf_kind_w(uint32_t L, uint32_t kind, const Lanes &ln, int w)
-{
-    if (kind == 5) return L & SGN;   // Spec_Node_R1: VECTOR_SIGN
-    if (kind == 1) return add_tree_w<W, 1>(L, ln) & SGN;
-    if (kind == 3) return add_tree_w<W, 2>(L, ln) & SGN;
-    const bool spc2 = kind == 4;
-    const uint32_t h = L & SGN;
-    const uint32_t par = spc2 ? xor_tree_w<W, 2>(h) : xor_tree_w<W, 1>(h);
-    uint32_t mg;
-    if constexpr (CA2) mg = pk_add(ca2_qabs(L, w), (1u << (w - 1)) * 0x00010001u);   // order-preserving, >= 0
-    else mg = L & 0x7FFF7FFFu;
-    const uint32_t br = bitrev_n(ln.pos & (uint32_t)(W - 1), LPAR);
-    uint32_t klo = ((mg & 0xFFFFu) << 4) | br, khi = ((mg >> 16) << 4) | br;
-    const uint32_t mlo0 = klo, mhi0 = khi;
-    klo = spc2 ? min_tree_w<W, 2>(klo) : min_tree_w<W, 1>(klo);
-    khi = spc2 ? min_tree_w<W, 2>(khi) : min_tree_w<W, 1>(khi);
-    const uint32_t flo = (klo == mlo0) ? (par & 0x8000u) : 0u;
-    const uint32_t fhi = (khi == mhi0) ? (par & 0x80000000u) : 0u;
-    return h ^ flo ^ fhi;
-}
-// group classes of a word (the host's do_prunning result, polar_sc_host.cpp word_info):
-// per group g, bits 7g..7g+3 = class (NODE_* codes), 7g+4..7g+6 = PR1 leaf kind; bit 28 =
-// PRUNING_LEVEL 2
-constexpr uint32_t WN_R0 = 0x00, WN_R1 = 0x0F, WN_REP = 0x02, WN_SPC = 0x04, WN_RN = 0x08;
-__device__ __forceinline__ uint32_t wgroup_type(uint32_t info, int g) { return (info >> (7 * g)) & 15u; }
-__device__ __forceinline__ uint32_t wgroup_kind(uint32_t info, int g) { return (info >> (7 * g + 4)) & 7u; }
-// node class of groups [g0, g0 + cnt) as the F / G loops aggregate it (my_module.h:403-471,
-// 739-806; polar_sc_host.cpp node_class)
-__device__ __forceinline__ uint32_t wnode_class(uint32_t info, int g0, int cnt)
-{
-    uint32_t r0 = 0, r1 = 0x0F;
-    bool r0_but_last = true, r1_but_first = true;
-    for (int t = 0; t < cnt; t++) {
-        const uint32_t T = wgroup_type(info, g0 + t);
-        r0 |= T;
-        r1 &= T;
-        if (t + 1 < cnt && T != WN_R0) r0_but_last = false;
-        if (t > 0 && T != WN_R1) r1_but_first = false;
-    }
-    if (r0 == WN_R0) return WN_R0;
-    if (r1 == WN_R1) return WN_R1;
-    if (r0_but_last && wgroup_type(info, g0 + cnt - 1) == WN_REP) return WN_REP;
-    if (r1_but_first && wgroup_type(info, g0) == WN_SPC) return WN_SPC;
-    return WN_RN;
-}
-// G_SPC_STATE on the W lanes of a node inside a word (my_module.h:1737-1842): hard decisions,
-// parity over the node, flip at the minimum (|lambda|, group, bitrev_{LPAR}(position))
-template <int W>
-__device__ __forceinline__ uint32_t word_spc(uint32_t L, const Lanes &ln)
-{
-    const uint32_t h = L & SGN;
-    const uint32_t par = xor_tree_w<W, 1>(h);
-    const uint32_t mg = spc_mag(L), lk = spc_lane_key(ln);
-    uint32_t klo = ((mg & 0xFFu) << 24) | lk, khi = (((mg >> 16) & 0xFFu) << 24) | lk;
-    klo = min_tree_w<W, 1>(klo);
-    khi = min_tree_w<W, 1>(khi);
-    const uint32_t flo = ((par & 0x8000u) && (klo & 15u) == lk) ? 0x8000u : 0u;
-    const uint32_t fhi = ((par & 0x80000000u) && (khi & 15u) == lk) ? 0x80000000u : 0u;
-    return h ^ flo ^ fhi;
-}
-// the PAR-word leaf of group g at lanes [B, B + PAR): its PR1 decoder or Spec_P{PAR} exact
-template <int B>
-__device__ __forceinline__ uint32_t word_leaf(uint32_t L, uint32_t fb, uint32_t info, int g, const Lanes &ln)
-{
-    const uint32_t kind = wgroup_kind(info, g);
-    if (kind) return leaf_kind_w<PARW>(L, kind, ln, QB);
-    const uint32_t fbm = ((fb >> ln.pos) & 1u) ? SGN : 0u;
-    return leaf_dp<B, PARW>(L, fb, fbm, ln, QB);
-}
-// compile_node (polar_sc_host.cpp) inside one device word: the node of W LLRs at lanes
-// [B, B + W) (W / PAR >= 2 groups), its LLRs L valid on those lanes; returns x (sign-position
-// flags) on the same lanes. F / G at these levels are the stage functions (G saturated), the
-// PAR-word leaves exact; children pruned at PRUNING_LEVEL 2 as the FSM prunes them.
-template <int B, int W>
-__device__ uint32_t word_node(uint32_t L, uint32_t fb, uint32_t info, const Lanes &ln)
-{
-    constexpr int H = W / 2;               // child LLRs
-    constexpr int h = (W >> LPAR) / 2;     // groups per child
-    const int g0 = B >> LPAR;
-    const bool prune = (info >> 28) & 1u;
-    const uint32_t tl = prune ? wnode_class(info, g0, h) : WN_RN;
-    const uint32_t tr = prune ? wnode_class(info, g0 + h, h) : WN_RN;
-    const uint32_t P = xorlane<H>(L);      // the partner: on a-lanes b, on b-lanes a
-    const uint32_t gr = (ln.pos >> LPAR) - (uint32_t)g0;   // group of the lane relative to g0
-    uint32_t xa = 0;
-    const bool lz = tl == WN_R0;           // H0 route: no F, G with u = 0, then H0
-    if (!lz) {
-        const uint32_t La = dp_F(L, P, QB);   // valid on [B, B + H)
-        if (tl == WN_REP) {
-            xa = group_chain<h>(0u, add_tree_w<PARW, 1>(La, ln), gr) & SGN;   // F_REP_STATE
-        } else {
-            if constexpr (h == 1) xa = word_leaf<B>(La, fb, info, g0, ln);
-            else xa = word_node<B, H>(La, fb, info, ln);
-        }
-    }
-    const uint32_t Lb = dp_G<true>(P, L, lz ? 0u : xorlane<H>(xa));   // valid on [B + H, B + W)
-    uint32_t xb;
-    if (tr == WN_R1) {
-        xb = Lb & SGN;                         // G_R1_STATE
-    } else if (tr == WN_SPC) {
-        xb = word_spc<H>(Lb, ln);              // G_SPC_STATE
-    } else {
-        if constexpr (h == 1) xb = word_leaf<B + H>(Lb, fb, info, g0 + 1, ln);
-        else xb = word_node<B + H, H>(Lb, fb, info, ln);
-    }
-    const uint32_t xbp = xorlane<H>(xb);
-    return bsel(ln.template amask<H>(), lz ? xbp : (xa ^ xbp), xb);
-}
+// (the PAR-word helpers -- bitrev_n .. word_node, spc keys, PARW -- live in polar_sc_device.h:
+// the generated pair kernels of PAR 4 / 8 decode their device words with them too)
 
 // F/G with NB_ITER = 1 followed by R_STATE: Spec_Polar_Decoder on reg_result
 // (my_module.h:544-612). Inside a PAR-word leaf (PAR > 16) G may be exact (FB_EXACT) and

@@ -127,7 +127,7 @@ __device__ __forceinline__ u32 G_split_x(u32 ma, u32 mb, u32 X, u32 &LT)
 // node (and one slot row); PAR 32 (5): two device words = rows (0, 1) / (2, 3) of a register;
 // PAR 16: one device word = one row
 constexpr bool PAIR_P64 = LPAR == 6, PAIR_P32 = LPAR == 5;
-static_assert(LPAR >= 4 && LPAR <= 6, "pair plans: PAR 16, 32 or 64");
+static_assert(LPAR >= 2 && LPAR <= 6, "pair plans: PAR 4 .. 64");
 __device__ __forceinline__ u32 bitrev2(u32 r) { return ((r & 1u) << 1) | (r >> 1); }
 // SPC key bits below the register index (bits 0..5): the tie order of equal magnitudes inside a
 // register -- PAR 16: (word = row, then bitrev4(position)); PAR 32: (PAR word row / 2, then
@@ -135,14 +135,24 @@ __device__ __forceinline__ u32 bitrev2(u32 r) { return ((r & 1u) << 1) | (r >> 1
 // word) = (bitrev4(position), then bitrev2(row)) (polar_sc_interp.h spc_word_key / spc_lane_key)
 __device__ __forceinline__ u32 spc_sub(u32 row, const Lanes &ln)
 {
+    // PAR 4 / 8: (word = row, group, bitrev_{LPAR}(position in the group)), polar_sc_device.h
+    // spc_lane_key
+    if constexpr (LPAR < 4) return (row << 4) | spc_lane_key(ln);
     if constexpr (PAIR_P64) return (ln.br << 2) | bitrev2(row);
     else if constexpr (PAIR_P32) return ((row >> 1) << 5) | (ln.br << 1) | (row & 1u);
     else return (row << 4) | ln.br;
 }
+// the key bits of a lane inside one device word: bitrev4(position) (PAR >= 16), or (group,
+// bitrev_{LPAR}(position in the group)) for PAR 4 / 8
+__device__ __forceinline__ u32 spc_lk(const Lanes &ln)
+{
+    if constexpr (LPAR < 4) return spc_lane_key(ln);
+    else return ln.br;
+}
 // the same for a node of two words (row r holds word r & 1): PAR 16 two PAR words, PAR 32 one
 __device__ __forceinline__ u32 spc_sub2(u32 row, const Lanes &ln)
 {
-    return PAIR_P32 ? (ln.br << 1) | (row & 1u) : ((row & 1u) << 4) | ln.br;
+    return PAIR_P32 ? (ln.br << 1) | (row & 1u) : ((row & 1u) << 4) | spc_lk(ln);
 }
 // REP accumulation of one register's four row totals (row_sum_biased values, +8192 per half):
 // PAR 16 -- four PAR words in order (word 4 i + row); PAR 32 -- two PAR words, the exact totals
@@ -159,6 +169,68 @@ __device__ __forceinline__ u32 rep_acc_rows(u32 acc, u32 t0, u32 t1, u32 t2, u32
         return rep_acc(rep_acc(rep_acc(rep_acc(acc, t0), t1), t2), t3);
     }
 }
+// PAR 4 / 8 (LPAR < 4): the PAR words of a device word are its lane groups. REP accumulates the
+// exact pair tree of every group (ADD_TREE_{PAR}), groups in lane order within a word, words in
+// order, in exact SM arithmetic with the REP clamp (the interpreter's rep_body, polar_sc_device.h
+// group_chain). group_order: per lane the totals of groups 0 .. PPW - 1 of its own row's word.
+// (templates on the group width PW = PARW, so that PAR >= 16 plans never instantiate them)
+template <int PW>
+__device__ __forceinline__ void group_order(u32 t, u32 gr, u32 *o)
+{
+    if constexpr (16 / PW == 2) {
+        const u32 p = xorlane<PW>(t);
+        o[0] = (gr & 1u) ? p : t;
+        o[1] = (gr & 1u) ? t : p;
+    } else {
+        const u32 v1 = xorlane<PW>(t), v2 = xorlane<2 * PW>(t), v3 = xorlane<PW>(v2);
+#pragma unroll
+        for (u32 k = 0; k < 4; k++) {
+            const u32 j = (gr & 3u) ^ k;
+            o[k] = j == 0 ? t : j == 1 ? v1 : j == 2 ? v2 : v3;
+        }
+    }
+}
+// one register of a node (row r = word 4 i + r), acc the same in every lane
+template <int PW = PARW>
+__device__ __forceinline__ u32 rep_groups_rows(u32 acc, u32 lam, const Lanes &ln)
+{
+    u32 o[PPW > 1 ? PPW : 1];
+    group_order<PW>(add_tree_w<PW, 1>(lam, ln), ln.pos >> LPAR, o);
+    X4 r[PPW > 1 ? PPW : 1];
+#pragma unroll
+    for (int k = 0; k < PPW; k++) r[k] = rows4(o[k]);
+#pragma unroll
+    for (int k = 0; k < PPW; k++) acc = rep_sat_add(acc, r[k].t0);
+#pragma unroll
+    for (int k = 0; k < PPW; k++) acc = rep_sat_add(acc, r[k].t1);
+#pragma unroll
+    for (int k = 0; k < PPW; k++) acc = rep_sat_add(acc, r[k].t2);
+#pragma unroll
+    for (int k = 0; k < PPW; k++) acc = rep_sat_add(acc, r[k].t3);
+    return acc;
+}
+// a node of two words (row r holds word r & 1) / of one word (replicated in the rows)
+template <int PW = PARW>
+__device__ __forceinline__ u32 rep_groups_2(u32 lam, const Lanes &ln)
+{
+    u32 o[PPW > 1 ? PPW : 1];
+    group_order<PW>(add_tree_w<PW, 1>(lam, ln), ln.pos >> LPAR, o);
+    X2 q[PPW > 1 ? PPW : 1];
+#pragma unroll
+    for (int k = 0; k < PPW; k++) q[k] = swap16(o[k]);
+    u32 acc = 0u;
+#pragma unroll
+    for (int k = 0; k < PPW; k++) acc = rep_sat_add(acc, q[k].a);
+#pragma unroll
+    for (int k = 0; k < PPW; k++) acc = rep_sat_add(acc, q[k].b);
+    return acc;
+}
+template <int PW = PARW>
+__device__ __forceinline__ u32 rep_groups_1(u32 lam, const Lanes &ln)
+{
+    return group_chain<16 / PW>(0u, add_tree_w<PW, 1>(lam, ln), ln.pos >> LPAR);
+}
+
 // the exact SM chain (rep_any_zero fallback) over one register: SM16 per lane v (row r = word
 // 4 i + r) -> the ADD_TREE of each PAR word (PAR 64: words (0, 2), (1, 3), then the halves,
 // then the positions; PAR 32: words (0, 1), then the positions -- rep_add_tree's order),
@@ -847,6 +919,10 @@ __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int 
 #pragma unroll
         for (int o = 0; o < 2; o++) {
             const u32 lam = F_pair(prow(a, o), prow(b, o)), sg = pk_sra(lam, 15);
+            if constexpr (LPAR < 4) {   // PAR 4 / 8: the exact SM chain over the groups
+                acc = rep_groups_rows(acc, lam, c.lanes());
+                continue;
+            }
             const X4 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));
             if constexpr (PAIR_SOLO) acc = rep_acc_solo(acc, t.t0, t.t1, t.t2, t.t3);
             else acc = rep_acc_rows(acc, t.t0, t.t1, t.t2, t.t3);
@@ -854,7 +930,7 @@ __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int 
     }
     // (CA2: the exact sums of ADD_TREE_{n}_CA2 / VECTOR_ADD are this chain, and a zero total
     // decides 0: no fallback)
-    if (!CA2 && (PAIR_SOLO ? rep_any_zero_lo(acc) : rep_any_zero(acc))) {
+    if (!CA2 && LPAR >= 4 && (PAIR_SOLO ? rep_any_zero_lo(acc) : rep_any_zero(acc))) {
         const Lanes ln = c.lanes();
         acc = 0;
         for (int j = 0; j < n4; j += 2) {

@@ -44,6 +44,10 @@ struct PairGen {
     // which include the leftmost path
     bool ca2 = false, left = false;
     int q = 6, p16 = 1;
+    // PAR 4 / 8 (pw): the PAR words are lane groups of a device word; one-word leaf records
+    // decode the whole word tree (leaf_word_gen: frozen bits + group classes from reserved[1]),
+    // REP runs the exact group chains (polar_sc_pair.h rep_groups_*), SPC keys take the group
+    bool pw = false;
 
     PairGen(const std::vector<polar_sc_op> &ops_, int lg, bool solo_ = false)
         : ops(ops_), LG(lg), solo(solo_), wpr(solo_ ? 8 : 4) {}
@@ -210,14 +214,19 @@ struct PairGen {
                 o << "    FS_[" << k << "] = " << P(pd, 16 * k) << " ^ " << P(pd, n4 + 16 * k) << ";\n";
             // (solo: the words of a register in order 8 i + r, then 8 i + 4 + r, into the low half)
             const int mw = min_width(op);
-            for (int i = 0; i < n4; i++) {
+            if (pw) {
+                for (int i = 0; i < n4; i++)
+                    o << "    acc_ = rep_groups_rows(acc_, F_split_sm<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i)
+                      << ", FS_[" << i / 16 << "]), ln);\n";
+            }
+            for (int i = 0; i < n4 && !pw; i++) {
                 o << "    { const X4 t_ = rows4(row_sum_biased(" << (mw ? "F_split_biased_min<" : "F_split_biased<") << i % 16
                   << (mw ? ", " + std::to_string(mw) : std::string()) << ">(" << M(pd, i) << ", " << M(pd, n4 + i)
                   << ", FS_[" << i / 16 << "])));\n"
                   << "      acc_ = " << (solo ? "rep_acc_solo" : "rep_acc_rows") << "(acc_, t_.t0, t_.t1, t_.t2, t_.t3); }\n";
                 chunk_fence(i, n4);
             }
-            if (!ca2) {   // (CA2: the two's complement chain is exact and a zero total decides 0)
+            if (!ca2 && !pw) {   // (CA2: the two's complement chain is exact and a zero total decides 0)
                 o << "    if (" << (solo ? "rep_any_zero_lo" : "rep_any_zero") << "(acc_)) {\n      acc_ = 0u;\n";
                 for (int i = 0; i < n4; i++)
                     o << "      acc_ = " << (solo ? "rep_sm_solo" : "rep_sm_rows") << "(acc_, F_split_sm<" << i % 16 << ">("
@@ -464,7 +473,10 @@ struct PairGen {
                                          : "    const u32 M_ = pk_min(bsel(xm_, pk_abs_i16(d_), pk_add(m_.a, m_.b)), GSAT2);\n")
                   << "    const u32 S_ = plane_mask<0>(s_.b) ^ (xm_ & ~pk_sra(d_, 15));\n";
             }
-            if (ca2)
+            if (pw)
+                o << "    " << x << " = leaf_word_gen<0x" << std::hex << (op.fb & 0xFFFFu) << "u, 0x" << (uint32_t)op.reserved[1]
+                  << std::dec << "u>(M_, S_, ln);\n  }\n";
+            else if (ca2)
                 o << "    " << x << " = leaf_gen_ca2<0x" << std::hex << (op.fb & 0xFFFFu) << std::dec << "u, " << mw
                   << ">(M_, S_, ln);\n  }\n";
             else
@@ -476,8 +488,14 @@ struct PairGen {
             const std::string x = var("x");
             const int mw = min_width(op);
             o << "  u32 " << x << ";\n  { // REP n " << n << "\n    const X2 m_ = " << sw << "(" << M(pd, 0)
-              << "), s_ = " << sw << "(s" << pd << "[0]);\n    const u32 FS_ = s_.a ^ s_.b;\n"
-              << "    const u32 t_ = row_sum_biased("
+              << "), s_ = " << sw << "(s" << pd << "[0]);\n    const u32 FS_ = s_.a ^ s_.b;\n";
+            if (pw) {
+                o << "    const u32 acc_ = " << (n == 1 ? "rep_groups_1" : "rep_groups_2") << "(F_split_sm<0>(m_.a, m_.b, FS_), ln);\n"
+                  << "    " << x << " = pk_sra(acc_, 15);\n  }\n";
+                (n == 1 ? small1 : small2)[op.pos] = x;
+                break;
+            }
+            o << "    const u32 t_ = row_sum_biased("
               << (mw ? "F_split_biased_min<0, " + std::to_string(mw) + ">" : std::string("F_split_biased<0>"))
               << "(m_.a, m_.b, FS_));\n";
             // (2 words: two PAR 16 words in order, or one PAR 32 word -- rep2_acc / rep2_sm)
@@ -513,7 +531,7 @@ struct PairGen {
                   << "    u32 par_ = row_xor(h_);\n";
                 // key bits below the magnitude: bitrev4(position), and for 2 words the word
                 // (PAR 16: above it; PAR 32: below it, spc_sub2)
-                const std::string wk = n == 1 ? "ln.br" : "spc_sub2(c.row, ln)";
+                const std::string wk = n == 1 ? "spc_lk(ln)" : "spc_sub2(c.row, ln)";
                 o << "    u32 klo_ = row_min_u32(((l_ & 0xFFu) << 24) | " << wk << ");\n"
                   << "    u32 khi_ = row_min_u32((((l_ >> 16) & 0xFFu) << 24) | " << wk << ");\n";
                 if (n == 2)
@@ -756,7 +774,7 @@ std::string pair_source(const polar_sc_plan &p)
     o << "#define POLAR_LANE_REMAP 1\n" << (solo ? "#define POLAR_SOLO 1\n" : "") << (ca2 ? "#define POLAR_CA2 1\n" : "")
       << "#define POLAR_Q " << p.cfg.llr_bits
       << "\n#define POLAR_LPAR "
-      << (p.cfg.par == 64 ? 6 : p.cfg.par == 32 ? 5 : 4)
+      << (p.cfg.par == 64 ? 6 : p.cfg.par == 32 ? 5 : p.cfg.par == 16 ? 4 : p.cfg.par == 8 ? 3 : 2)
       << "\n" << (p.cfg.extended ? "" : "#define POLAR_EXT 0\n")   // EXTENDED = 0: saturating leaves
       << "#include \"polar_sc_pair.h\"\n"
       << "namespace polar {\n"
@@ -779,6 +797,7 @@ std::string pair_source(const polar_sc_plan &p)
         g.left = std::get<2>(v);
         g.q = p.cfg.llr_bits;
         g.p16 = (int)p.p16;
+        g.pw = p.ppw > 1;
         g.sub_function(std::get<0>(v), p.tune.sub_inline == 2, std::get<1>(v));
         o << g.o.str();
     }
