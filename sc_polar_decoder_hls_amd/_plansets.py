@@ -222,6 +222,19 @@ def par48_gpu_items():
         out.append(("planted16384_p%d_fused" % par, pm, P, {"kernel": 3, "layout": 1, "sub_root": 2}))
         out.append(("tier32768_p%d" % par, mask("frozen_n_32768_k_29492"), P,
                     {"kernel": 3, "layout": 1, "tier_words": 512, "sub_words": 128}))
+        # CA2: the first word informative (MIN reaches the leaf of word 0), every pruning level
+        C = dict(P, sigmag=0)
+        fm = ca2_first_mask(16384)
+        for n in ("frozen_n_2048_k_1024", "frozen_n_65536_k_32768"):
+            out.append(("%s_p%d_ca2" % (n, par), mask(n), C, None))
+        for c7 in (SHIPPED_C7, (1, 1, 1, 1, 1, 1, 0), (0, 0, 0, 0, 0, 0, 0)):
+            out.append(("first16384_p%d_ca2_pl%d" % (par, c7[0]), fm, dict(c7_fields(c7), **C), None))
+            out.append(("planted16384_p%d_ca2_pl%d" % (par, c7[0]), pm, dict(c7_fields(c7), **C), None))
+        for q in (5, 8, 9):
+            for ext in (1, 0):
+                out.append(("first16384_p%d_ca2_q%d_e%d" % (par, q, ext), fm, dict(C, llr_bits=q, extended=ext), None))
+        out.append(("first2048_p%d_ca2_s32" % par, ca2_first_mask(2048), C, {"kernel": 3, "layout": 1, "sub_words": 32}))
+        out.append(("first16384_p%d_ca2_fused" % par, fm, C, {"kernel": 3, "layout": 1, "sub_root": 2}))
     return out
 
 

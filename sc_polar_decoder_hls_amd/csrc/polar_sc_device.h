@@ -1131,10 +1131,14 @@ __device__ __forceinline__ u32 word_gen(u32 L, const Lanes &ln)
     const u32 xbp = xorlane<H>(xb);
     return bsel(ln.template amask<H>(), lz ? xbp : (xa ^ xbp), xb);
 }
-// a PAR 4 / 8 leaf record of the generated kernels on split operands: 16-bit masks like leaf_ms
+// a PAR 4 / 8 leaf record of the generated kernels on split operands (S: 16-bit sign masks):
+// 16-bit masks like leaf_ms. CA2: the word tree runs on the two's complement values, which the
+// split form gives back exactly (a zero's sign is don't-care: (0 ^ S) - S = 0; MIN = magnitude
+// 2^(w-1) with the sign set -> -2^(w-1))
 template <u32 FB, u32 INFO>
 __device__ __forceinline__ u32 leaf_word_gen(u32 M, u32 S, const Lanes &ln)
 {
-    return pk_sra(word_gen<0, 16, FB, INFO>(M | (S & SGN), ln), 15);
+    if constexpr (CA2) return pk_sra(word_gen<0, 16, FB, INFO>(pk_sub(M ^ S, S), ln), 15);
+    else return pk_sra(word_gen<0, 16, FB, INFO>(M | (S & SGN), ln), 15);
 }
 }  // namespace polar

@@ -877,8 +877,13 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     for (const polar_sc_op &o : p->ops)
         if ((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && ((o.fb >> 16) & 7u) != 0u) leaf_kinds = true;
     const bool pair_par = c.par == 16 || c.par == 32 || c.par == 64;
-    const bool pair_fmt = dflt || ((pair_par || c.par == 4 || c.par == 8) && c.sigmag == 1 && c.llr_bits <= 9) ||
-                          (pair_par && c.sigmag == 0 && !leaf_kinds && c.llr_bits <= 9 && !(c.llr_bits == 9 && c.par == 64));
+    // (CA2 at PAR 4 / 8 too: the word trees on two's complement values, every PRUNING_LEVEL --
+    // their PR1 leaves, the CA2 R1 decoder included, are the word tree's; ppw > 1 leaf records
+    // carry no kind bits)
+    const bool par48 = c.par == 4 || c.par == 8;
+    const bool pair_fmt = dflt || ((pair_par || par48) && c.sigmag == 1 && c.llr_bits <= 9) ||
+                          ((pair_par || par48) && c.sigmag == 0 && !leaf_kinds && c.llr_bits <= 9 &&
+                           !(c.llr_bits == 9 && c.par == 64));
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR
     // level's F / G / H then run inside the straight-line code instead of as interpreter ops

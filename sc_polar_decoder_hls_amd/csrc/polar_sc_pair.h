@@ -190,6 +190,23 @@ __device__ __forceinline__ void group_order(u32 t, u32 gr, u32 *o)
         }
     }
 }
+// the REP input of one register: F of the split operands as the word trees take it -- SM16, or
+// (CA2) two's complement, with the key min and the MIN sign (MW > 0) on the leftmost path
+template <int I, int MW>
+__device__ __forceinline__ u32 F_split_rep(u32 ma, u32 mb, u32 FS)
+{
+    if constexpr (CA2) {
+        if constexpr (MW > 0) {
+            const u32 m = pk_min_key<MW>(ma, mb), sg = plane_mask<I>(FS) | pk_sra(ca2_minbit<MW>(m), 15);
+            return pk_sub(m ^ sg, sg);
+        } else {
+            const u32 m = pk_min(ma, mb), sg = plane_mask<I>(FS);
+            return pk_sub(m ^ sg, sg);
+        }
+    } else {
+        return F_split_sm<I>(ma, mb, FS);
+    }
+}
 // one register of a node (row r = word 4 i + r), acc the same in every lane
 template <int PW = PARW>
 __device__ __forceinline__ u32 rep_groups_rows(u32 acc, u32 lam, const Lanes &ln)
@@ -919,8 +936,8 @@ __device__ __forceinline__ void prep_body(const PairCtx &c, int s0, int n4, int 
 #pragma unroll
         for (int o = 0; o < 2; o++) {
             const u32 lam = F_pair(prow(a, o), prow(b, o)), sg = pk_sra(lam, 15);
-            if constexpr (LPAR < 4) {   // PAR 4 / 8: the exact SM chain over the groups
-                acc = rep_groups_rows(acc, lam, c.lanes());
+            if constexpr (LPAR < 4) {   // PAR 4 / 8: the exact chain over the groups (SM / CA2)
+                acc = rep_groups_rows(acc, CA2 ? pk_sub((lam & MAG) ^ sg, sg) : lam, c.lanes());
                 continue;
             }
             const X4 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200u)));

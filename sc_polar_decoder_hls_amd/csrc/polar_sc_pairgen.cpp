@@ -216,8 +216,8 @@ struct PairGen {
             const int mw = min_width(op);
             if (pw) {
                 for (int i = 0; i < n4; i++)
-                    o << "    acc_ = rep_groups_rows(acc_, F_split_sm<" << i % 16 << ">(" << M(pd, i) << ", " << M(pd, n4 + i)
-                      << ", FS_[" << i / 16 << "]), ln);\n";
+                    o << "    acc_ = rep_groups_rows(acc_, F_split_rep<" << i % 16 << ", " << mw << ">(" << M(pd, i) << ", "
+                      << M(pd, n4 + i) << ", FS_[" << i / 16 << "]), ln);\n";
             }
             for (int i = 0; i < n4 && !pw; i++) {
                 o << "    { const X4 t_ = rows4(row_sum_biased(" << (mw ? "F_split_biased_min<" : "F_split_biased<") << i % 16
@@ -490,7 +490,8 @@ struct PairGen {
             o << "  u32 " << x << ";\n  { // REP n " << n << "\n    const X2 m_ = " << sw << "(" << M(pd, 0)
               << "), s_ = " << sw << "(s" << pd << "[0]);\n    const u32 FS_ = s_.a ^ s_.b;\n";
             if (pw) {
-                o << "    const u32 acc_ = " << (n == 1 ? "rep_groups_1" : "rep_groups_2") << "(F_split_sm<0>(m_.a, m_.b, FS_), ln);\n"
+                o << "    const u32 acc_ = " << (n == 1 ? "rep_groups_1" : "rep_groups_2") << "(F_split_rep<0, " << mw
+                  << ">(m_.a, m_.b, FS_), ln);\n"
                   << "    " << x << " = pk_sra(acc_, 15);\n  }\n";
                 (n == 1 ? small1 : small2)[op.pos] = x;
                 break;

@@ -9,7 +9,9 @@ bitrev_{PAR}(position)) (spc_lane_key).
 
 CPU: plan selection and the generated source. GPU: bit-exact with the literal FSM at PAR 4 / 8
 on reference, planted (every pruned group class) and structured masks, AWGN and edge LLRs,
-PRUNING_LEVEL 0 / 1 / 2, EXTENDED 0 / 1, LLR_BITS 6 / 8 / 9."""
+PRUNING_LEVEL 0 / 1 / 2, EXTENDED 0 / 1, LLR_BITS 5 .. 9, SIGMAG and CA2 (the word trees on
+two's complement values converted from the split form; MIN on the leftmost path reaches the leaf
+of word 0 through the key-min F of the _L decoder)."""
 import numpy as np
 import pytest
 
@@ -33,8 +35,12 @@ def test_par48_plans_take_the_pair_kernel(pkg):
                 for pl in (0, 1, 2):
                     d = pkg.Decoder(m, config=cfg(pkg, par=par, llr_bits=q, extended=ext, pruning_level=pl))
                     assert d.stats["kernel"] == 3, (par, q, ext, pl, d.stats["kernel"])
-        # CA2 at PAR 4 / 8 stays on the interpreter (no CA2 word tree in the generated code)
-        assert pkg.Decoder(m, config=cfg(pkg, par=par, sigmag=0)).stats["kernel"] != 3
+            # CA2: the word trees on two's complement values, every pruning level
+            for pl in (0, 1, 2):
+                d = pkg.Decoder(m, config=cfg(pkg, par=par, llr_bits=q, sigmag=0, pruning_level=pl))
+                assert d.stats["kernel"] == 3, (par, q, "ca2", pl, d.stats["kernel"])
+        src = pkg.Decoder(m, config=cfg(pkg, par=par, sigmag=0)).kernel_source()
+        assert "#define POLAR_CA2 1" in src and "polar_psub_0_L(" in src and "F_split_rep<" in src
         src = pkg.Decoder(m, config=cfg(pkg, par=par)).kernel_source()
         assert "#define POLAR_LPAR %d" % (2 if par == 4 else 3) in src
         assert "leaf_word_gen<" in src and "leaf_gen<" not in src
@@ -76,6 +82,7 @@ def frames(mask, q, n_awgn, n_edge, seed):
     e = rng.integers(-(amp + 1), amp + 1, size=(n_edge, mask.size))
     e[:, rng.integers(0, mask.size, mask.size // 8)] = -(amp + 1)
     e[:, rng.integers(0, mask.size, mask.size // 8)] = 0
+    e[0, :64] = -(amp + 1)                        # (CA2: MIN on the leftmost path)
     llr = np.concatenate([awgn, e])
     return llr.astype(np.int16 if q > 8 else np.int8)
 
@@ -92,7 +99,7 @@ def test_par48_pair_kernel_gpu(pkg, cuda, oracle_mod, item):
     out = dec.decode(cuda.from_numpy(llr).cuda())
     cuda.cuda.synchronize()
     c7 = (c.pruning_level, c.elag_r1, c.elag_rep, c.elag_spc, c.elag_rep2, c.elag_spc2, c.elag_h0)
-    ref = oracle_mod.decode_fsm(mask, llr, config=c7, llr_bits=q, par=c.par, sigmag=1, extended=c.extended)
+    ref = oracle_mod.decode_fsm(mask, llr, config=c7, llr_bits=q, par=c.par, sigmag=c.sigmag, extended=c.extended)
     _assert_same(pkg.unpack_bits(out.cpu().numpy(), mask.size), ref, "PAR %d %s" % (c.par, name))
 
 
