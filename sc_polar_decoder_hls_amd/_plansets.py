@@ -189,6 +189,18 @@ def ca2_gpu_items():
             for ext in (1, 0):
                 out.append(("first16384_p%d_q%d_e%d" % (par, q, ext), fm, {"par": par, "llr_bits": q, "extended": ext}, None))
     out.append(("first16384_pl0", fm, {"pruning_level": 0}, None))
+    # PRUNING_LEVEL 1 at PAR 16: the leaf records' REP / SPC / REP2 / SPC2 / R1 decoders
+    for c7 in PRUNING_SWEEP:
+        if c7[0] == 1:
+            out.append(("first16384_pl1_%s" % "".join(map(str, c7[1:])), fm, c7_fields(c7), None))
+    out.append(("first2048_pl1_q8_e0", ca2_first_mask(2048), dict(c7_fields((1, 1, 1, 1, 1, 1, 0)), llr_bits=8,
+                                                                   extended=0), None))
+    # ... and at PAR 32 / 64: the decoders of the whole PAR word (OP_PLEAF)
+    for par in (32, 64):
+        for c7 in ((1, 1, 0, 0, 0, 0, 0), (1, 1, 1, 1, 0, 0, 0), (1, 1, 1, 1, 1, 1, 0)):
+            out.append(("first16384_p%d_pl1_%s" % (par, "".join(map(str, c7[1:]))), fm, dict(c7_fields(c7), par=par), None))
+        out.append(("first16384_p%d_pl1_q8_e0" % par, fm, dict(c7_fields((1, 1, 1, 1, 1, 1, 0)), par=par, llr_bits=8,
+                                                             extended=0), None))
     out.append(("first2048_p64_pl0", ca2_first_mask(2048), {"par": 64, "pruning_level": 0}, None))
     for wpg in (1, 2, 4, 8):
         out.append(("wave_mask_w%d" % wpg, wave_mask(), {}, {"kernel": 3, "layout": 1, "waves_per_group": wpg, "sub_words": 64}))
@@ -327,7 +339,7 @@ def sweep_items():
         out += [("planted%d" % N, sweep_planted_mask(N), c7_fields(c7), None) for N in PLANTED_N]
     # script_tests.sh:105-106's loop at PAR 16, QUANT 8 on the default (pair) kernel
     out += [("frozen_n_32768_k_29492", mask("frozen_n_32768_k_29492"), dict(c7_fields(c7), llr_bits=8, par=par), None)
-            for c7 in PRUNING_SWEEP for par in (16, 8, 4)]
+            for c7 in PRUNING_SWEEP for par in (16, 64, 32, 8, 4)]
     for q in (5, 7, 8):
         for c7 in (SHIPPED_C7, (1, 1, 1, 1, 1, 1, 0)):
             out += [(n, mask(n), dict(c7_fields(c7), llr_bits=q), None) for n in QBITS_MASKS]

@@ -678,12 +678,6 @@ __device__ __forceinline__ u32 leaf_ca2(u32 M, u32 S, const Lanes &ln)
         return bselo(ln.template amask<H>(), xa ^ xorlane<H>(xb), xb);
     }
 }
-template <u32 FB, int MW>
-__device__ __forceinline__ u32 leaf_gen_ca2(u32 M, u32 S, const Lanes &ln)
-{
-    static_assert(((FB >> 16) & 7u) == 0u, "CA2 pair plans: plain leaves only");
-    return leaf_ca2<FB & 0xFFFFu, 0, 16, MW>(M, S, ln);
-}
 
 // ---------------------------------------------------------------------------------------
 // REP nodes (Spec_REP, functions.h:3086-3107) -- value path. The reference decision is the
@@ -1140,5 +1134,15 @@ __device__ __forceinline__ u32 leaf_word_gen(u32 M, u32 S, const Lanes &ln)
 {
     if constexpr (CA2) return pk_sra(word_gen<0, 16, FB, INFO>(pk_sub(M ^ S, S), ln), 15);
     else return pk_sra(word_gen<0, 16, FB, INFO>(M | (S & SGN), ln), 15);
+}
+// A CA2 leaf record of the generated kernels: leaf_ca2, or its PRUNING_LEVEL 1 decoder (fb bits
+// 16..18: REP / SPC / REP2 / SPC2 / R1, the interpreter's leaf_kind_w on the two's complement
+// word; the split form gives it back exactly, MIN included)
+template <u32 FB, int MW>
+__device__ __forceinline__ u32 leaf_gen_ca2(u32 M, u32 S, const Lanes &ln)
+{
+    constexpr u32 KIND = (FB >> 16) & 7u;
+    if constexpr (KIND == 0) return leaf_ca2<FB & 0xFFFFu, 0, 16, MW>(M, S, ln);
+    else return pk_sra(leaf_kind_w<16>(pk_sub(M ^ S, S), KIND, ln, QB), 15);
 }
 }  // namespace polar

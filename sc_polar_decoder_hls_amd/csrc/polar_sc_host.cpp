@@ -873,16 +873,17 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // and PAR 4 / 8 SIGMAG (the PAR words = lane groups of a device word: every one-word leaf
     // record decodes its whole word tree with the frozen bits and group classes as template
     // constants, polar_sc_device.h word_gen; REP over the groups, polar_sc_pair.h rep_groups_*)
-    bool leaf_kinds = false;
-    for (const polar_sc_op &o : p->ops)
-        if ((o.code == POLAR_OP_FLEAF || o.code == POLAR_OP_GLEAF) && ((o.fb >> 16) & 7u) != 0u) leaf_kinds = true;
+    // (and PRUNING_LEVEL 1 everywhere: the 16-LLR leaf records' REP / SPC / REP2 / SPC2 / R1
+    // decoders, in CA2 on the two's complement word (leaf_gen_ca2), and at PAR 32 / 64 the
+    // decoders of the whole PAR word, OP_PLEAF records after its F / G: polar_sc_pair.h
+    // pleaf_pair, the interpreter's op_pleaf on the pair layout)
     const bool pair_par = c.par == 16 || c.par == 32 || c.par == 64;
     // (CA2 at PAR 4 / 8 too: the word trees on two's complement values, every PRUNING_LEVEL --
     // their PR1 leaves, the CA2 R1 decoder included, are the word tree's; ppw > 1 leaf records
     // carry no kind bits)
     const bool par48 = c.par == 4 || c.par == 8;
     const bool pair_fmt = dflt || ((pair_par || par48) && c.sigmag == 1 && c.llr_bits <= 9) ||
-                          ((pair_par || par48) && c.sigmag == 0 && !leaf_kinds && c.llr_bits <= 9 &&
+                          ((pair_par || par48) && c.sigmag == 0 && c.llr_bits <= 9 &&
                            !(c.llr_bits == 9 && c.par == 64));
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR
@@ -899,7 +900,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // groups, tools/pair_ab.py: C3 1.64 -> 1.16 ms, C5 4.18 -> 1.78, C5 at 64 frames 3.57 ->
     // 1.55, N = 16384 x 4096 frames 0.39 -> 0.24, N = 4096 x 16384 0.36 -> 0.23);
     // polar_sc_tuning.kernel = 2 keeps the hybrid kernel
-    const bool want_pair = !p->jit && jit_on && !kinds && pair_fmt && p->G >= 128 && (t.kernel == 3 || t.kernel == 0);
+    const bool want_pair = !p->jit && jit_on && pair_fmt && p->G >= 128 && (t.kernel == 3 || t.kernel == 0);
     // an explicit kernel / subtree size that cannot be honoured is an error, not a silent
     // fallback to another kernel (A/B measurements force them)
     if ((t.kernel == 3 && !want_pair) ||

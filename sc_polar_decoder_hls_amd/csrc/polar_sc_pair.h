@@ -190,6 +190,84 @@ __device__ __forceinline__ void group_order(u32 t, u32 gr, u32 *o)
         }
     }
 }
+// PAR 32 / 64 at PRUNING_LEVEL 1 (OP_PLEAF): the leaf decoder of the PAR word held by one
+// register (PAR 64: row r = word r) or by a two-word node (PAR 32: row r = word r & 1) --
+// R1 (5) / REP (1) / SPC (2) / REP2 (3) / SPC2 (4), R_STATE (my_module.h:566-593;
+// library.h:187-280) as the interpreter's op_pleaf computes it: the word pair trees first
+// (PAR 64: words (0, 2), (1, 3), then the halves; exact SM or CA2 sums), then the lane tree;
+// SPC keys (|lambda|, bitrev_{LPAR}(16 j + position)). v: the SM16 / two's complement word
+// per lane; returns sign-position flags.
+template <int KIND>
+__device__ __forceinline__ u32 pleaf_pair(u32 v, const Lanes &ln, u32 row)
+{
+    if constexpr (KIND == 5) {
+        return v & SGN;
+    } else if constexpr (KIND == 1 || KIND == 3) {
+        u32 t = v;
+        if constexpr (PAIR_P64) {
+            const X2 q = swap32(t);
+            t = CA2 ? pk_add(q.a, q.b) : G_sm<0>(q.a, q.b, 0u);
+        }
+        {
+            const X2 q = swap16(t);
+            t = CA2 ? pk_add(q.a, q.b) : G_sm<0>(q.a, q.b, 0u);
+        }
+        if constexpr (CA2) {
+            t = pk_add(t, xorlane<8>(t));
+            t = pk_add(t, xorlane<4>(t));
+            t = pk_add(t, xorlane<2>(t));
+            if constexpr (KIND == 1) t = pk_add(t, xorlane<1>(t));
+            return t & SGN;
+        } else if constexpr (KIND == 1) {
+            return leaf_rep(t, ln);
+        } else {
+            return leaf_rep2(t, ln);
+        }
+    } else {
+        constexpr bool spc2 = KIND == 4;
+        u32 par = v & SGN;
+        if constexpr (PAIR_P64) {
+            const X2 q = swap32(par);
+            par = q.a ^ q.b;
+        }
+        {
+            const X2 q = swap16(par);
+            par = q.a ^ q.b;
+        }
+        par ^= xorlane<8>(par);
+        par ^= xorlane<4>(par);
+        par ^= xorlane<2>(par);
+        if constexpr (!spc2) par ^= xorlane<1>(par);
+        const u32 mg = CA2 ? pk_add(ca2_qabs(v, QB), (1u << (QB - 1)) * 0x00010001u) : (v & MAG);
+        const u32 wk = (ln.br << (LPAR - 4)) | bitrev_n(PAIR_P64 ? row : (row & 1u), LPAR - 4);
+        const u32 mlo = ((mg & 0xFFFFu) << 8) | wk, mhi = ((mg >> 16) << 8) | wk;
+        u32 klo = mlo, khi = mhi;
+        if constexpr (PAIR_P64) {
+            const X2 a = swap32(klo), b = swap32(khi);
+            klo = __builtin_elementwise_min(a.a, a.b);
+            khi = __builtin_elementwise_min(b.a, b.b);
+        }
+        {
+            const X2 a = swap16(klo), b = swap16(khi);
+            klo = __builtin_elementwise_min(a.a, a.b);
+            khi = __builtin_elementwise_min(b.a, b.b);
+        }
+        klo = __builtin_elementwise_min(klo, xorlane<8>(klo));
+        khi = __builtin_elementwise_min(khi, xorlane<8>(khi));
+        klo = __builtin_elementwise_min(klo, xorlane<4>(klo));
+        khi = __builtin_elementwise_min(khi, xorlane<4>(khi));
+        klo = __builtin_elementwise_min(klo, xorlane<2>(klo));
+        khi = __builtin_elementwise_min(khi, xorlane<2>(khi));
+        if constexpr (!spc2) {
+            klo = __builtin_elementwise_min(klo, xorlane<1>(klo));
+            khi = __builtin_elementwise_min(khi, xorlane<1>(khi));
+        }
+        const u32 flo = klo == mlo ? (par & 0x8000u) : 0u;
+        const u32 fhi = khi == mhi ? (par & 0x80000000u) : 0u;
+        return (v & SGN) ^ flo ^ fhi;
+    }
+}
+
 // the REP input of one register: F of the split operands as the word trees take it -- SM16, or
 // (CA2) two's complement, with the key min and the MIN sign (MW > 0) on the leftmost path
 template <int I, int MW>

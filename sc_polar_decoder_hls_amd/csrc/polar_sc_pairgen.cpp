@@ -477,7 +477,7 @@ struct PairGen {
                 o << "    " << x << " = leaf_word_gen<0x" << std::hex << (op.fb & 0xFFFFu) << "u, 0x" << (uint32_t)op.reserved[1]
                   << std::dec << "u>(M_, S_, ln);\n  }\n";
             else if (ca2)
-                o << "    " << x << " = leaf_gen_ca2<0x" << std::hex << (op.fb & 0xFFFFu) << std::dec << "u, " << mw
+                o << "    " << x << " = leaf_gen_ca2<0x" << std::hex << (op.fb & 0x7FFFFu) << std::dec << "u, " << mw
                   << ">(M_, S_, ln);\n  }\n";
             else
                 o << "    " << x << " = leaf_gen<0x" << std::hex << (op.fb & 0x7FFFFu) << std::dec << "u>(M_, S_, ln);\n  }\n";
@@ -579,10 +579,28 @@ struct PairGen {
         }
     }
 
+    // PAR 32 / 64, PRUNING_LEVEL 1: the leaf decoder of the PAR word the previous F / G wrote
+    // (this record's own node, 2 / 4 words: polar_sc_pair.h pleaf_pair)
+    void pleaf_op(const polar_sc_op &op, int pd)
+    {
+        const unsigned kind = (op.fb >> 16) & 7u;
+        const std::string x = var("x"), mp = M(pd, 0);
+        o << "  u32 " << x << ";\n  { // PLEAF n " << op.n << " kind " << kind << "\n    const u32 sm_ = plane_mask<0>(s" << pd
+          << "[0]);\n    " << x << " = pk_sra(pleaf_pair<" << kind << ">("
+          << (ca2 ? "pk_sub(" + mp + " ^ sm_, sm_)" : mp + " | (sm_ & SGN)") << ", ln, c.row), 15);\n  }\n";
+        if (op.n == 2) small2[op.pos] = x;
+        else if (op.n == wpr) put_mask(op.pos / wpr, 1, x);
+        else throw std::runtime_error("pairgen: PLEAF of an unexpected size");
+    }
+
     void op(const polar_sc_op &op)
     {
         const int pd = LG - op.level, cd = pd - 1;
         fence();
+        if (op.code == POLAR_OP_PLEAF) {
+            pleaf_op(op, pd);
+            return;
+        }
         if (op.code == POLAR_OP_H || op.code == POLAR_OP_H0) {
             // H of a node of 2n words: small when the node is 2 or 4 words
             if (op.n <= 2) small_op(op, pd, cd);

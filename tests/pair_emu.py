@@ -280,6 +280,11 @@ def rep_sm_rows(acc, v, ln):
     return acc
 
 
+def spc_lk(ln):
+    """polar_sc_pair.h spc_lk at PAR >= 16: bitrev4(position)"""
+    return ln.br
+
+
 def spc_sub2(row, ln):
     """two-word nodes, PAR 16: (row & 1, bitrev4(position))"""
     return ((V(row) & 1) << 4) | ln.br

@@ -48,13 +48,13 @@ def test_formats_vs_oracle(pkg, cuda, oracle_mod, fmt):
             _assert_same(got, ref, "%s fmt %s cfg %s storage %d" % (name, fmt, c7, dec.stats["storage"]))
             if par == 16 and sigmag == 1 and q <= 8:   # EXTENDED 0: the generated kernels
                 assert dec.stats["kernel"] in (1, 3), (name, fmt, c7, dec.stats["kernel"])
-            if par in (32, 64) and sigmag == 1 and c7[0] != 1 and mask.size >= 2048:
+            if par in (32, 64) and sigmag == 1 and mask.size >= 2048:
                 assert dec.stats["kernel"] == 3, (name, fmt, c7, dec.stats["kernel"])   # the pair kernel
             if par == 16 and sigmag == 1 and q == 9 and mask.size >= 2048:   # 16-bit slots
                 assert dec.stats["kernel"] == 3, (name, fmt, c7, dec.stats["kernel"])
             if par in (4, 8) and mask.size >= 2048:   # PAR words as lane groups (SIGMAG, CA2)
                 assert dec.stats["kernel"] == 3, (name, fmt, c7, dec.stats["kernel"])
-            if sigmag == 0 and par >= 16 and c7[0] != 1 and mask.size >= 2048 and not (q == 9 and par == 64):
+            if sigmag == 0 and par >= 16 and mask.size >= 2048 and not (q == 9 and par == 64):
                 assert dec.stats["kernel"] == 3, (name, fmt, c7, dec.stats["kernel"])   # CA2 on the pair kernel
 
 
@@ -160,12 +160,13 @@ def test_script_tests_pruning_sweep(pkg, cuda, oracle_mod, par):
         _assert_same(got, oracle_mod.decode_fsm(mask, llr, config=c7, llr_bits=8, par=par), "PAR %d %s" % (par, c7))
 
 
-@pytest.mark.parametrize("par", [16, 8, 4])
+@pytest.mark.parametrize("par", [16, 64, 32, 8, 4])
 def test_script_tests_pruning_sweep_pair_kernel(pkg, cuda, oracle_mod, par):
     """The same loop on the kernel the plans select by default: the generated pair kernel for
-    every configuration, PRUNING_LEVEL 1's REP / SPC / REP2 / SPC2 leaves included (PAR 8 / 4:
-    the word trees of the leaf records with their group classes as template constants,
-    polar_sc_device.h word_gen)."""
+    every configuration, PRUNING_LEVEL 1's REP / SPC / REP2 / SPC2 leaves included (PAR 64 / 32:
+    the decoders of the whole PAR word, polar_sc_pair.h pleaf_pair; PAR 8 / 4: the word trees
+    of the leaf records with their group classes as template constants, polar_sc_device.h
+    word_gen)."""
     mask = util.mask("frozen_n_32768_k_29492")
     awgn, _ = util.synth_frames(mask, 8, ebn0_db=3.5, seed=16)
     llr = np.clip(awgn.astype(np.int32) * 4, -127, 127).astype(np.int8)

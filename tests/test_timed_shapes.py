@@ -18,8 +18,12 @@ from test_gpu_parity import _assert_same
 # (mask, frames per GPU, layout, waves per block of the launch): C3 decodes in the frame-pair
 # layout (one block per pair), C5 in the solo layout (one block per frame, subtrees of 512
 # words) -- the automatic layout's choice for those batches on a 256-CU MI355X
+# (+ the automatic layout's crossover, DESIGN.md 3.2.2 "The switch point, measured": 2048 frames
+# of N = 65536 are the last batch in the solo layout, 3072 the first back in the pair layout, at
+# one wave per pair so that the 1536 pairs stay one dispatch round)
 SHAPES = [("frozen_n_65536_k_32768", 4096, 1, 1), ("frozen_n_262144_k_131072", 512, 2, 4),
-          ("frozen_n_262144_k_131072", 64, 2, 8)]
+          ("frozen_n_262144_k_131072", 64, 2, 8), ("frozen_n_65536_k_32768", 2048, 2, 1),
+          ("frozen_n_65536_k_32768", 3072, 1, 1)]
 
 
 def noiseless_batch(torch, mask, batch, seed):
@@ -63,7 +67,7 @@ def test_timed_shape_full_batch(pkg, cuda, oracle_mod, name, batch, layout, W):
     # the code object build() prewarmed (the ROCm clang driver's), not a hipRTC rebuild on this
     # machine (a cache-key mismatch once made every timed kernel hipRTC code)
     assert info["compiler"] == 1, info
-    if W == 1:
+    if W == 1 and layout == 1:
         # C3: the subtrees' parent level in LDS (the roots are read as F / G of it), F-descent
         # chains in the generated kernel
         S = dec.stats["sub_words"]

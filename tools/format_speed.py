@@ -23,6 +23,11 @@ def formats():
     out = [dict(par=16, sigmag=1, extended=1, llr_bits=6)]
     out += [dict(par=p, sigmag=s, extended=e, llr_bits=q) for p, s, e, q in _plansets.FORMATS]
     out += [dict(par=16, sigmag=1, extended=1, llr_bits=6, pruning_level=lvl) for lvl in (1, 0)]
+    # PRUNING_LEVEL 1 with every leaf decoder (the format matrix's configuration): PAR 64 / 32
+    # (PAR-word decoders) and CA2 at PAR 16 / 64 (round 6: on the pair kernel)
+    pl1 = dict(zip(("pruning_level", "elag_r1", "elag_rep", "elag_spc", "elag_rep2", "elag_spc2", "elag_h0"),
+                   (1, 1, 1, 1, 1, 1, 0)))
+    out += [dict(pl1, par=p, sigmag=sg, extended=1, llr_bits=6) for p, sg in ((16, 1), (64, 1), (32, 1), (16, 0), (64, 0))]
     return out
 
 
@@ -33,6 +38,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--formats", default="",
                     help="only these formats: 'par,sigmag,extended,llr_bits;...' (the shipped one is always first)")
+    ap.add_argument("--pl1-only", action="store_true", help="only the PRUNING_LEVEL 1 entries (and the shipped one)")
     args = ap.parse_args()
     import torch
     import sc_polar_decoder_hls_amd as pkg
@@ -45,6 +51,8 @@ def main():
     if args.formats:
         keep = [tuple(int(x) for x in f.split(",")) for f in args.formats.split(";")]
         fmts = [fmts[0]] + [dict(par=p, sigmag=sg, extended=e, llr_bits=q) for p, sg, e, q in keep]
+    if args.pl1_only:
+        fmts = [fmts[0]] + [f for f in fmts if f.get("elag_rep2")]
     for fmt in fmts:
         cfg = pkg.default_config()
         for k, v in fmt.items():
