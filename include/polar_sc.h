@@ -44,9 +44,9 @@ extern "C" {
  *   * extended 1/0 (config.h:14: exact or saturating leaves);
  *   * par 4, 8, 16, 32 or 64 (script_tests.sh:11 runs 16 and 64, script_RTL_sim.sh 4..64).
  * The shipped datapath (sigmag 1, par 16, llr_bits <= 8; either extended, every pruning level
- * and elag combination) runs the generated kernels, and so do PAR 32 and 64 (sigmag 1,
- * either extended, llr_bits <= 8, pruning_level 0 / 2) for N >= 2048; every other format runs the schedule
- * interpreter compiled for it. elag_rare = 1
+ * and elag combination) runs the generated kernels; for N >= 2048 so does every other format
+ * (the pair kernel: par 4 .. 64, sigmag 0 / 1, llr_bits 5..9, every pruning level) except CA2
+ * at llr_bits 9 with par 64; the rest runs the schedule interpreter compiled for it. elag_rare = 1
  * (does not compile in the reference, my_module.h:255 vs :1511) is rejected with -ENOTSUP.
  */
 typedef struct polar_sc_config {
@@ -242,7 +242,8 @@ int polar_sc_decode_u16(const polar_sc_plan *plan, const int8_t *llr_dev, uint16
 
 /* Same as polar_sc_decode with int16 channel values ([batch][N] int16, the low llr_bits of
  * each are the LLR): the channel for 9-bit LLRs beyond the int8 range (LLR_BITS 9,
- * script/parser_comp.sh:12). Runs the schedule interpreter of the plan's format. */
+ * script/parser_comp.sh:12). Pair plans of 9-bit LLRs (N >= 2048) read the int16 frames
+ * directly; other plans run the schedule interpreter of the plan's format. */
 int polar_sc_decode_i16(const polar_sc_plan *plan, const int16_t *llr_dev, uint64_t *hard_bits_dev,
                         size_t batch, void *stream);
 

@@ -745,16 +745,41 @@ uint64_t code_key(const polar_sc_plan &p)
 }
 
 namespace {
-// cache entries: <key>.coz = "PSCZ" + the object's size (u64, little endian) + the object
-// deflated by zlib (code objects compress ~2.1x: the prewarmed set that travels with the library
-// to every GPU box is ~70 MB instead of ~150); a plain <key>.co (older caches) still loads
+// cache entries: <key>.cox = "PSCX" + the object's size (u64, little endian) + the object as
+// an xz stream (the generated code is 8-bit instruction encodings that LZMA packs ~5x against
+// zlib's ~2x: the prewarmed set that travels with the library to every GPU box is ~70 MB
+// instead of ~175). liblzma comes from the image (liblzma.so.5, no header there): its two
+// stable buffer functions through dlopen. Without it entries are stored as <key>.coz = "PSCZ"
+// + size + zlib deflate; both, and a plain <key>.co, still load.
 std::string cache_path(const std::string &src, bool rtc = true)
 {
     const std::string dir = cache_dir();
     if (dir.empty()) return "";
     char name[40];
-    std::snprintf(name, sizeof name, "/%016llx.coz", (unsigned long long)source_key(src, rtc));
+    std::snprintf(name, sizeof name, "/%016llx.cox", (unsigned long long)source_key(src, rtc));
     return dir + name;
+}
+
+struct Lzma {
+    // lzma_easy_buffer_encode / lzma_stream_buffer_decode (lzma/container.h); lzma_ret 0 = LZMA_OK
+    typedef int (*enc_t)(uint32_t preset, int check, const void *allocator, const uint8_t *in, size_t in_size,
+                         uint8_t *out, size_t *out_pos, size_t out_size);
+    typedef int (*dec_t)(uint64_t *memlimit, uint32_t flags, const void *allocator, const uint8_t *in, size_t *in_pos,
+                         size_t in_size, uint8_t *out, size_t *out_pos, size_t out_size);
+    enc_t enc = nullptr;
+    dec_t dec = nullptr;
+    Lzma()
+    {
+        if (void *h = dlopen("liblzma.so.5", RTLD_NOW | RTLD_LOCAL)) {
+            enc = (enc_t)dlsym(h, "lzma_easy_buffer_encode");
+            dec = (dec_t)dlsym(h, "lzma_stream_buffer_decode");
+        }
+    }
+};
+const Lzma &lzma_lib()
+{
+    static const Lzma l;
+    return l;
 }
 
 bool read_all(const std::string &path, std::vector<char> &buf)
@@ -769,20 +794,37 @@ bool cache_load(const std::string &path, std::vector<char> &code)
 {
     if (path.empty()) return false;
     std::vector<char> buf;
-    std::string used = path;
-    if (read_all(path, buf) && buf.size() > 12 && std::memcmp(buf.data(), "PSCZ", 4) == 0) {
-        uint64_t n = 0;
+    std::string used = path;   // <key>.cox
+    bool ok = false;
+    if (read_all(path, buf) && buf.size() > 12 && std::memcmp(buf.data(), "PSCX", 4) == 0 && lzma_lib().dec) {
+        uint64_t n = 0, memlimit = ~0ull;
         std::memcpy(&n, buf.data() + 4, 8);
         if (n < 4 || n > (1ull << 32)) return false;
         std::vector<char> out(n);
-        uLongf len = (uLongf)n;
-        if (uncompress((Bytef *)out.data(), &len, (const Bytef *)buf.data() + 12, (uLong)(buf.size() - 12)) != Z_OK ||
-            len != n)
+        size_t in_pos = 0, out_pos = 0;
+        if (lzma_lib().dec(&memlimit, 0u, nullptr, (const uint8_t *)buf.data() + 12, &in_pos, buf.size() - 12,
+                           (uint8_t *)out.data(), &out_pos, (size_t)n) != 0 ||
+            out_pos != n)
             return false;
         buf.swap(out);
-    } else {
-        used = path.substr(0, path.size() - 1);   // <key>.co: an uncompressed entry
-        if (!read_all(used, buf)) return false;
+        ok = true;
+    }
+    if (!ok) {
+        used = path.substr(0, path.size() - 1) + "z";   // <key>.coz
+        if (read_all(used, buf) && buf.size() > 12 && std::memcmp(buf.data(), "PSCZ", 4) == 0) {
+            uint64_t n = 0;
+            std::memcpy(&n, buf.data() + 4, 8);
+            if (n < 4 || n > (1ull << 32)) return false;
+            std::vector<char> out(n);
+            uLongf len = (uLongf)n;
+            if (uncompress((Bytef *)out.data(), &len, (const Bytef *)buf.data() + 12, (uLong)(buf.size() - 12)) != Z_OK ||
+                len != n)
+                return false;
+            buf.swap(out);
+        } else {
+            used = path.substr(0, path.size() - 1);   // <key>.co: an uncompressed entry
+            if (!read_all(used, buf)) return false;
+        }
     }
     if (buf.size() < 4 || std::memcmp(buf.data(), "\x7f" "ELF", 4) != 0) return false;
     code.swap(buf);
@@ -793,19 +835,33 @@ bool cache_load(const std::string &path, std::vector<char> &code)
 void cache_store(const std::string &path, const std::vector<char> &obj)
 {
     if (path.empty()) return;
-    uLongf clen = compressBound((uLong)obj.size());
-    std::vector<char> code(12 + clen);
-    if (compress2((Bytef *)code.data() + 12, &clen, (const Bytef *)obj.data(), (uLong)obj.size(), 6) != Z_OK) return;
-    code.resize(12 + clen);
+    std::vector<char> code;
+    std::string dst = path;
     const uint64_t n = obj.size();
-    std::memcpy(code.data(), "PSCZ", 4);
+    if (lzma_lib().enc) {
+        // xz, preset 6, CRC64 check (LZMA_CHECK_CRC64 = 4)
+        code.resize(12 + obj.size() + obj.size() / 2 + 65536);
+        size_t pos = 0;
+        if (lzma_lib().enc(6u, 4, nullptr, (const uint8_t *)obj.data(), obj.size(), (uint8_t *)code.data() + 12, &pos,
+                           code.size() - 12) != 0)
+            return;
+        code.resize(12 + pos);
+        std::memcpy(code.data(), "PSCX", 4);
+    } else {
+        uLongf clen = compressBound((uLong)obj.size());
+        code.resize(12 + clen);
+        if (compress2((Bytef *)code.data() + 12, &clen, (const Bytef *)obj.data(), (uLong)obj.size(), 6) != Z_OK) return;
+        code.resize(12 + clen);
+        std::memcpy(code.data(), "PSCZ", 4);
+        dst = path.substr(0, path.size() - 1) + "z";
+    }
     std::memcpy(code.data() + 4, &n, 8);
-    const size_t slash = path.rfind('/');
-    (void)mkdir(path.substr(0, slash).c_str(), 0755);
+    const size_t slash = dst.rfind('/');
+    (void)mkdir(dst.substr(0, slash).c_str(), 0755);
     // unique per process and call: prewarm compiles from several threads, and two of them may
     // store the same key
     static std::atomic<unsigned> seq{0};
-    const std::string tmp = path + ".tmp." + std::to_string((long)getpid()) + "." + std::to_string(seq++);
+    const std::string tmp = dst + ".tmp." + std::to_string((long)getpid()) + "." + std::to_string(seq++);
     {
         std::ofstream f(tmp, std::ios::binary);
         if (!f) return;
@@ -815,7 +871,7 @@ void cache_store(const std::string &path, const std::vector<char> &obj)
             return;
         }
     }
-    if (std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
+    if (std::rename(tmp.c_str(), dst.c_str()) != 0) std::remove(tmp.c_str());
 }
 
 // ---- generated kernels compiled by the ROCm toolchain's clang driver ----------------------

@@ -20,20 +20,22 @@ READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 
 
 def read_code(path):
-    """the ELF code object of a cache entry: <key>.coz ("PSCZ", u64 size, zlib stream,
-    polar_sc_jit.cpp cache_store) or a plain object file"""
+    """the ELF code object of a cache entry: <key>.cox ("PSCX", u64 size, xz stream) or
+    <key>.coz ("PSCZ", u64 size, zlib stream) -- polar_sc_jit.cpp cache_store -- or a plain
+    object file"""
+    import lzma
     import struct
     import zlib
     data = open(path, "rb").read()
-    if data[:4] == b"PSCZ":
+    if data[:4] in (b"PSCX", b"PSCZ"):
         n, = struct.unpack_from("<Q", data, 4)
-        data = zlib.decompress(data[12:])
+        data = lzma.decompress(data[12:]) if data[:4] == b"PSCX" else zlib.decompress(data[12:])
         assert len(data) == n, path
     return data
 
 
 def cache_entries(d):
-    return glob.glob(os.path.join(d, "*.coz")) + glob.glob(os.path.join(d, "*.co"))
+    return sum((glob.glob(os.path.join(d, "*." + e)) for e in ("cox", "coz", "co")), [])
 
 
 def kernels(path):
