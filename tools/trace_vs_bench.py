@@ -39,7 +39,7 @@ def main():
     args = ap.parse_args()
     lines = ["config | kernel | trace calls | all-dispatch avg (us) | timed-loop avg (us) | bench kernel_ms (us) | "
              "timed avg / bench | frac (bench) | frac (trace, timed loop)"]
-    for name in ("c2", "c3", "c5", "c5b64"):
+    for name in ("c2", "c3", "c5", "c5b64", "c4share"):
         jpath = os.path.join(args.dir, "bench_%s.json" % name)
         if not os.path.exists(jpath):
             continue
