@@ -377,3 +377,22 @@ def prewarm_all(verbose=False):
     _build.prewarm_items(ca2_items(), verbose=verbose)
     _build.prewarm_items(q9_items(), verbose=verbose)
     _build.prewarm_items(par48_gpu_items(), verbose=verbose)
+    _build.prewarm_items(high_rate_items(), verbose=verbose)
+
+
+# ---- high-rate codes across the formats (tests/test_gpu_formats.py
+# test_high_rate_codes_formats): the rate-0.9 codes of script_tests.sh:7-9 and the N = 1024
+# K = 922 code of script_RTL_sim.sh:87-97 (PAR 4..64 at QUANT 8; N = 1024 on the pair kernel
+# since round 6), at LLR_BITS 6 and 8, SIGMAG and CA2 ------------------------------------------
+HIGH_RATE_MASKS = ("frozen_n_1024_k_922", "frozen_n_2048_k_1844", "frozen_n_4096_k_3686")
+HIGH_RATE_FORMATS = [(p, s, e, q) for q in (6, 8) for p, s, e in
+                     ((64, 1, 1), (32, 1, 1), (16, 1, 1), (8, 1, 1), (4, 1, 1), (64, 0, 0), (16, 0, 1), (4, 0, 1))]
+
+
+def high_rate_items():
+    out = []
+    for n in HIGH_RATE_MASKS:
+        for p, s, e, q in HIGH_RATE_FORMATS:
+            out.append(("%s_p%d_%s_e%d_q%d" % (n, p, "sm" if s else "ca2", e, q), mask(n),
+                        {"par": p, "sigmag": s, "extended": e, "llr_bits": q}, None))
+    return out

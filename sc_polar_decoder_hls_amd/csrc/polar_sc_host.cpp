@@ -900,7 +900,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // groups, tools/pair_ab.py: C3 1.64 -> 1.16 ms, C5 4.18 -> 1.78, C5 at 64 frames 3.57 ->
     // 1.55, N = 16384 x 4096 frames 0.39 -> 0.24, N = 4096 x 16384 0.36 -> 0.23);
     // polar_sc_tuning.kernel = 2 keeps the hybrid kernel
-    const bool want_pair = !p->jit && jit_on && pair_fmt && p->G >= 128 && (t.kernel == 3 || t.kernel == 0);
+    const bool want_pair = !p->jit && jit_on && pair_fmt && p->G >= 64 && (t.kernel == 3 || t.kernel == 0);
     // an explicit kernel / subtree size that cannot be honoured is an error, not a silent
     // fallback to another kernel (A/B measurements force them)
     if ((t.kernel == 3 && !want_pair) ||

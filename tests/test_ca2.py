@@ -53,7 +53,7 @@ def test_ca2_plans_take_the_pair_kernel(pkg):
                     want = 1 if (q == 9 and par == 64) else 3   # (9-bit PAR 64: no accumulator headroom)
                     assert (d.stats["kernel"] == 3) == (want == 3), (par, q, ext, pl, d.stats["kernel"])
     # PRUNING_LEVEL 1: the leaf decoders (REP / SPC / REP2 / SPC2 / R1) on the pair kernel, at
-    # PAR 32 / 64 those of the whole PAR word (OP_PLEAF, pleaf_pair); N <= 1024 on the interpreter
+    # PAR 32 / 64 those of the whole PAR word (OP_PLEAF, pleaf_pair)
     d1 = pkg.Decoder(m, config=cfg(pkg, pruning_level=1, elag_r1=1, elag_rep=1, elag_spc=1, elag_rep2=1, elag_spc2=1))
     assert d1.stats["kernel"] == 3
     kinds = {(o["fb"] >> 16) & 7 for o in d1.schedule() if o["op"] in ("FLEAF", "GLEAF")}
@@ -62,7 +62,9 @@ def test_ca2_plans_take_the_pair_kernel(pkg):
         dp = pkg.Decoder(m, config=cfg(pkg, par=par, pruning_level=1, elag_r1=1, elag_rep=1, elag_spc=1, elag_rep2=1,
                                        elag_spc2=1))
         assert dp.stats["kernel"] == 3 and "pleaf_pair<5>" in dp.kernel_source(), par
-    assert pkg.Decoder(util.mask("FB_N1024_K512"), config=cfg(pkg)).stats["kernel"] != 3
+    # (N = 1024: the pair kernel too since round 6; below it the interpreter)
+    assert pkg.Decoder(util.mask("FB_N1024_K512"), config=cfg(pkg)).stats["kernel"] == 3
+    assert pkg.Decoder(util.mask("FB_N512_K256"), config=cfg(pkg)).stats["kernel"] != 3
     src = pkg.Decoder(m, config=cfg(pkg)).kernel_source()
     assert "#define POLAR_CA2 1" in src and "polar_psub_0_L(" in src and "leaf_gen_ca2<" in src
     assert "POLAR_CA2" not in pkg.Decoder(m).kernel_source()

@@ -97,11 +97,11 @@ def test_hybrid_source_compiles(pkg, sub_words):
 def test_llr_bits_kernels_compile(pkg, q):
     """LLR_BITS 5..8 plans are specialised through POLAR_Q in the hipRTC kernels: the per-mask
     kernel (N <= 1024) and the pair kernel (N >= 2048), PRUNING_LEVEL 1 leaf decoders included,
-    and, for plans that would use the hipcc interpreter (PAR 64 PRUNING_LEVEL 1: PAR-word leaf
-    decoders), the interpreter compiled by hipRTC."""
+    the pair kernel for the other formats from N = 1024 (PAR 64 PRUNING_LEVEL 1: PAR-word leaf
+    decoders, round 6), and below that the interpreter compiled by hipRTC."""
     for name, pr, par, kernel in (("FB_N1024_K512", 2, 16, 1), ("frozen_n_4096_k_2048", 2, 16, 3),
                                   ("FB_N1024_K512", 1, 16, 1), ("frozen_n_4096_k_2048", 1, 16, 3),
-                                  ("FB_N1024_K512", 1, 64, 2)):
+                                  ("FB_N1024_K512", 1, 64, 3), ("FB_N512_K256", 1, 64, 2)):
         c = pkg.default_config()
         c.llr_bits, c.pruning_level, c.par = q, pr, par
         dec = pkg.Decoder(util.mask(name), config=c)

@@ -71,6 +71,8 @@ TABLES = [
     ("FB_N8_K4", "tab", "Frozen_Bit_Tab/FB_N8_K4.txt", 8, 4),
     ("frozen_n_1024_k_512", "mask", "Generated_Frozen_Bit/frozen_n_1024_k_512.txt", 1024, 512),
     ("frozen_n_1024_k_768", "mask", "Generated_Frozen_Bit/frozen_n_1024_k_768.txt", 1024, 768),
+    # (the N = 1024 code of script_RTL_sim.sh:87-97's PAR 4..64 loop)
+    ("frozen_n_1024_k_922", "mask", "Generated_Frozen_Bit/frozen_n_1024_k_922.txt", 1024, 922),
     ("frozen_n_2048_k_1024", "mask", "Generated_Frozen_Bit/frozen_n_2048_k_1024.txt", 2048, 1024),
     ("frozen_n_4096_k_2048", "mask", "Generated_Frozen_Bit/frozen_n_4096_k_2048.txt", 4096, 2048),
     ("frozen_n_8192_k_4096", "mask", "Generated_Frozen_Bit/frozen_n_8192_k_4096.txt", 8192, 4096),
