@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--formats", default="",
                     help="only these formats: 'par,sigmag,extended,llr_bits;...' (the shipped one is always first)")
     ap.add_argument("--pl1-only", action="store_true", help="only the PRUNING_LEVEL 1 entries (and the shipped one)")
+    ap.add_argument("--kernel", type=int, default=0, help="polar_sc_tuning.kernel for the non-shipped formats "
+                    "(1: the schedule interpreter, for before / after comparisons)")
     args = ap.parse_args()
     import torch
     import sc_polar_decoder_hls_amd as pkg
@@ -57,7 +59,7 @@ def main():
         cfg = pkg.default_config()
         for k, v in fmt.items():
             setattr(cfg, k, v)
-        dec = pkg.Decoder(mask, cfg)
+        dec = pkg.Decoder(mask, cfg, tuning={"kernel": args.kernel} if args.kernel and fmt is not fmts[0] else None)
         # LLR_BITS 9 takes the int16 channel (polar_sc_decode_i16)
         llr = llr8.to(torch.int16) if fmt["llr_bits"] > 8 else llr8
         dec.prepare(args.frames)
