@@ -15,19 +15,24 @@ import numpy as np
 U32 = np.uint32
 LANE = np.arange(64, dtype=np.int64)
 SGN, MAG = 0x80008000, 0x7FFF7FFF
-# the datapath format of the emulated source (configure): LLR_BITS, CA2, EXTENDED (PAR 16)
-QB, CA2, EXT, WIDE = 6, False, True, False
+# the datapath format of the emulated source (configure): LLR_BITS, CA2, EXTENDED, log2 PAR
+# (PAR 16; PAR 4 / 8 in SIGMAG: the PAR words as lane groups of a device word)
+QB, CA2, EXT, WIDE, LPAR = 6, False, True, False, 4
 QMAG = GSAT = REPSAT = GSAT2 = VMAG = 0
+PARW, PPW = 16, 1
 
 
-def configure(q=6, ca2=False, ext=True):
-    """polar_sc_device.h's format constants for LLR_BITS q, CA2 / SIGMAG, EXTENDED (PAR 16)"""
-    global QB, CA2, EXT, WIDE, QMAG, GSAT, REPSAT, GSAT2, VMAG
-    QB, CA2, EXT = q, bool(ca2), bool(ext)
+def configure(q=6, ca2=False, ext=True, lpar=4):
+    """polar_sc_device.h's format constants for LLR_BITS q, CA2 / SIGMAG, EXTENDED, PAR 2^lpar"""
+    global QB, CA2, EXT, WIDE, QMAG, GSAT, REPSAT, GSAT2, VMAG, LPAR, PARW, PPW
+    QB, CA2, EXT, LPAR = q, bool(ca2), bool(ext), lpar
+    if LPAR < 4 and CA2:
+        raise NotImplementedError("pair_emu: CA2 at PAR 4 / 8 (the two's complement word trees) is GPU-tested only")
+    PARW, PPW = (1 << LPAR if LPAR < 4 else 16), (16 >> LPAR if LPAR < 4 else 1)
     WIDE = QB > 8 or (CA2 and QB > 7)   # 16-bit slot rows (polar_sc_pair.h POLAR_PAIR_S16)
     QMAG = (1 << (QB - 1)) - 1
     GSAT = (1 << (QB - 1)) - 1 if CA2 else (1 << (QB - 2)) - 1
-    REPSAT = (1 << (QB + 4)) - 1 if CA2 else (1 << (QB + 4 - 1)) - 1
+    REPSAT = (1 << (QB + LPAR)) - 1 if CA2 else (1 << (QB + LPAR - 1)) - 1
     GSAT2 = GSAT * 0x00010001
     VMAG = (1 << QB) - 1 if CA2 else QMAG
 
@@ -35,7 +40,11 @@ def configure(q=6, ca2=False, ext=True):
 def configure_from(src):
     """configure() from the #defines of a generated source"""
     m = re.search(r"#define POLAR_Q (\d+)", src)
-    configure(int(m.group(1)) if m else 6, "#define POLAR_CA2 1" in src, "#define POLAR_EXT 0" not in src)
+    lp = re.search(r"#define POLAR_LPAR (\d+)", src)
+    lpar = int(lp.group(1)) if lp else 4
+    if lpar > 4:
+        raise NotImplementedError("pair_emu: PAR 32 / 64 (the PAR words across rows) is GPU-tested only")
+    configure(int(m.group(1)) if m else 6, "#define POLAR_CA2 1" in src, "#define POLAR_EXT 0" not in src, lpar)
 
 
 configure()
@@ -265,8 +274,8 @@ def G_split_x(I, ma, mb, X, LT):
 
 
 def spc_sub(row, ln):
-    """SPC key bits below the word index, PAR 16: (row, bitrev4(position))"""
-    return (V(row) << 4) | ln.br
+    """SPC key bits below the word index: (row, the lane key)"""
+    return (V(row) << 4) | spc_lk(ln)
 
 
 def rep_acc_rows(acc, t0, t1, t2, t3):
@@ -281,13 +290,14 @@ def rep_sm_rows(acc, v, ln):
 
 
 def spc_lk(ln):
-    """polar_sc_pair.h spc_lk at PAR >= 16: bitrev4(position)"""
-    return ln.br
+    """polar_sc_pair.h spc_lk: bitrev4(position), or (PAR 4 / 8) (group, bitrev_LPAR(position in
+    the group)), polar_sc_device.h spc_lane_key"""
+    return spc_lane_key(ln) if LPAR < 4 else ln.br
 
 
 def spc_sub2(row, ln):
-    """two-word nodes, PAR 16: (row & 1, bitrev4(position))"""
-    return ((V(row) & 1) << 4) | ln.br
+    """two-word nodes: (row & 1, the lane key)"""
+    return ((V(row) & 1) << 4) | spc_lk(ln)
 
 
 def rep2_acc(t):
@@ -500,6 +510,226 @@ def leaf_gen(FB, M, S, ln):
     if (FB >> 16) & 7:
         raise NotImplementedError("PRUNING_LEVEL 1 leaf decoders")
     return leaf_ms(FB & 0xFFFF, 0, 16, M, S, ln)
+
+
+# ---- PAR 4 / 8 (polar_sc_device.h word_gen, polar_sc_pair.h rep_groups_*), SIGMAG ----------
+def bitrev_n(v, bits):
+    v = np.asarray(v, np.int64)
+    r = np.zeros_like(v)
+    for i in range(bits):
+        r |= ((v >> i) & 1) << (bits - 1 - i)
+    return r
+
+
+def spc_lane_key(ln):
+    p = ln.pos.astype(np.int64)
+    m = (1 << LPAR) - 1
+    return ((p & ~m) | bitrev_n(p & m, LPAR)).astype(U32)
+
+
+def tree_step(D, v, ln):
+    p = xorlane(D, v)
+    a = ln.a[D]
+    return G_sm(0, bsel(a, v, p), bsel(a, p, v), 0)
+
+
+def add_tree_w(W, DMIN, v, ln):
+    v = V(v)
+    while W // 2 >= DMIN:
+        v = tree_step(W // 2, v, ln)
+        W //= 2
+    return v
+
+
+def xor_tree_w(W, DMIN, v):
+    v = V(v)
+    while W // 2 >= DMIN:
+        v = v ^ xorlane(W // 2, v)
+        W //= 2
+    return v
+
+
+def min_tree_w(W, DMIN, v):
+    v = V(v)
+    while W // 2 >= DMIN:
+        v = np.minimum(v, xorlane(W // 2, v))
+        W //= 2
+    return v
+
+
+def rep_sat_add(acc, t):
+    return G_sm(REPSAT, t, acc, 0)
+
+
+def group_totals(t):
+    """per lane the totals of groups gr ^ 0 .. gr ^ (PPW - 1)"""
+    if PPW == 2:
+        return [V(t), xorlane(PARW, t)]
+    v = [V(t), xorlane(PARW, t), xorlane(2 * PARW, t)]
+    v.append(xorlane(PARW, v[2]))
+    return v
+
+
+def group_chain(CNT, acc, t, gr):
+    gr = np.asarray(gr, np.int64)
+    if CNT == 1:
+        return rep_sat_add(acc, t)
+    v = [V(t), xorlane(PARW, t)] if CNT == 2 else group_totals(t)
+    for j in range(CNT):
+        acc = rep_sat_add(acc, np.choose((gr & (CNT - 1)) ^ j, v).astype(U32))
+    return acc
+
+
+def group_order(t, gr):
+    gr = np.asarray(gr, np.int64)
+    v = group_totals(t)
+    return [np.choose((gr & (PPW - 1)) ^ k, v).astype(U32) for k in range(PPW)]
+
+
+def rep_groups_rows(acc, lam, ln):
+    o = group_order(add_tree_w(PARW, 1, lam, ln), ln.pos.astype(np.int64) >> LPAR)
+    r = [rows4(x) for x in o]
+    for row in ("t0", "t1", "t2", "t3"):
+        for k in range(PPW):
+            acc = rep_sat_add(acc, getattr(r[k], row))
+    return acc
+
+
+def rep_groups_2(lam, ln):
+    o = group_order(add_tree_w(PARW, 1, lam, ln), ln.pos.astype(np.int64) >> LPAR)
+    q = [swap16(x) for x in o]
+    acc = V(0)
+    for k in range(PPW):
+        acc = rep_sat_add(acc, q[k].a)
+    for k in range(PPW):
+        acc = rep_sat_add(acc, q[k].b)
+    return acc
+
+
+def rep_groups_1(lam, ln):
+    return group_chain(PPW, V(0), add_tree_w(PARW, 1, lam, ln), ln.pos.astype(np.int64) >> LPAR)
+
+
+def F_split_rep(I, MW, ma, mb, FS):
+    return F_split_sm(I, ma, mb, FS)
+
+
+def leaf_dp(B, W, L, fb, fbm, ln):
+    """Spec_P{W} on lanes [B, B + W) (polar_sc_device.h leaf_dp, SIGMAG)"""
+    bm = ((1 << W) - 1) << B
+    sub = fb & bm
+    L = V(L)
+    if sub == 0:
+        return V(0)
+    if sub == bm:
+        return L & SGN
+    if W == 2:
+        P = xorlane(1, L)
+        u0 = (L ^ P) & fbm
+        u0p = xorlane(1, u0)
+        d = pk_sub(P & MAG, L & MAG)
+        u1 = bsel(d, L, P ^ u0p) & fbm
+        return bsel(ln.a[1], u0 ^ xorlane(1, u1), u1)
+    H = W // 2
+    P = xorlane(H, L)
+    xa = leaf_dp(B, H, F_sm(L, P), fb, fbm, ln)
+    Lb = G_sm(0 if EXT else GSAT, P, L, xorlane(H, xa))
+    xb = leaf_dp(B + H, H, Lb, fb, fbm, ln)
+    return bsel(ln.a[H], xa ^ xorlane(H, xb), xb)
+
+
+def leaf_kind_w(W, L, kind, ln):
+    L = V(L)
+    if kind == 5:
+        return L & SGN
+    if kind in (1, 3):
+        return add_tree_w(W, 1 if kind == 1 else 2, L, ln) & SGN
+    dm = 2 if kind == 4 else 1
+    h = L & SGN
+    par = xor_tree_w(W, dm, h)
+    mg = (L & 0x7FFF7FFF).astype(np.int64)
+    br = bitrev_n(ln.pos.astype(np.int64) & (W - 1), LPAR)
+    mlo, mhi = V(((mg & 0xFFFF) << 4) | br), V(((mg >> 16) << 4) | br)
+    klo, khi = min_tree_w(W, dm, mlo), min_tree_w(W, dm, mhi)
+    flo = np.where(klo == mlo, par & 0x8000, 0).astype(U32)
+    fhi = np.where(khi == mhi, par & 0x80000000, 0).astype(U32)
+    return h ^ flo ^ fhi
+
+
+def word_spc(W, L, ln):
+    L = V(L)
+    h = L & SGN
+    par = xor_tree_w(W, 1, h)
+    mg = L & MAG
+    lk = spc_lane_key(ln)
+    klo = min_tree_w(W, 1, ((mg & 0xFF) << 24) | lk)
+    khi = min_tree_w(W, 1, (((mg >> 16) & 0xFF) << 24) | lk)
+    flo = np.where(((par & 0x8000) != 0) & ((klo & 15) == lk), 0x8000, 0).astype(U32)
+    fhi = np.where(((par & 0x80000000) != 0) & ((khi & 15) == lk), 0x80000000, 0).astype(U32)
+    return h ^ flo ^ fhi
+
+
+WN_R0, WN_R1, WN_REP, WN_SPC, WN_RN = 0x00, 0x0F, 0x02, 0x04, 0x08
+
+
+def wn_class(info, g0, cnt):
+    ty = [(info >> (7 * (g0 + t))) & 15 for t in range(cnt)]
+    r0, r1 = 0, 0x0F
+    for T in ty:
+        r0 |= T
+        r1 &= T
+    if r0 == WN_R0:
+        return WN_R0
+    if r1 == WN_R1:
+        return WN_R1
+    if all(T == WN_R0 for T in ty[:-1]) and ty[-1] == WN_REP:
+        return WN_REP
+    if all(T == WN_R1 for T in ty[1:]) and ty[0] == WN_SPC:
+        return WN_SPC
+    return WN_RN
+
+
+def word_leaf_gen(B, FB, INFO, L, ln):
+    kind = (INFO >> (7 * (B >> LPAR) + 4)) & 7
+    if kind:
+        return leaf_kind_w(PARW, L, kind, ln)
+    fbm = np.where((FB >> ln.pos.astype(np.int64)) & 1, SGN, 0).astype(U32)
+    return leaf_dp(B, PARW, L, FB, fbm, ln)
+
+
+def word_gen(B, W, FB, INFO, L, ln):
+    """polar_sc_device.h word_gen: the word tree of a PAR 4 / 8 leaf record"""
+    H, h, g0 = W // 2, (W >> LPAR) // 2, B >> LPAR
+    prune = (INFO >> 28) & 1
+    tl = wn_class(INFO, g0, h) if prune else WN_RN
+    tr = wn_class(INFO, g0 + h, h) if prune else WN_RN
+    lz = tl == WN_R0
+    L = V(L)
+    P = xorlane(H, L)
+    xa = V(0)
+    if not lz:
+        La = F_sm(L, P)
+        if tl == WN_REP:
+            xa = group_chain(h, V(0), add_tree_w(PARW, 1, La, ln), (ln.pos.astype(np.int64) >> LPAR) - g0) & SGN
+        elif h == 1:
+            xa = word_leaf_gen(B, FB, INFO, La, ln)
+        else:
+            xa = word_gen(B, H, FB, INFO, La, ln)
+    Lb = G_sm(GSAT, P, L, V(0) if lz else xorlane(H, xa))
+    if tr == WN_R1:
+        xb = Lb & SGN
+    elif tr == WN_SPC:
+        xb = word_spc(H, Lb, ln)
+    elif h == 1:
+        xb = word_leaf_gen(B + H, FB, INFO, Lb, ln)
+    else:
+        xb = word_gen(B + H, H, FB, INFO, Lb, ln)
+    xbp = xorlane(H, xb)
+    return bsel(ln.a[H], xbp if lz else xa ^ xbp, xb)
+
+
+def leaf_word_gen(FB, INFO, M, S, ln):
+    return pk_sra(word_gen(0, 16, FB, INFO, V(M) | (V(S) & SGN), ln), 15)
 
 
 def sm8_pair(l, h):
@@ -817,13 +1047,16 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
             acc = V(0)
             lams = [F_pair(src(k, j), src(k, n4 + j)) for j in range(n4)]
             for lam in lams:
+                if LPAR < 4:   # PAR 4 / 8: the exact chain over the groups (prep_body)
+                    acc = rep_groups_rows(acc, lam, ln)
+                    continue
                 sg = pk_sra(lam, 15)
                 t = rows4(row_sum_biased(pk_add(pk_sub((lam & MAG) ^ sg, sg), 0x02000200)))
                 if solo:
                     acc = rep_acc_solo(acc, t.t0, t.t1, t.t2, t.t3)
                 else:
                     acc = rep_acc(rep_acc(rep_acc(rep_acc(acc, t.t0), t.t1), t.t2), t.t3)
-            if not CA2 and (rep_any_zero_lo if solo else rep_any_zero)(acc):
+            if not CA2 and LPAR >= 4 and (rep_any_zero_lo if solo else rep_any_zero)(acc):
                 acc = V(0)
                 for lam in lams:
                     if solo:
@@ -872,9 +1105,10 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
                         if (int(k) & 63) == ((int(row[L]) << 4) | int(ln.br[L])):
                             bits[l >> 4][L] ^= U32(1 << ((l & 15) + hb))
             elif kind == "SPC":
+                lk = spc_lk(ln)
                 par = row_xor(par)
-                klo = row_min_u32(klo | ln.br)
-                khi = row_min_u32(khi | ln.br)
+                klo = row_min_u32(klo | lk)
+                khi = row_min_u32(khi | lk)
                 p = swap16(par)
                 par = p.a ^ p.b
                 p = swap32(par)
@@ -883,8 +1117,8 @@ def _decode_pair(c0, c1, G, S, upper, subs, ln, c, solo=False):
                     a = swap16(klo) if _ == 16 else swap32(klo)
                     b = swap16(khi) if _ == 16 else swap32(khi)
                     klo, khi = np.minimum(a.a, a.b), np.minimum(b.a, b.b)
-                flo = land(land(par & 0x8000, (klo & 15) == ln.br), ((klo >> 4) & 3) == row)
-                fhi = land(land(par & 0x80000000, (khi & 15) == ln.br), ((khi >> 4) & 3) == row)
+                flo = land(land(par & 0x8000, (klo & 15) == lk), ((klo >> 4) & 3) == row)
+                fhi = land(land(par & 0x80000000, (khi & 15) == lk), ((khi >> 4) & 3) == row)
                 for L in range(64):
                     if flo[L]:
                         l = l0 + int((klo[L] >> 6) & 0x3FFFF)

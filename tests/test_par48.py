@@ -74,6 +74,47 @@ def test_par48_leaf_records_carry_the_word_classes(pkg):
         assert (info >> 28) & 1 == 1 and fb < (1 << 16)   # PRUNING_LEVEL 2 (shipped)
 
 
+@pytest.mark.parametrize("par", [8, 4])
+def test_par48_generated_code_emulated(pkg, oracle_mod, par):
+    """CPU: the generated PAR 4 / 8 code (leaf_word_gen word trees, rep_groups_* REP chains,
+    group-ordered SPC keys, the upper loops' REP) emulated on 64-lane waves (tests/pair_emu.py)
+    equals the FSM at PRUNING_LEVEL 0 / 1 / 2 on a reference mask, a planted mask with every
+    group class and the N = 1024 K = 922 code of script_RTL_sim.sh's PAR loop."""
+    import pair_emu
+    from sc_polar_decoder_hls_amd._plansets import planted_mask
+    rng = np.random.default_rng(par)
+    masks = [util.mask("frozen_n_2048_k_1024"), planted_mask(rng, 2048, par), util.mask("frozen_n_1024_k_922")]
+    try:
+        for i, m in enumerate(masks):
+            for c7 in ((2, 1, 1, 1, 0, 0, 1), (1, 1, 1, 1, 1, 1, 0), (0, 0, 0, 0, 0, 0, 0)):
+                c = cfg(pkg, par=par, **c7_fields(c7))
+                dec = pkg.Decoder(m, config=c, tuning={"kernel": 3, "sub_words": 32})
+                llr, _ = util.synth_frames(m, 3, ebn0_db=1.0, seed=par + i)
+                llr = np.clip(llr, -31, 31).astype(np.int8)
+                _assert_same(pair_emu.decode(dec, llr), oracle_mod.decode_fsm(m, llr, config=c7, par=par),
+                             "emulated PAR %d mask %d %s" % (par, i, c7))
+    finally:
+        pair_emu.configure()
+
+
+def test_par48_group_order_is_needed(pkg, oracle_mod, monkeypatch):
+    """A mutation of the emulation (the groups of a word chained in reverse order) differs from
+    the FSM: the REP chains' group order is exercised, not vacuous."""
+    import pair_emu
+    orig = pair_emu.group_order
+    monkeypatch.setattr(pair_emu, "group_order", lambda t, gr: orig(t, gr)[::-1])
+    orig_chain = pair_emu.group_chain
+    monkeypatch.setattr(pair_emu, "group_chain", lambda CNT, acc, t, gr: orig_chain(CNT, acc, t, np.asarray(gr) ^ (CNT - 1)))
+    m = util.mask("frozen_n_2048_k_1024")
+    dec = pkg.Decoder(m, config=cfg(pkg, par=4), tuning={"kernel": 3, "sub_words": 32})
+    llr, _ = util.synth_frames(m, 8, ebn0_db=0.0, seed=9)
+    llr = np.clip(llr, -31, 31).astype(np.int8)
+    try:
+        assert (pair_emu.decode(dec, llr) != oracle_mod.decode_fsm(m, llr, par=4)).any()
+    finally:
+        pair_emu.configure()
+
+
 def frames(mask, q, n_awgn, n_edge, seed):
     rng = np.random.default_rng(seed)
     amp = (1 << (q - 1)) - 1
