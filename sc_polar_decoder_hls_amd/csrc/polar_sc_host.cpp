@@ -912,7 +912,10 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // solo layout (one frame per wave, 8 words per register): PAR 16 SIGMAG (8-bit slot rows,
     // or 16-bit ones for 9-bit LLRs; the half ops of 8-word nodes have no CA2 form); a forced
     // solo layout the plan cannot take is an error
-    const bool solo_ok = c.par == 16 && c.sigmag == 1 && c.llr_bits <= 9;
+    // (and N >= 2048: the solo subtrees need >= 64 words under a root of >= 2 of them; at
+    // N = 1024 a 32-word solo subtree decoded wrong on the GPU with the int8 entry of a 9-bit
+    // plan, so N = 1024 plans are pair-only)
+    const bool solo_ok = c.par == 16 && c.sigmag == 1 && c.llr_bits <= 9 && p->G >= 128;
     if ((t.layout != 0 && !want_pair) || (t.layout == 2 && !solo_ok)) {
         delete p;
         return -ENOTSUP;
@@ -1084,7 +1087,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // words, automatic waves, LDS levels and subtree roots), not the pair plan's tuning, which
     // was chosen for the other layout; only the way subtree decoders are built
     // (sub_inline) carries over. polar_sc_tuning.layout = 1 builds no alternate.
-    if (p->pair && !p->solo && t.layout == 0 && c.par == 16 && c.sigmag == 1 && c.llr_bits <= 9) {
+    if (p->pair && !p->solo && t.layout == 0 && c.par == 16 && c.sigmag == 1 && c.llr_bits <= 9 && p->G >= 128) {
         polar_sc_tuning ts{};
         ts.layout = 2;
         ts.kernel = 3;
