@@ -74,7 +74,7 @@ def test_ca2_plans_take_the_pair_kernel(pkg):
     assert s8["scratch_bytes_per_wave"] > s7["scratch_bytes_per_wave"]
 
 
-@pytest.mark.parametrize("N", [2048, 8192])
+@pytest.mark.parametrize("N", [1024, 2048, 8192])
 def test_ca2_generated_code_emulated(pkg, oracle_mod, N):
     """CPU: the CA2 subtree decoders and upper levels emulated on 64-lane waves equal the FSM
     (structured masks, the first word informative so that leaf 0 meets MIN, edge LLRs)."""
