@@ -184,8 +184,6 @@ def ca2_gpu_items():
     fm = ca2_first_mask(16384)
     for par in (16, 32, 64):
         for q in (5, 6, 7, 8, 9):
-            if q == 9 and par == 64:
-                continue
             for ext in (1, 0):
                 out.append(("first16384_p%d_q%d_e%d" % (par, q, ext), fm, {"par": par, "llr_bits": q, "extended": ext}, None))
     out.append(("first16384_pl0", fm, {"pruning_level": 0}, None))
@@ -386,7 +384,8 @@ def prewarm_all(verbose=False):
 # since round 6), at LLR_BITS 6 and 8, SIGMAG and CA2 ------------------------------------------
 HIGH_RATE_MASKS = ("frozen_n_1024_k_922", "frozen_n_2048_k_1844", "frozen_n_4096_k_3686")
 HIGH_RATE_FORMATS = [(p, s, e, q) for q in (6, 8) for p, s, e in
-                     ((64, 1, 1), (32, 1, 1), (16, 1, 1), (8, 1, 1), (4, 1, 1), (64, 0, 0), (16, 0, 1), (4, 0, 1))]
+                     ((64, 1, 1), (32, 1, 1), (16, 1, 1), (8, 1, 1), (4, 1, 1), (64, 0, 0), (16, 0, 1), (4, 0, 1))] + \
+    [(64, 0, 1, 9), (64, 0, 0, 9)]   # (CA2 at LLR_BITS 9, PAR 64: the saturating REP accumulate)
 
 
 def high_rate_items():

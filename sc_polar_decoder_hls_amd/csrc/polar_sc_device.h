@@ -698,6 +698,15 @@ __device__ __forceinline__ u32 row_sum_biased(u32 v)
 // acc = clamp(acc + T, -511, 511) with T = row total - 16 * 512 (two's complement halves)
 __device__ __forceinline__ u32 rep_acc(u32 acc, u32 total_biased)
 {
+    if constexpr (CA2 && REPSAT >= 0x4000u) {
+        // CA2 with LLR_BITS 9 at PAR 64: |acc| <= 2^15 - 1 plus a PAR word's total overflows
+        // the 16-bit half; the saturating packed add (v_pk_add_i16 clamp) then the symmetric
+        // bound is the clamp of the exact sum (qadd, functions.h:63-75)
+        const i16x2 t = __builtin_bit_cast(i16x2, pk_sub(total_biased, 0x20002000u));
+        i16x2 v = __builtin_elementwise_add_sat(__builtin_bit_cast(i16x2, acc), t);
+        v = __builtin_elementwise_max(v, (i16x2){(short)-(int)REPSAT, (short)-(int)REPSAT});
+        return __builtin_bit_cast(u32, v);
+    }
     u32 t = pk_sub(pk_add(acc, total_biased), 0x20002000u);
     i16x2 v = __builtin_bit_cast(i16x2, t);
     v = __builtin_elementwise_min(v, (i16x2){(short)REPSAT, (short)REPSAT});

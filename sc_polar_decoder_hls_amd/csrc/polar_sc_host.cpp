@@ -867,9 +867,8 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // EXTENDED, the saturating G and POLAR_EXT 0 leaves when not)
     // and 9-bit LLRs (16-bit stage slots, the int16 channel: polar_sc_pair.h SLOT16)
     // and CA2 (polar_sc_pair.h POLAR_CA2: the split code on magnitude + sign, MIN absorbing on
-    // the leftmost path) with plain leaves (PRUNING_LEVEL 0 / 2; the PRUNING_LEVEL 1 decoders of
-    // CA2 stay on the interpreter), except 9-bit LLRs at PAR 64, whose 16-bit REP accumulator
-    // (2^15 - 1) leaves no headroom in a 16-bit half
+    // the leftmost path; 9-bit LLRs at PAR 64, whose REP accumulator bound 2^15 - 1 fills a
+    // 16-bit half, accumulate with the saturating packed add, polar_sc_device.h rep_acc)
     // and PAR 4 / 8 SIGMAG (the PAR words = lane groups of a device word: every one-word leaf
     // record decodes its whole word tree with the frozen bits and group classes as template
     // constants, polar_sc_device.h word_gen; REP over the groups, polar_sc_pair.h rep_groups_*)
@@ -883,8 +882,7 @@ int polar_sc_plan_create_tuned(polar_sc_plan **out, uint32_t N, const uint8_t *i
     // carry no kind bits)
     const bool par48 = c.par == 4 || c.par == 8;
     const bool pair_fmt = dflt || ((pair_par || par48) && c.sigmag == 1 && c.llr_bits <= 9) ||
-                          ((pair_par || par48) && c.sigmag == 0 && c.llr_bits <= 9 &&
-                           !(c.llr_bits == 9 && c.par == 64));
+                          ((pair_par || par48) && c.sigmag == 0 && c.llr_bits <= 9);
     p->jit = (polar_host::jit_supported(N) && jit_on && !kinds && dflt) ? 1 : 0;
     // generated subtrees of 64 words (1024 LLRs), 128 (2048 LLRs) from N = 32768: the 2048-LLR
     // level's F / G / H then run inside the straight-line code instead of as interpreter ops

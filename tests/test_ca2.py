@@ -50,8 +50,7 @@ def test_ca2_plans_take_the_pair_kernel(pkg):
             for ext in (0, 1):
                 for pl in (0, 2):
                     d = pkg.Decoder(m, config=cfg(pkg, par=par, llr_bits=q, extended=ext, pruning_level=pl))
-                    want = 1 if (q == 9 and par == 64) else 3   # (9-bit PAR 64: no accumulator headroom)
-                    assert (d.stats["kernel"] == 3) == (want == 3), (par, q, ext, pl, d.stats["kernel"])
+                    assert d.stats["kernel"] == 3, (par, q, ext, pl, d.stats["kernel"])
     # PRUNING_LEVEL 1: the leaf decoders (REP / SPC / REP2 / SPC2 / R1) on the pair kernel, at
     # PAR 32 / 64 those of the whole PAR word (OP_PLEAF, pleaf_pair)
     d1 = pkg.Decoder(m, config=cfg(pkg, pruning_level=1, elag_r1=1, elag_rep=1, elag_spc=1, elag_rep2=1, elag_spc2=1))
