@@ -45,8 +45,8 @@ extern "C" {
  *   * par 4, 8, 16, 32 or 64 (script_tests.sh:11 runs 16 and 64, script_RTL_sim.sh 4..64).
  * The shipped datapath (sigmag 1, par 16, llr_bits <= 8; either extended, every pruning level
  * and elag combination) runs the generated kernels; for N >= 1024 so does every other format
- * (the pair kernel: par 4 .. 64, sigmag 0 / 1, llr_bits 5..9, every pruning level) except CA2
- * at llr_bits 9 with par 64; the rest runs the schedule interpreter compiled for it. elag_rare = 1
+ * (the pair kernel: par 4 .. 64, sigmag 0 / 1, llr_bits 5..9, every pruning level); smaller
+ * codes outside the shipped datapath run the schedule interpreter compiled for it. elag_rare = 1
  * (does not compile in the reference, my_module.h:255 vs :1511) is rejected with -ENOTSUP.
  */
 typedef struct polar_sc_config {
