@@ -76,8 +76,8 @@ typedef struct polar_sc_tuning {
     int32_t kernel;           /* 0 = automatic; 1 = the schedule interpreter for every N
                                  (no per-mask / generated-subtree code); 2 = the hybrid
                                  kernel (8-frame groups) for N > 1024; 3 = the pair kernel
-                                 (one frame pair per wave) for N >= 2048 in the generated
-                                 datapaths above. A forced kernel or sub_words the plan
+                                 (one frame pair per wave) for N >= 2048, and N = 1024
+                                 outside the shipped datapath. A forced kernel or sub_words the plan
                                  cannot use is an error (-ENOTSUP / -EINVAL), never a
                                  silent fallback */
     int32_t waves_per_group;  /* interpreter / hybrid launches: waves per 8-frame group, 0 =
@@ -197,7 +197,8 @@ typedef struct polar_sc_plan_stats {
                                          code for every mixed subtree of sub_words),
                                          3 = pair kernel (one frame pair per wave, generated
                                          subtree decoders, upper levels over stage-slot
-                                         rows; the default for N >= 2048)                */
+                                         rows; the default for N >= 2048, and for
+                                         N = 1024 outside the shipped datapath)          */
     uint32_t sub_words;               /* hybrid / pair: subtree size in 16-LLR words      */
     uint32_t n_sub_kinds;             /* hybrid / pair: distinct generated subtree decoders */
     uint32_t n_sub_calls;             /* hybrid / pair: subtree decoder calls per frame
@@ -242,7 +243,7 @@ int polar_sc_decode_u16(const polar_sc_plan *plan, const int8_t *llr_dev, uint16
 
 /* Same as polar_sc_decode with int16 channel values ([batch][N] int16, the low llr_bits of
  * each are the LLR): the channel for 9-bit LLRs beyond the int8 range (LLR_BITS 9,
- * script/parser_comp.sh:12). Pair plans of 9-bit LLRs (N >= 2048) read the int16 frames
+ * script/parser_comp.sh:12). Pair plans of 9-bit LLRs (N >= 1024) read the int16 frames
  * directly; other plans run the schedule interpreter of the plan's format. */
 int polar_sc_decode_i16(const polar_sc_plan *plan, const int16_t *llr_dev, uint64_t *hard_bits_dev,
                         size_t batch, void *stream);
